@@ -1,0 +1,622 @@
+// libdcnr C ABI: the native runtime that sequences the DCN-R forward/backward
+// kernels on one HIP stream over caller-owned memory (include/dcnr.h).
+//
+// Forward  = DCN_RecSys.forward (train.py:155-170):
+//   gather+x0+cross (1 kernel) -> initial Linear (MFMA GEMM) ->
+//   per ResBlock: L1 GEMM -> BN1 stats/finalize -> BN1+ReLU+dropout ->
+//                 L2 GEMM -> BN2 stats/finalize -> BN2 + residual + ReLU
+//   -> deep head dot -> logits
+// Backward = loss.backward() (train.py:225), reverse order, BN backward with
+// deterministic fp64 column reductions, dW by split-K MFMA GEMMs over the batch,
+// cross backward + dense embedding-grad scatter in one kernel.
+#include "dcnr_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+namespace dcnr {
+
+static thread_local char g_err[1024] = "";
+
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+namespace {
+
+#define TRY(x)                       \
+  do {                               \
+    dcnr_status st_ = (x);           \
+    if (st_ != DCNR_OK) return st_;  \
+  } while (0)
+
+constexpr int MAX_CAT = 64;
+constexpr int MAX_RES = 8;
+constexpr int MAX_CROSS = 7;
+constexpr int64_t PART_CHUNKS = 2100;  // >= rowcol chunk count (2048 target + rounding)
+
+struct Dims {
+  int K, D, Dp, H, Hp, L, R, prec, es;
+  int widths[2 + MAX_CAT];
+  int64_t rows[2 + MAX_CAT];
+  float dropout;
+};
+
+dcnr_status make_dims(const dcnr_model_desc* d, Dims* o) {
+  if (!d) { set_error("null desc"); return DCNR_BAD_ARG; }
+  if (d->n_cat < 0 || d->n_cat > MAX_CAT || (d->n_cat > 0 && !d->cat_rows)) {
+    set_error("n_cat=%d unsupported (max %d)", d->n_cat, MAX_CAT);
+    return DCNR_BAD_ARG;
+  }
+  if (d->n_res < 1 || d->n_res > MAX_RES) {
+    set_error("n_res_blocks=%d unsupported (1..%d)", d->n_res, MAX_RES);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  if (d->n_cross < 0 || d->n_cross > MAX_CROSS) {
+    set_error("n_cross_layers=%d unsupported (0..%d)", d->n_cross, MAX_CROSS);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  if (d->emb_dim < 1 || d->hidden < 1 || d->n_num < 0 || d->n_users < 1 || d->n_items < 1) {
+    set_error("bad model dims");
+    return DCNR_BAD_ARG;
+  }
+  if (d->precision != DCNR_PREC_FP32 && d->precision != DCNR_PREC_BF16) {
+    set_error("bad precision %d", d->precision);
+    return DCNR_BAD_ARG;
+  }
+  o->K = d->n_cat;
+  o->widths[0] = o->widths[1] = d->emb_dim;
+  o->rows[0] = d->n_users;
+  o->rows[1] = d->n_items;
+  int D = 2 * d->emb_dim;
+  for (int k = 0; k < d->n_cat; ++k) {
+    int64_t n = d->cat_rows[k];
+    if (n < 1) { set_error("cat table %d has %lld rows", k, (long long)n); return DCNR_BAD_ARG; }
+    int w = (int)std::sqrt((double)n) + 1;  // train.py:139 int(np.sqrt(n_cat)) + 1
+    while ((int64_t)(w - 1) * (w - 1) > n) --w;        // guard fp rounding of sqrt
+    while ((int64_t)w * w <= n) ++w;
+    o->widths[2 + k] = w;
+    o->rows[2 + k] = n;
+    D += w;
+  }
+  D += d->n_num;
+  o->D = D;
+  o->Dp = (int)rup(D, 8);
+  o->H = d->hidden;
+  o->Hp = (int)rup(d->hidden, 8);
+  o->L = d->n_cross;
+  o->R = d->n_res;
+  o->prec = d->precision;
+  o->es = d->precision == DCNR_PREC_BF16 ? 2 : 4;
+  o->dropout = d->dropout;
+  if (o->Hp > 2048 || o->D > 1024) {
+    set_error("hidden_dim=%d / input_dim=%d unsupported", o->H, o->D);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  return DCNR_OK;
+}
+
+// ------------------------------------------------------------- workspace
+struct Bump {
+  char* base; size_t off = 0;
+  explicit Bump(void* b) : base((char*)b) {}
+  void* take(size_t bytes) {
+    off = (off + 255) & ~(size_t)255;
+    void* p = base ? base + off : nullptr;
+    off += bytes;
+    return p;
+  }
+};
+
+struct BnBufs { float *scale, *shift, *mean, *invstd; };
+
+struct Layout {
+  int* err;
+  void* W0p; void* W0t; float* b0p;
+  void* W1p[MAX_RES]; void* W1t[MAX_RES]; float* b1p[MAX_RES];
+  void* W2p[MAX_RES]; void* W2t[MAX_RES]; float* b2p[MAX_RES];
+  void* x0;
+  void* h[MAX_RES + 1];
+  void* t1[MAX_RES]; void* t2[MAX_RES];
+  void* a1;
+  float* zc; float* zdeep;
+  BnBufs bn[2 * MAX_RES];
+  float* part; double* sums; float* coef;
+  // backward
+  void* G; void* dt2; void* du; void* da;
+  float* dx0; float* slab; int64_t slab_elems; float* cpart; size_t cpart_elems;
+  double* bce_part;
+  size_t total;
+};
+
+Layout make_layout(const Dims& d, int64_t B, int mode, void* ws) {
+  Layout L;
+  memset(&L, 0, sizeof(L));
+  Bump b(ws);
+  const bool train = mode == DCNR_TRAIN;
+  const size_t es = d.es;
+  const size_t act = (size_t)B * d.Hp * es;
+  L.err = (int*)b.take(256);
+  L.W0p = b.take((size_t)d.Hp * d.Dp * es);
+  L.W0t = train ? b.take((size_t)d.Dp * d.Hp * es) : nullptr;
+  L.b0p = (float*)b.take(d.Hp * 4);
+  for (int j = 0; j < d.R; ++j) {
+    L.W1p[j] = b.take((size_t)d.Hp * d.Hp * es);
+    L.W2p[j] = b.take((size_t)d.Hp * d.Hp * es);
+    L.W1t[j] = train ? b.take((size_t)d.Hp * d.Hp * es) : nullptr;
+    L.W2t[j] = train ? b.take((size_t)d.Hp * d.Hp * es) : nullptr;
+    L.b1p[j] = (float*)b.take(d.Hp * 4);
+    L.b2p[j] = (float*)b.take(d.Hp * 4);
+  }
+  L.x0 = b.take((size_t)B * d.Dp * es);
+  if (train) {
+    for (int j = 0; j <= d.R; ++j) L.h[j] = b.take(act);
+    for (int j = 0; j < d.R; ++j) { L.t1[j] = b.take(act); L.t2[j] = b.take(act); }
+  } else {
+    void* h0 = b.take(act);
+    void* h1 = b.take(act);
+    for (int j = 0; j <= d.R; ++j) L.h[j] = (j & 1) ? h1 : h0;
+    void* t = b.take(act);
+    for (int j = 0; j < d.R; ++j) L.t1[j] = L.t2[j] = t;
+  }
+  L.a1 = b.take(act);
+  L.zc = (float*)b.take(B * 4);
+  L.zdeep = (float*)b.take(B * 4);
+  for (int i = 0; i < 2 * d.R; ++i) {
+    L.bn[i].scale = (float*)b.take(d.Hp * 4);
+    L.bn[i].shift = (float*)b.take(d.Hp * 4);
+    L.bn[i].mean = (float*)b.take(d.Hp * 4);
+    L.bn[i].invstd = (float*)b.take(d.Hp * 4);
+  }
+  L.part = (float*)b.take((size_t)PART_CHUNKS * 3 * d.Hp * 4);
+  L.sums = (double*)b.take((size_t)(3 * d.Hp + 1) * 8);
+  L.coef = (float*)b.take((size_t)3 * d.Hp * 4);
+  if (train) {
+    L.G = b.take(act);
+    L.dt2 = b.take(act);
+    L.du = b.take(act);
+    L.da = b.take(act);
+    L.dx0 = (float*)b.take((size_t)B * d.Dp * 4);
+    L.slab_elems = (int64_t)64 * d.Hp * std::max(d.Hp, d.Dp);
+    L.slab = (float*)b.take((size_t)L.slab_elems * 4);
+    L.cpart_elems = cross_bwd_part_elems(d.D, d.L);
+    L.cpart = (float*)b.take(L.cpart_elems * 4);
+  }
+  L.bce_part = (double*)b.take(bce_ws_bytes());
+  L.total = b.off + 256;
+  return L;
+}
+
+// ------------------------------------------------------------- params
+struct Params {
+  const float* tab[2 + MAX_CAT];
+  const float *W0, *b0;
+  struct Blk {
+    const float *w1, *b1, *g1, *be1; float *rm1, *rv1; int64_t* nbt1;
+    const float *w2, *b2, *g2, *be2; float *rm2, *rv2; int64_t* nbt2;
+  } blk[MAX_RES];
+  const float* cb[MAX_CROSS]; const float* cw[MAX_CROSS];
+  const float *wf, *bf;
+};
+
+Params map_params(const Dims& d, void* const* p) {
+  Params P;
+  int i = 0;
+  for (int t = 0; t < 2 + d.K; ++t) P.tab[t] = (const float*)p[i++];
+  P.W0 = (const float*)p[i++];
+  P.b0 = (const float*)p[i++];
+  for (int j = 0; j < d.R; ++j) {
+    auto& B = P.blk[j];
+    B.w1 = (const float*)p[i++]; B.b1 = (const float*)p[i++];
+    B.g1 = (const float*)p[i++]; B.be1 = (const float*)p[i++];
+    B.rm1 = (float*)p[i++]; B.rv1 = (float*)p[i++]; B.nbt1 = (int64_t*)p[i++];
+    B.w2 = (const float*)p[i++]; B.b2 = (const float*)p[i++];
+    B.g2 = (const float*)p[i++]; B.be2 = (const float*)p[i++];
+    B.rm2 = (float*)p[i++]; B.rv2 = (float*)p[i++]; B.nbt2 = (int64_t*)p[i++];
+  }
+  for (int l = 0; l < d.L; ++l) { P.cb[l] = (const float*)p[i++]; P.cw[l] = (const float*)p[i++]; }
+  P.wf = (const float*)p[i++];
+  P.bf = (const float*)p[i++];
+  return P;
+}
+
+struct Grads {
+  float* tab[2 + MAX_CAT];
+  float *W0, *b0;
+  struct Blk { float *w1, *b1, *g1, *be1, *w2, *b2, *g2, *be2; } blk[MAX_RES];
+  float* cb[MAX_CROSS]; float* cw[MAX_CROSS];
+  float *wf, *bf;
+};
+
+Grads map_grads(const Dims& d, void* const* g) {
+  Grads G;
+  int i = 0;
+  for (int t = 0; t < 2 + d.K; ++t) G.tab[t] = (float*)g[i++];
+  G.W0 = (float*)g[i++];
+  G.b0 = (float*)g[i++];
+  for (int j = 0; j < d.R; ++j) {
+    auto& B = G.blk[j];
+    B.w1 = (float*)g[i++]; B.b1 = (float*)g[i++]; B.g1 = (float*)g[i++]; B.be1 = (float*)g[i++];
+    B.w2 = (float*)g[i++]; B.b2 = (float*)g[i++]; B.g2 = (float*)g[i++]; B.be2 = (float*)g[i++];
+  }
+  for (int l = 0; l < d.L; ++l) { G.cb[l] = (float*)g[i++]; G.cw[l] = (float*)g[i++]; }
+  G.wf = (float*)g[i++];
+  G.bf = (float*)g[i++];
+  return G;
+}
+
+GatherDesc make_gather(const Dims& d, const Params& P, int n_num) {
+  GatherDesc g;
+  memset(&g, 0, sizeof(g));
+  g.n_tab = 2 + d.K;
+  for (int t = 0; t < g.n_tab; ++t) {
+    g.tab[t] = P.tab[t];
+    g.rows[t] = d.rows[t];
+    g.width[t] = d.widths[t];
+  }
+  g.n_num = n_num;
+  g.D = d.D;
+  return g;
+}
+
+CrossParams make_cross(const Dims& d, const Params& P) {
+  CrossParams c;
+  memset(&c, 0, sizeof(c));
+  c.L = d.L;
+  for (int l = 0; l < d.L; ++l) { c.w[l] = P.cw[l]; c.b[l] = P.cb[l]; }
+  c.wf_cross = P.wf + d.H;
+  return c;
+}
+
+dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train, hipStream_t s) {
+  // weights -> padded T copies (+ transposes for backward); biases -> padded f32
+  std::vector<PackDesc> v;
+  auto add = [&](const float* src, void* dst, void* dst_t, int rows, int cols, int ld, int ld_t,
+                 int rows_p, int cols_p) {
+    PackDesc p{src, dst, dst_t, rows, cols, ld, ld_t, rows_p, cols_p};
+    v.push_back(p);
+  };
+  add(P.W0, L.W0p, train ? L.W0t : nullptr, d.H, d.D, d.Dp, d.Hp, d.Hp, d.Dp);
+  for (int j = 0; j < d.R; ++j) {
+    add(P.blk[j].w1, L.W1p[j], train ? L.W1t[j] : nullptr, d.H, d.H, d.Hp, d.Hp, d.Hp, d.Hp);
+    add(P.blk[j].w2, L.W2p[j], train ? L.W2t[j] : nullptr, d.H, d.H, d.Hp, d.Hp, d.Hp, d.Hp);
+  }
+  std::vector<PackDesc> vb;
+  auto addb = [&](const float* src, float* dst) {
+    PackDesc p{src, dst, nullptr, 1, d.H, d.Hp, 0, 1, 0};
+    vb.push_back(p);
+  };
+  addb(P.b0, L.b0p);
+  for (int j = 0; j < d.R; ++j) { addb(P.blk[j].b1, L.b1p[j]); addb(P.blk[j].b2, L.b2p[j]); }
+  for (size_t o = 0; o < v.size(); o += MAX_PACK) {
+    PackBatch pb;
+    pb.n = (int)std::min<size_t>(MAX_PACK, v.size() - o);
+    for (int i = 0; i < pb.n; ++i) pb.d[i] = v[o + i];
+    TRY(pack_weights(d.prec, pb, s));
+  }
+  for (size_t o = 0; o < vb.size(); o += MAX_PACK) {
+    PackBatch pb;
+    pb.n = (int)std::min<size_t>(MAX_PACK, vb.size() - o);
+    for (int i = 0; i < pb.n; ++i) pb.d[i] = vb[o + i];
+    TRY(pack_weights(DCNR_PREC_FP32, pb, s));
+  }
+  return DCNR_OK;
+}
+
+dcnr_status linear_fwd(const Dims& d, const void* A, int lda, const void* W, int K,
+                       const float* bias, void* out, int64_t B, hipStream_t s) {
+  GemmArgs g;
+  memset(&g, 0, sizeof(g));
+  g.A = A; g.lda = lda; g.B = W; g.ldb = K;
+  g.C = out; g.ldc = d.Hp; g.bias = bias;
+  g.M = B; g.N = d.Hp; g.K = K; g.k_per_split = K;
+  return gemm(d.prec, false, false, EPI_STORE, g, 1, s);
+}
+
+// dW[N][Kc] = sum_b dY[b][n] X[b][k]   (real extents Nr x Kr written to out)
+dcnr_status linear_dw(const Dims& d, const Layout& L, const void* dY, int ldy, int N,
+                      const void* X, int ldx, int Kc, int64_t B, float* out, int Nr, int Kr,
+                      int accumulate, hipStream_t s) {
+  int64_t tiles = cdiv(N, 128) * cdiv(Kc, 128);
+  int64_t S = std::max<int64_t>(1, std::min<int64_t>(512 / tiles, cdiv(B, 256)));
+  int64_t kps = rup(cdiv(B, S), 64);
+  S = cdiv(B, kps);
+  if (S * (int64_t)N * Kc > L.slab_elems) {
+    S = std::max<int64_t>(1, L.slab_elems / ((int64_t)N * Kc));
+    kps = rup(cdiv(B, S), 64);
+    S = cdiv(B, kps);
+  }
+  GemmArgs g;
+  memset(&g, 0, sizeof(g));
+  g.A = dY; g.lda = ldy; g.B = X; g.ldb = ldx;
+  g.C = L.slab; g.ldc = Kc;
+  g.M = N; g.N = Kc; g.K = B; g.k_per_split = kps; g.slab_stride = (int64_t)N * Kc;
+  TRY(gemm(d.prec, true, true, EPI_SPLITK, g, (int)S, s));
+  return splitk_reduce(L.slab, (int)S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s);
+}
+
+dcnr_status hook(const dcnr_model_desc* desc, const Dims& d, const Layout& L, hipStream_t s) {
+  if (!desc->bn_allreduce) return DCNR_OK;
+  int rc = desc->bn_allreduce(desc->bn_allreduce_ctx, L.sums, 3 * (int64_t)d.Hp + 1, (void*)s);
+  if (rc != 0) {
+    set_error("bn_allreduce hook failed (%d)", rc);
+    return DCNR_HIP_ERROR;
+  }
+  return DCNR_OK;
+}
+
+dcnr_status bn_layer_fwd(const dcnr_model_desc* desc, const Dims& d, const Layout& L,
+                         const void* t, int64_t B, bool train, const float* gamma,
+                         const float* beta, float* rm, float* rv, int64_t* nbt,
+                         const BnBufs& bb, hipStream_t s) {
+  BnFinal f{gamma, beta, rm, rv, nbt, bb.scale, bb.shift, bb.mean, bb.invstd};
+  if (train) {
+    int nc = 0;
+    TRY(col_stats(d.prec, t, B, d.Hp, d.Hp, L.part, &nc, s));
+    TRY(reduce_partials_nk(L.part, nc, 2, d.Hp, L.sums, (double)B, s));
+    TRY(hook(desc, d, L, s));
+  }
+  return bn_finalize2(L.sums, d.Hp, d.H, train ? 1 : 0, f, s);
+}
+
+}  // namespace
+}  // namespace dcnr
+
+using namespace dcnr;
+
+extern "C" {
+
+int dcnr_abi_version(void) { return DCNR_ABI_VERSION; }
+const char* dcnr_last_error(void) { return g_err; }
+
+int64_t dcnr_input_dim(const dcnr_model_desc* desc) {
+  Dims d;
+  if (make_dims(desc, &d) != DCNR_OK) return -1;
+  return d.D;
+}
+
+dcnr_status dcnr_workspace_size(const dcnr_model_desc* desc, int64_t B, int mode, size_t* bytes) {
+  Dims d;
+  TRY(make_dims(desc, &d));
+  if (!bytes || B < 0) { set_error("bad args"); return DCNR_BAD_ARG; }
+  *bytes = make_layout(d, B, mode, nullptr).total;
+  return DCNR_OK;
+}
+
+dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
+                         const int64_t* user_ids, const int64_t* item_ids,
+                         const int64_t* cat_features, const float* num_features, int64_t B,
+                         int mode, uint64_t dropout_seed, float* logits, void* ws,
+                         size_t ws_bytes, dcnr_stream_t stream) {
+  Dims d;
+  TRY(make_dims(desc, &d));
+  hipStream_t s = (hipStream_t)stream;
+  const bool train = mode == DCNR_TRAIN;
+  if (!params || !logits || !ws || B < 0 || (B > 0 && (!user_ids || !item_ids)) ||
+      (d.K > 0 && B > 0 && !cat_features) || (desc->n_num > 0 && B > 0 && !num_features)) {
+    set_error("dcnr_forward: null argument");
+    return DCNR_BAD_ARG;
+  }
+  if (train && B < 2) {
+    set_error("Expected more than 1 value per channel when training");
+    return DCNR_BAD_ARG;
+  }
+  Layout L = make_layout(d, B, mode, ws);
+  if (ws_bytes < L.total) {
+    set_error("workspace too small: %zu < %zu", ws_bytes, L.total);
+    return DCNR_WORKSPACE_TOO_SMALL;
+  }
+  if (B == 0) return DCNR_OK;
+  Params P = map_params(d, params);
+  TRY(pack_all(d, P, L, train, s));
+  const int check = (desc->flags & DCNR_FLAG_CHECK_INDICES) ? 1 : 0;
+  if (check) TRY(fill_zero(L.err, 4, s));
+  GatherDesc g = make_gather(d, P, desc->n_num);
+  CrossParams cp = make_cross(d, P);
+  TRY(gather_cross_fwd(d.prec, g, cp, user_ids, item_ids, cat_features, num_features, B, L.x0,
+                       d.Dp, L.zc, L.err, check, s));
+  TRY(linear_fwd(d, L.x0, d.Dp, L.W0p, d.Dp, L.b0p, L.h[0], B, s));
+  const float p = train ? d.dropout : 0.f;
+  for (int j = 0; j < d.R; ++j) {
+    const auto& Bk = P.blk[j];
+    TRY(linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
+    TRY(bn_layer_fwd(desc, d, L, L.t1[j], B, train, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
+                     L.bn[2 * j], s));
+    TRY(bn_relu_drop(d.prec, L.t1[j], L.a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
+                     dropout_seed, j, s));
+    TRY(linear_fwd(d, L.a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
+    TRY(bn_layer_fwd(desc, d, L, L.t2[j], B, train, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
+                     L.bn[2 * j + 1], s));
+    TRY(bn_add_relu2(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp, L.bn[2 * j + 1].scale,
+                     L.bn[2 * j + 1].shift, s));
+  }
+  TRY(row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
+  TRY(head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
+  return DCNR_OK;
+}
+
+dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void* const* grads,
+                          const int64_t* user_ids, const int64_t* item_ids,
+                          const int64_t* cat_features, const float* num_features, int64_t B,
+                          const float* dlogits, int accumulate, void* ws, size_t ws_bytes,
+                          dcnr_stream_t stream) {
+  Dims d;
+  TRY(make_dims(desc, &d));
+  hipStream_t s = (hipStream_t)stream;
+  if (!params || !grads || !dlogits || !ws || B < 2) {
+    set_error("dcnr_backward: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  Layout L = make_layout(d, B, DCNR_TRAIN, ws);
+  if (ws_bytes < L.total) {
+    set_error("workspace too small: %zu < %zu", ws_bytes, L.total);
+    return DCNR_WORKSPACE_TOO_SMALL;
+  }
+  Params P = map_params(d, params);
+  Grads Gr = map_grads(d, grads);
+  const float* dz = dlogits;
+  const int Hp = d.Hp, H = d.H;
+  const float p = d.dropout;
+  if (!accumulate)
+    for (int t = 0; t < 2 + d.K; ++t)
+      TRY(fill_zero(Gr.tab[t], (size_t)d.rows[t] * d.widths[t] * 4, s));
+
+  const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
+  for (int j = d.R - 1; j >= 0; --j) {
+    const auto& Bk = P.blk[j];
+    auto& Gk = Gr.blk[j];
+    const BnBufs& bn1 = L.bn[2 * j];
+    const BnBufs& bn2 = L.bn[2 * j + 1];
+    int nc = 0;
+    // ---- out = relu(BN2(t2) + h_j):  du, BN2 backward
+    TRY(bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, B, Hp,
+                       Hp, L.part, &nc, s));
+    TRY(reduce_partials_nk(L.part, nc, 3, Hp, L.sums, (double)B, s));
+    if (!Gin) TRY(sums_to_grad(L.sums + 2 * Hp, H, Gr.wf, accumulate, s));  // dW_f[:H]
+    TRY(sums_to_grad(L.sums + Hp, H, Gk.g2, accumulate, s));               // dgamma2
+    TRY(sums_to_grad(L.sums, H, Gk.be2, accumulate, s));                   // dbeta2
+    TRY(hook(desc, d, L, s));
+    TRY(bn_bwd_coef(L.sums, Hp, H, Bk.g2, bn2.invstd, L.coef, 1, s));
+    TRY(bwd_bn2_apply2(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, L.coef,
+                       B, Hp, Hp, L.dt2, L.du, L.part, &nc, s));
+    TRY(reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
+    TRY(sums_to_grad(L.sums, H, Gk.b2, accumulate, s));                    // dbias2
+    // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
+    TRY(bn_relu_drop(d.prec, L.t1[j], L.a1, B, Hp, Hp, bn1.scale, bn1.shift, p, 0, j, s));
+    TRY(linear_dw(d, L, L.dt2, Hp, Hp, L.a1, Hp, Hp, B, Gk.w2, H, H, accumulate, s));
+    {
+      GemmArgs g;
+      memset(&g, 0, sizeof(g));
+      g.A = L.dt2; g.lda = Hp; g.B = L.W2t[j]; g.ldb = Hp; g.C = L.da; g.ldc = Hp;
+      g.M = B; g.N = Hp; g.K = Hp; g.k_per_split = Hp;
+      TRY(gemm(d.prec, false, false, EPI_STORE, g, 1, s));
+    }
+    // ---- relu/dropout + BN1 backward
+    TRY(bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean, bn1.invstd, B, Hp, Hp,
+                      p, 0, j, L.part, &nc, s));
+    TRY(reduce_partials_nk(L.part, nc, 2, Hp, L.sums, (double)B, s));
+    TRY(sums_to_grad(L.sums + Hp, H, Gk.g1, accumulate, s));
+    TRY(sums_to_grad(L.sums, H, Gk.be1, accumulate, s));
+    TRY(hook(desc, d, L, s));
+    TRY(bn_bwd_coef(L.sums, Hp, H, Bk.g1, bn1.invstd, L.coef, 1, s));
+    TRY(bwd_bn1_apply2(d.prec, L.da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, L.a1,
+                       L.part, &nc, s));
+    TRY(reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
+    TRY(sums_to_grad(L.sums, H, Gk.b1, accumulate, s));
+    // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
+    TRY(linear_dw(d, L, L.a1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s));
+    {
+      GemmArgs g;
+      memset(&g, 0, sizeof(g));
+      g.A = L.a1; g.lda = Hp; g.B = L.W1t[j]; g.ldb = Hp; g.C = L.G; g.ldc = Hp;
+      g.resid = L.du; g.ldr = Hp;
+      g.M = B; g.N = Hp; g.K = Hp; g.k_per_split = Hp;
+      TRY(gemm(d.prec, false, false, EPI_STORE_RESID, g, 1, s));
+    }
+    Gin = L.G;
+  }
+  // ---- initial layer
+  int nc = 0;
+  TRY(col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
+  TRY(reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
+  TRY(sums_to_grad(L.sums, H, Gr.b0, accumulate, s));
+  TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s));
+  {
+    GemmArgs g;
+    memset(&g, 0, sizeof(g));
+    g.A = L.G; g.lda = Hp; g.B = L.W0t; g.ldb = Hp; g.C = L.dx0; g.ldc = d.Dp; g.out_f32 = 1;
+    g.M = B; g.N = d.Dp; g.K = Hp; g.k_per_split = Hp;
+    TRY(gemm(d.prec, false, false, EPI_STORE, g, 1, s));
+  }
+  // ---- cross stack + head bias + embedding scatter
+  GatherDesc g = make_gather(d, P, desc->n_num);
+  CrossBwdParams cb;
+  memset(&cb, 0, sizeof(cb));
+  cb.cp = make_cross(d, P);
+  for (int l = 0; l < d.L; ++l) { cb.dw[l] = Gr.cw[l]; cb.db[l] = Gr.cb[l]; }
+  cb.dwf_cross = Gr.wf + H;
+  cb.dbf = Gr.bf;
+  for (int t = 0; t < 2 + d.K; ++t) cb.emb_grad[t] = Gr.tab[t];
+  TRY(cross_bwd_scatter(g, cb, user_ids, item_ids, cat_features, num_features, dz, B, L.dx0, d.Dp,
+                        L.cpart, L.cpart_elems, accumulate, s));
+  return DCNR_OK;
+}
+
+size_t dcnr_bce_workspace_size(void) { return bce_ws_bytes() + 256; }
+
+dcnr_status dcnr_bce_with_logits(const float* logits, const float* labels, int64_t B, float* loss,
+                                 float* dlogits, float grad_scale, void* ws, size_t ws_bytes,
+                                 dcnr_stream_t stream) {
+  if (!logits || !labels || !loss || !ws || B < 1) {
+    set_error("dcnr_bce_with_logits: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  if (ws_bytes < bce_ws_bytes()) {
+    set_error("dcnr_bce_with_logits: workspace too small");
+    return DCNR_WORKSPACE_TOO_SMALL;
+  }
+  return bce(logits, labels, B, loss, dlogits, grad_scale, (double*)ws, (hipStream_t)stream);
+}
+
+dcnr_status dcnr_adam_step(int32_t n_tensors, float* const* params, const float* const* grads,
+                           float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
+                           float lr, float beta1, float beta2, float eps, float weight_decay,
+                           int64_t step, int decoupled, dcnr_stream_t stream) {
+  if (n_tensors < 0 || (n_tensors > 0 && (!params || !grads || !exp_avg || !exp_avg_sq || !numel)) ||
+      step < 1) {
+    set_error("dcnr_adam_step: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  return adam(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, lr, beta1, beta2, eps,
+              weight_decay, step, decoupled, (hipStream_t)stream);
+}
+
+dcnr_status dcnr_row_inv_norms(const float* table, int64_t N, int32_t d, float* inv_norms,
+                               dcnr_stream_t stream) {
+  if (!table || !inv_norms || d < 1 || N < 0) {
+    set_error("dcnr_row_inv_norms: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  return row_inv_norms(table, N, d, inv_norms, (hipStream_t)stream);
+}
+
+size_t dcnr_cosine_topk_workspace_size(int64_t N, int64_t Q, int32_t k) {
+  return topk_ws(N, Q, k) + 256;
+}
+
+dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t N, int32_t d,
+                             const float* queries, int64_t Q, int32_t k, int64_t* idx, float* dist,
+                             void* ws, size_t ws_bytes, dcnr_stream_t stream) {
+  if (!table || !inv_norms || !queries || !idx || !dist || (Q > 0 && !ws)) {
+    set_error("dcnr_cosine_topk: null argument");
+    return DCNR_BAD_ARG;
+  }
+  if (k > N) {
+    set_error("Expected n_neighbors <= n_samples_fit, but n_neighbors = %d, n_samples_fit = %lld",
+              k, (long long)N);
+    return DCNR_BAD_ARG;
+  }
+  return cosine_topk(table, inv_norms, N, d, queries, Q, k, idx, dist, ws, ws_bytes,
+                     (hipStream_t)stream);
+}
+
+dcnr_status dcnr_check_errors(void* ws, size_t ws_bytes, dcnr_stream_t stream) {
+  if (!ws || ws_bytes < 4) { set_error("bad workspace"); return DCNR_BAD_ARG; }
+  int flag = 0;
+  DCNR_HIP(hipMemcpyAsync(&flag, ws, 4, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  DCNR_HIP(hipStreamSynchronize((hipStream_t)stream));
+  if (flag) {
+    set_error("index out of range in self");
+    return DCNR_INDEX_OOB;
+  }
+  return DCNR_OK;
+}
+
+}  // extern "C"

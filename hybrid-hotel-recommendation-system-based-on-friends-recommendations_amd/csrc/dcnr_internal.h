@@ -1,0 +1,220 @@
+// Internal declarations shared by the libdcnr HIP translation units.
+// gfx950 (MI355X / CDNA4) only: 64-lane waves, MFMA, 160 KiB LDS per CU.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/dcnr.h"
+
+namespace dcnr {
+
+typedef __bf16 bf16;
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+constexpr int WAVE = 64;
+
+// ---------------------------------------------------------------- errors
+void set_error(const char* fmt, ...);
+#define DCNR_HIP(call)                                                              \
+  do {                                                                              \
+    hipError_t e_ = (call);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      ::dcnr::set_error("%s:%d %s: %s", __FILE__, __LINE__, #call, hipGetErrorString(e_)); \
+      return DCNR_HIP_ERROR;                                                        \
+    }                                                                               \
+  } while (0)
+#define DCNR_LAUNCH_CHECK()                                                         \
+  do {                                                                              \
+    hipError_t e_ = hipGetLastError();                                              \
+    if (e_ != hipSuccess) {                                                         \
+      ::dcnr::set_error("%s:%d launch: %s", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      return DCNR_HIP_ERROR;                                                        \
+    }                                                                               \
+  } while (0)
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int64_t rup(int64_t a, int64_t b) { return cdiv(a, b) * b; }
+
+// ------------------------------------------------------------- storage T
+template <typename T> struct St;
+template <> struct St<float> {
+  static __device__ __forceinline__ float ld(const float* p) { return *p; }
+  static __device__ __forceinline__ void st(float* p, float v) { *p = v; }
+};
+template <> struct St<bf16> {
+  static __device__ __forceinline__ float ld(const bf16* p) { return (float)(*p); }
+  static __device__ __forceinline__ void st(bf16* p, float v) { *p = (bf16)v; }
+};
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Counter-based dropout keep-test: deterministic in (seed, layer, row, col),
+// so backward regenerates the forward mask without storing it.
+__device__ __forceinline__ bool dropout_keep(uint64_t seed, int layer, int64_t row, int col,
+                                             uint32_t thresh) {
+  uint64_t x = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(layer + 1));
+  x += (uint64_t)row * 0x100000001B3ull + (uint64_t)col * 0xC2B2AE3D27D4EB4Full;
+  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27; x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return (uint32_t)(x >> 32) >= thresh;
+}
+
+// ------------------------------------------------------------------ GEMM
+// C[M,N] = A[M,K] . B[N,K]^T   (logical).  A_T: A stored [K][lda] (m fastest),
+// else [M][lda] (k fastest).  B_T: B stored [K][ldb] (n fastest), else [N][ldb].
+// K, lda, ldb, and (for A_T/B_T) M/N are multiples of 8; pad columns are 0.
+enum GemmEpi : int {
+  EPI_STORE = 0,        // out(T or f32) = acc + bias[n]  (bias may be null)
+  EPI_STORE_RESID = 1,  // out = acc + resid[m*ldr+n]
+  EPI_SPLITK = 2,       // f32 slab[split][m][n] = acc
+};
+
+struct GemmArgs {
+  const void* A; int64_t lda;
+  const void* B; int64_t ldb;
+  void* C; int64_t ldc;
+  const float* bias;
+  const void* resid; int64_t ldr;
+  int64_t M, N, K;
+  int64_t k_per_split;   // split-K chunk (multiple of BK), = K when no split
+  int64_t slab_stride;   // elements between split slabs (EPI_SPLITK)
+  int out_f32;           // 1: C is float, 0: C is T
+};
+
+// precision 0 = fp32 (f32 MFMA), 1 = bf16 (bf16 MFMA).
+dcnr_status gemm(int precision, bool a_t, bool b_t, int epi, const GemmArgs& a, int splits,
+                 hipStream_t s);
+
+// ------------------------------------------------------------ elementwise
+struct PackDesc {            // W [rows][cols] f32 -> dst T [rows_p][ld] (+ optional transpose)
+  const float* src; void* dst; void* dst_t;
+  int rows, cols, ld, ld_t;  // dst ld >= cols (pad 0), dst_t is [cols_p][ld_t] with ld_t >= rows
+  int rows_p, cols_p;
+};
+constexpr int MAX_PACK = 20;
+struct PackBatch { PackDesc d[MAX_PACK]; int n; };
+dcnr_status pack_weights(int precision, const PackBatch& pb, hipStream_t s);
+
+struct GatherDesc {
+  const float* tab[66];  // user, item, cat...
+  int64_t rows[66];
+  int width[66];
+  int n_tab;             // 2 + n_cat
+  int n_num;
+  int D;
+};
+struct CrossParams {
+  const float* w[8];     // [D] each
+  const float* b[8];     // [D]
+  int L;
+  const float* wf_cross; // final_linear.weight + H  ([D])
+};
+
+dcnr_status gather_cross_fwd(int precision, const GatherDesc& g, const CrossParams& cp,
+                             const int64_t* user, const int64_t* item, const int64_t* cat,
+                             const float* num, int64_t B, void* x0, int ldx, float* zc,
+                             int* err, int check, hipStream_t s);
+
+struct CrossBwdParams {
+  CrossParams cp;
+  float* dw[8]; float* db[8];  // grads (final)
+  float* dwf_cross;            // grad final_linear.weight + H
+  float* dbf;                  // grad final_linear.bias
+  float* emb_grad[66];         // dense embedding grads (scatter-add)
+};
+dcnr_status cross_bwd_scatter(const GatherDesc& g, const CrossBwdParams& p,
+                              const int64_t* user, const int64_t* item, const int64_t* cat,
+                              const float* num, const float* dz, int64_t B,
+                              const float* dx0_deep, int ld_dx, float* part, size_t part_elems,
+                              int accumulate, hipStream_t s);
+size_t cross_bwd_part_elems(int D, int L);
+
+// Column reductions: partial sums per row-chunk, part[nchunks][NK][N] (f32),
+// reduced in fixed order into sums[3][N] (f64; components >= NK zeroed) with
+// the row count at sums[3N] (the slot a SyncBN all-reduce also sums).
+dcnr_status col_stats(int precision, const void* t, int64_t B, int N, int ld, float* part,
+                      int* nchunks, hipStream_t s);                  // NK=2: t, t^2
+dcnr_status col_sum(int precision, const void* x, int64_t B, int N, int ld, float* part,
+                    int* nchunks, hipStream_t s);                    // NK=1
+dcnr_status reduce_partials_nk(const float* part, int nchunks, int NK, int N, double* sums,
+                               double count, hipStream_t s);
+
+struct BnFinal {   // per BN layer
+  const float* gamma; const float* beta; float* rmean; float* rvar; int64_t* nbt;
+  float* scale; float* shift;   // y = t*scale + shift  (N)
+  float* mean; float* invstd;   // saved for backward
+};
+// N = padded width, Nr = real width (parameters have Nr entries; pads -> 0)
+dcnr_status bn_finalize2(const double* sums, int N, int Nr, int train, const BnFinal& f,
+                         hipStream_t s);
+// coef[3][N] for dt = coef0*dy - coef1*xhat - coef2
+dcnr_status bn_bwd_coef(const double* sums, int N, int Nr, const float* gamma, const float* invstd,
+                        float* coef, int train, hipStream_t s);
+
+// a = dropout(relu(t*scale+shift))
+dcnr_status bn_relu_drop(int precision, const void* t, void* a, int64_t B, int N, int ld,
+                         const float* scale, const float* shift, float p, uint64_t seed,
+                         int layer, hipStream_t s);
+// out = relu(t*scale + shift + x)
+dcnr_status bn_add_relu2(int precision, const void* t, const void* x, void* out, int64_t B, int N,
+                         int ld, const float* scale, const float* shift, hipStream_t s);
+
+// backward helpers -----------------------------------------------------
+// du = g*[out>0], g = G[b,n] (G != null) or dz[b]*wf[n]; NK=3 partials:
+// [du, du*xhat, dz*out] (xhat = (t-mean)*invstd; the 3rd only when G == null)
+dcnr_status bwd_bn2_stats3(int precision, const void* G, const float* dz, const float* wf,
+                           const void* out, const void* t, const float* mean, const float* invstd,
+                           int64_t B, int N, int ld, float* part, int* nchunks, hipStream_t s);
+// dt = coef0*du - coef1*xhat - coef2 ; writes dt and du ; NK=1 partials of dt
+dcnr_status bwd_bn2_apply2(int precision, const void* G, const float* dz, const float* wf,
+                           const void* out, const void* t, const float* mean, const float* invstd,
+                           const float* coef, int64_t B, int N, int ld, void* dt, void* du,
+                           float* part, int* nchunks, hipStream_t s);
+// dr = da * keep/(1-p) * [t*scale+shift > 0] (in place); NK=2 partials [dr, dr*xhat]
+dcnr_status bwd_bn1_stats(int precision, void* da_dr, const void* t, const float* scale,
+                          const float* shift, const float* mean, const float* invstd, int64_t B,
+                          int N, int ld, float p, uint64_t seed, int layer, float* part,
+                          int* nchunks, hipStream_t s);
+// dt = coef0*dr - coef1*xhat - coef2 ; NK=1 partials of dt
+dcnr_status bwd_bn1_apply2(int precision, const void* dr, const void* t, const float* mean,
+                           const float* invstd, const float* coef, int64_t B, int N, int ld,
+                           void* dt, float* part, int* nchunks, hipStream_t s);
+// out[n] (+)= sums[n] as float, n < N
+dcnr_status sums_to_grad(const double* sums, int N, float* out, int accumulate, hipStream_t s);
+// out[n][k] (+)= sum_s slab[s][n][k]  (n < N, k < K; slab row stride ld_slab)
+dcnr_status splitk_reduce(const float* slab, int splits, int64_t slab_stride, int ld_slab,
+                          int N, int K, float* out, int accumulate, hipStream_t s);
+
+// head
+dcnr_status row_dot(int precision, const void* X, int ld, int N, const float* w, int64_t B,
+                    float* out, hipStream_t s);
+dcnr_status head_logits(const float* zdeep, const float* zc, const float* bf, int64_t B,
+                        float* logits, hipStream_t s);
+size_t bce_ws_bytes();
+dcnr_status bce(const float* z, const float* y, int64_t B, float* loss, float* dz, float scale,
+                double* part, hipStream_t s);
+
+// optimizer
+dcnr_status adam(int n, float* const* p, const float* const* g, float* const* m, float* const* v,
+                 const int64_t* numel, float lr, float b1, float b2, float eps, float wd,
+                 int64_t step, int decoupled, hipStream_t s);
+
+// knn
+dcnr_status row_inv_norms(const float* t, int64_t N, int d, float* out, hipStream_t s);
+size_t topk_ws(int64_t N, int64_t Q, int k);
+dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, const float* q,
+                        int64_t Q, int k, int64_t* idx, float* dist, void* ws, size_t ws_bytes,
+                        hipStream_t s);
+
+dcnr_status fill_zero(void* p, size_t bytes, hipStream_t s);
+
+}  // namespace dcnr

@@ -1,0 +1,536 @@
+// Row-major [B][ld] activation kernels of the deep tower: BatchNorm statistics,
+// BN/ReLU/dropout application, residual add, and their backward; all HBM
+// streaming with 16-byte accesses (8 bf16 or 4 fp32 per thread), column
+// partial sums reduced deterministically (fixed order, fp64) -- no atomics.
+//
+// Reference semantics: ResBlock.forward (train.py:112-122), nn.BatchNorm1d
+// (train: biased batch var for normalisation, running stats with momentum 0.1
+// and unbiased var; eval: running stats), nn.ReLU, nn.Dropout.
+#include "dcnr_internal.h"
+
+#include <cmath>
+#include <type_traits>
+
+namespace dcnr {
+namespace {
+
+constexpr int NT = 256;
+constexpr float BN_EPS = 1e-5f;
+constexpr double BN_MOM = 0.1;
+
+template <typename T> constexpr int VE = 16 / (int)sizeof(T);
+
+template <typename T>
+__device__ __forceinline__ void ldv(const T* p, float (&o)[VE<T>]) {
+  uint4 u = *reinterpret_cast<const uint4*>(p);
+  if constexpr (std::is_same<T, float>::value) {
+    o[0] = __uint_as_float(u.x); o[1] = __uint_as_float(u.y);
+    o[2] = __uint_as_float(u.z); o[3] = __uint_as_float(u.w);
+  } else {
+    const bf16* h = reinterpret_cast<const bf16*>(&u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (float)h[i];
+  }
+}
+template <typename T>
+__device__ __forceinline__ void stv(T* p, const float (&o)[VE<T>]) {
+  uint4 u;
+  if constexpr (std::is_same<T, float>::value) {
+    u.x = __float_as_uint(o[0]); u.y = __float_as_uint(o[1]);
+    u.z = __float_as_uint(o[2]); u.w = __float_as_uint(o[3]);
+  } else {
+    bf16* h = reinterpret_cast<bf16*>(&u);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = (bf16)o[i];
+  }
+  *reinterpret_cast<uint4*>(p) = u;
+}
+
+struct Geo {            // thread -> (row sub-index, column group)
+  int tcols, rpp, rsub, cg;
+  __device__ Geo(int N, int V) {
+    tcols = (N + V - 1) / V;
+    rpp = NT / tcols;
+    rsub = threadIdx.x / tcols;
+    cg = threadIdx.x % tcols;
+  }
+};
+
+// Generic row x column-group driver with NK per-column partial sums per chunk.
+template <typename T, int NK, class Op>
+__global__ __launch_bounds__(NT) void rowcol_kernel(Op op, int64_t B, int N, int rows_per_chunk,
+                                                    float* part) {
+  constexpr int V = VE<T>;
+  Geo g(N, V);
+  float acc[NK > 0 ? NK : 1][V];
+#pragma unroll
+  for (int k = 0; k < (NK > 0 ? NK : 1); ++k)
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[k][v] = 0.f;
+  const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
+  const int64_t r1 = min(B, r0 + rows_per_chunk);
+  if (g.rsub < g.rpp)
+    for (int64_t r = r0 + g.rsub; r < r1; r += g.rpp) op(r, g.cg * V, acc);
+  if constexpr (NK > 0) {
+    __shared__ float red[NT * NK * V];
+#pragma unroll
+    for (int k = 0; k < NK; ++k)
+#pragma unroll
+      for (int v = 0; v < V; ++v) red[(threadIdx.x * NK + k) * V + v] = acc[k][v];
+    __syncthreads();
+    if (g.rsub == 0) {
+      for (int k = 0; k < NK; ++k)
+        for (int v = 0; v < V; ++v) {
+          int c = g.cg * V + v;
+          if (c >= N) continue;
+          float s = 0.f;
+          for (int rs = 0; rs < g.rpp; ++rs) s += red[((rs * g.tcols + g.cg) * NK + k) * V + v];
+          part[((int64_t)blockIdx.x * NK + k) * N + c] = s;
+        }
+    }
+  }
+}
+
+template <typename T, int NK, class Op>
+dcnr_status run_rowcol(const Op& op, int64_t B, int N, float* part, int* nchunks, hipStream_t s) {
+  constexpr int V = VE<T>;
+  if (N % 8 || (N + V - 1) / V > NT) {
+    set_error("rowcol: unsupported width %d", N);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  int64_t want = 2048;
+  int rows = (int)std::max<int64_t>(16, cdiv(B, want));
+  int nc = (int)cdiv(B, rows);
+  if (nchunks) *nchunks = nc;
+  if (B <= 0) return DCNR_OK;
+  hipLaunchKernelGGL((rowcol_kernel<T, NK, Op>), dim3(nc), dim3(NT), 0, s, op, B, N, rows, part);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+// ---------------------------------------------------------------- ops
+template <typename T> struct StatsOp {   // sum t, sum t^2
+  const T* t; int ld;
+  __device__ void operator()(int64_t r, int c, float (&acc)[2][VE<T>]) const {
+    float x[VE<T>]; ldv<T>(t + r * ld + c, x);
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) { acc[0][v] += x[v]; acc[1][v] += x[v] * x[v]; }
+  }
+};
+
+template <typename T> struct ColSumOp {
+  const T* x; int ld;
+  __device__ void operator()(int64_t r, int c, float (&acc)[1][VE<T>]) const {
+    float a[VE<T>]; ldv<T>(x + r * ld + c, a);
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) acc[0][v] += a[v];
+  }
+};
+
+template <typename T> struct BnReluDropOp {  // a = dropout(relu(t*sc+sh))
+  const T* t; T* a; int ld; const float* sc; const float* sh;
+  float inv_keep; uint32_t thresh; uint64_t seed; int layer; int drop;
+  __device__ void operator()(int64_t r, int c, float (&)[1][VE<T>]) const {
+    float x[VE<T>]; ldv<T>(t + r * ld + c, x);
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) {
+      float y = fmaxf(x[v] * sc[c + v] + sh[c + v], 0.f);
+      if (drop) y = dropout_keep(seed, layer, r, c + v, thresh) ? y * inv_keep : 0.f;
+      x[v] = y;
+    }
+    stv<T>(a + r * ld + c, x);
+  }
+};
+
+template <typename T> struct BnAddReluOp {   // out = relu(t*sc+sh + x)
+  const T* t; const T* x; T* out; int ld; const float* sc; const float* sh;
+  __device__ void operator()(int64_t r, int c, float (&)[1][VE<T>]) const {
+    float a[VE<T>], b[VE<T>]; ldv<T>(t + r * ld + c, a); ldv<T>(x + r * ld + c, b);
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) a[v] = fmaxf(a[v] * sc[c + v] + sh[c + v] + b[v], 0.f);
+    stv<T>(out + r * ld + c, a);
+  }
+};
+
+// backward of out = relu(BN2(t2) + x): du = g*[out>0]
+template <typename T> struct Bwd2StatsOp {
+  const T* G; const float* dz; const float* wf; const T* out; const T* t;
+  const float* mean; const float* invstd; int ld;
+  __device__ void operator()(int64_t r, int c, float (&acc)[3][VE<T>]) const {
+    float o[VE<T>], tt[VE<T>], g[VE<T>];
+    ldv<T>(out + r * ld + c, o); ldv<T>(t + r * ld + c, tt);
+    if (G) ldv<T>(G + r * ld + c, g);
+    else {
+      float d = dz[r];
+#pragma unroll
+      for (int v = 0; v < VE<T>; ++v) g[v] = d * wf[c + v];
+    }
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) {
+      float du = o[v] > 0.f ? g[v] : 0.f;
+      float xh = (tt[v] - mean[c + v]) * invstd[c + v];
+      acc[0][v] += du;
+      acc[1][v] += du * xh;
+      if (!G) acc[2][v] += dz[r] * o[v];
+    }
+  }
+};
+
+// dt = kA*du - kB*xh - kC ; writes dt, du ; partial sum of dt (bias grad)
+template <typename T> struct Bwd2ApplyOp {
+  const T* G; const float* dz; const float* wf; const T* out; const T* t;
+  const float* mean; const float* invstd; const float* coef; int ld, N;
+  T* dt; T* du_out;
+  __device__ void operator()(int64_t r, int c, float (&acc)[1][VE<T>]) const {
+    float o[VE<T>], tt[VE<T>], g[VE<T>], d[VE<T>];
+    ldv<T>(out + r * ld + c, o); ldv<T>(t + r * ld + c, tt);
+    if (G) ldv<T>(G + r * ld + c, g);
+    else {
+      float dd = dz[r];
+#pragma unroll
+      for (int v = 0; v < VE<T>; ++v) g[v] = dd * wf[c + v];
+    }
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) {
+      float du = o[v] > 0.f ? g[v] : 0.f;
+      float xh = (tt[v] - mean[c + v]) * invstd[c + v];
+      float y = coef[c + v] * du - coef[N + c + v] * xh - coef[2 * N + c + v];
+      g[v] = du;
+      d[v] = y;
+      acc[0][v] += y;
+    }
+    stv<T>(dt + r * ld + c, d);
+    stv<T>(du_out + r * ld + c, g);
+  }
+};
+
+// dr = da * keep/(1-p) * [t*sc+sh > 0] (in place) ; partials [dr, dr*xh]
+template <typename T> struct Bwd1StatsOp {
+  T* da; const T* t; const float* sc; const float* sh; const float* mean; const float* invstd;
+  int ld; float inv_keep; uint32_t thresh; uint64_t seed; int layer; int drop;
+  __device__ void operator()(int64_t r, int c, float (&acc)[2][VE<T>]) const {
+    float a[VE<T>], tt[VE<T>];
+    ldv<T>(da + r * ld + c, a); ldv<T>(t + r * ld + c, tt);
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) {
+      float pre = tt[v] * sc[c + v] + sh[c + v];
+      float dr = pre > 0.f ? a[v] : 0.f;
+      if (drop) dr = dropout_keep(seed, layer, r, c + v, thresh) ? dr * inv_keep : 0.f;
+      float xh = (tt[v] - mean[c + v]) * invstd[c + v];
+      a[v] = dr;
+      acc[0][v] += dr;
+      acc[1][v] += dr * xh;
+    }
+    stv<T>(da + r * ld + c, a);
+  }
+};
+
+template <typename T> struct Bwd1ApplyOp {
+  const T* dr; const T* t; const float* mean; const float* invstd; const float* coef; int ld, N;
+  T* dt;
+  __device__ void operator()(int64_t r, int c, float (&acc)[1][VE<T>]) const {
+    float a[VE<T>], tt[VE<T>];
+    ldv<T>(dr + r * ld + c, a); ldv<T>(t + r * ld + c, tt);
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) {
+      float xh = (tt[v] - mean[c + v]) * invstd[c + v];
+      float y = coef[c + v] * a[v] - coef[N + c + v] * xh - coef[2 * N + c + v];
+      a[v] = y;
+      acc[0][v] += y;
+    }
+    stv<T>(dt + r * ld + c, a);
+  }
+};
+
+// ------------------------------------------------------------ small kernels
+// part [nchunks][NK][N] f32 -> sums [3][N] f64 (components >= NK zeroed) + count at [3N]
+__global__ void reduce_partials_kernel(const float* part, int nchunks, int NK, int N, double* sums,
+                                       double count) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < 3 * N) {
+    int k = i / N, n = i % N;
+    double s = 0.0;
+    if (k < NK)
+      for (int c = 0; c < nchunks; ++c) s += (double)part[((int64_t)c * NK + k) * N + n];
+    sums[i] = s;
+  }
+  if (i == 0) sums[3 * N] = count;
+}
+
+__global__ void bn_finalize_kernel(const double* sums, int N, int Nr, int train, BnFinal f) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  if (n >= Nr) {  // padded column: stays exactly zero
+    f.scale[n] = 0.f; f.shift[n] = 0.f; f.mean[n] = 0.f; f.invstd[n] = 0.f;
+    return;
+  }
+  double mean, var;
+  if (train) {
+    double cnt = sums[3 * N];
+    mean = sums[n] / cnt;
+    var = sums[N + n] / cnt - mean * mean;
+    if (var < 0) var = 0;
+    f.rmean[n] = (float)((1.0 - BN_MOM) * (double)f.rmean[n] + BN_MOM * mean);
+    f.rvar[n] = (float)((1.0 - BN_MOM) * (double)f.rvar[n] + BN_MOM * var * cnt / (cnt - 1.0));
+    if (n == 0 && f.nbt) f.nbt[0] += 1;
+  } else {
+    mean = f.rmean[n];
+    var = f.rvar[n];
+  }
+  float inv = (float)(1.0 / sqrt(var + (double)BN_EPS));
+  float sc = f.gamma[n] * inv;
+  f.scale[n] = sc;
+  f.shift[n] = f.beta[n] - (float)mean * sc;
+  f.mean[n] = (float)mean;
+  f.invstd[n] = inv;
+}
+
+// coef = [gamma*invstd, gamma*invstd*S1/cnt, gamma*invstd*S0/cnt] (train) or [gamma*invstd, 0, 0]
+__global__ void bn_bwd_coef_kernel(const double* sums, int N, int Nr, const float* gamma,
+                                   const float* invstd, float* coef, int train) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float a = n < Nr ? gamma[n] * invstd[n] : 0.f;
+  coef[n] = a;
+  if (train) {
+    double cnt = sums[3 * N];
+    coef[N + n] = (float)((double)a * sums[N + n] / cnt);
+    coef[2 * N + n] = (float)((double)a * sums[n] / cnt);
+  } else {
+    coef[N + n] = 0.f;
+    coef[2 * N + n] = 0.f;
+  }
+}
+
+__global__ void sums_to_grad_kernel(const double* sums, int N, float* out, int accumulate) {
+  int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float v = (float)sums[n];
+  out[n] = accumulate ? out[n] + v : v;
+}
+
+__global__ void splitk_reduce_kernel(const float* slab, int splits, int64_t stride, int ld, int N,
+                                     int K, float* out, int accumulate) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (int64_t)N * K) return;
+  int n = (int)(i / K), k = (int)(i % K);
+  float s = 0.f;
+  for (int z = 0; z < splits; ++z) s += slab[z * stride + (int64_t)n * ld + k];
+  out[i] = accumulate ? out[i] + s : s;
+}
+
+template <typename T>
+__global__ void pack_kernel(PackBatch pb) {
+  const PackDesc& d = pb.d[blockIdx.y];
+  T* dst = (T*)d.dst;
+  int64_t tot = (int64_t)d.rows_p * d.ld;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    int r = (int)(i / d.ld), c = (int)(i % d.ld);
+    float v = (r < d.rows && c < d.cols) ? d.src[(int64_t)r * d.cols + c] : 0.f;
+    St<T>::st(dst + i, v);
+  }
+  if (d.dst_t) {
+    T* dt = (T*)d.dst_t;
+    int64_t tot2 = (int64_t)d.cols_p * d.ld_t;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot2;
+         i += (int64_t)gridDim.x * blockDim.x) {
+      int c = (int)(i / d.ld_t), r = (int)(i % d.ld_t);
+      float v = (r < d.rows && c < d.cols) ? d.src[(int64_t)r * d.cols + c] : 0.f;
+      St<T>::st(dt + i, v);
+    }
+  }
+}
+
+}  // namespace
+
+// ================================================================== API
+#define DISPATCH_T(prec, ...) \
+  ((prec) == DCNR_PREC_BF16 ? __VA_ARGS__##_impl<bf16> : __VA_ARGS__##_impl<float>)
+
+dcnr_status pack_weights(int precision, const PackBatch& pb, hipStream_t s) {
+  if (pb.n == 0) return DCNR_OK;
+  dim3 grid(64, pb.n);
+  if (precision == DCNR_PREC_BF16) hipLaunchKernelGGL(pack_kernel<bf16>, grid, dim3(NT), 0, s, pb);
+  else hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(NT), 0, s, pb);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+template <typename T>
+static dcnr_status col_stats_impl(const void* t, int64_t B, int N, int ld, float* part, int* nc,
+                                  hipStream_t s) {
+  StatsOp<T> op{(const T*)t, ld};
+  return run_rowcol<T, 2>(op, B, N, part, nc, s);
+}
+dcnr_status col_stats(int precision, const void* t, int64_t B, int N, int ld, float* part,
+                      int* nchunks, hipStream_t s) {
+  return precision == DCNR_PREC_BF16 ? col_stats_impl<bf16>(t, B, N, ld, part, nchunks, s)
+                                     : col_stats_impl<float>(t, B, N, ld, part, nchunks, s);
+}
+
+template <typename T>
+static dcnr_status col_sum_impl(const void* x, int64_t B, int N, int ld, float* part, int* nc,
+                                hipStream_t s) {
+  ColSumOp<T> op{(const T*)x, ld};
+  return run_rowcol<T, 1>(op, B, N, part, nc, s);
+}
+dcnr_status col_sum(int precision, const void* x, int64_t B, int N, int ld, float* part,
+                    int* nchunks, hipStream_t s) {
+  return precision == DCNR_PREC_BF16 ? col_sum_impl<bf16>(x, B, N, ld, part, nchunks, s)
+                                     : col_sum_impl<float>(x, B, N, ld, part, nchunks, s);
+}
+
+dcnr_status reduce_partials_nk(const float* part, int nchunks, int NK, int N, double* sums,
+                               double count, hipStream_t s) {
+  int tot = 3 * N;
+  hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)cdiv(std::max(tot, 1), NT)), dim3(NT),
+                     0, s, part, nchunks, NK, N, sums, count);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status bn_finalize2(const double* sums, int N, int Nr, int train, const BnFinal& f,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(N, NT)), dim3(NT), 0, s, sums, N, Nr,
+                     train, f);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status bn_bwd_coef(const double* sums, int N, int Nr, const float* gamma, const float* invstd,
+                        float* coef, int train, hipStream_t s) {
+  hipLaunchKernelGGL(bn_bwd_coef_kernel, dim3((unsigned)cdiv(N, NT)), dim3(NT), 0, s, sums, N, Nr,
+                     gamma, invstd, coef, train);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+template <typename T>
+static dcnr_status bn_relu_drop_impl(const void* t, void* a, int64_t B, int N, int ld,
+                                     const float* sc, const float* sh, float p, uint64_t seed,
+                                     int layer, hipStream_t s) {
+  BnReluDropOp<T> op{(const T*)t, (T*)a, ld, sc, sh, p > 0.f ? 1.f / (1.f - p) : 1.f,
+                     (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0), seed, layer,
+                     p > 0.f};
+  return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
+}
+dcnr_status bn_relu_drop(int precision, const void* t, void* a, int64_t B, int N, int ld,
+                         const float* scale, const float* shift, float p, uint64_t seed,
+                         int layer, hipStream_t s) {
+  return precision == DCNR_PREC_BF16
+             ? bn_relu_drop_impl<bf16>(t, a, B, N, ld, scale, shift, p, seed, layer, s)
+             : bn_relu_drop_impl<float>(t, a, B, N, ld, scale, shift, p, seed, layer, s);
+}
+
+template <typename T>
+static dcnr_status bn_add_relu_impl(const void* t, const void* x, void* out, int64_t B, int N,
+                                    int ld, const float* sc, const float* sh, hipStream_t s) {
+  BnAddReluOp<T> op{(const T*)t, (const T*)x, (T*)out, ld, sc, sh};
+  return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
+}
+dcnr_status bn_add_relu2(int precision, const void* t, const void* x, void* out, int64_t B, int N,
+                         int ld, const float* scale, const float* shift, hipStream_t s) {
+  return precision == DCNR_PREC_BF16
+             ? bn_add_relu_impl<bf16>(t, x, out, B, N, ld, scale, shift, s)
+             : bn_add_relu_impl<float>(t, x, out, B, N, ld, scale, shift, s);
+}
+
+template <typename T>
+static dcnr_status bwd2_stats_impl(const void* G, const float* dz, const float* wf, const void* out,
+                                   const void* t, const float* mean, const float* invstd,
+                                   int64_t B, int N, int ld, float* part, int* nc, hipStream_t s) {
+  Bwd2StatsOp<T> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, ld};
+  return run_rowcol<T, 3>(op, B, N, part, nc, s);
+}
+dcnr_status bwd_bn2_stats3(int precision, const void* G, const float* dz, const float* wf,
+                           const void* out, const void* t, const float* mean, const float* invstd,
+                           int64_t B, int N, int ld, float* part, int* nchunks, hipStream_t s) {
+  return precision == DCNR_PREC_BF16
+             ? bwd2_stats_impl<bf16>(G, dz, wf, out, t, mean, invstd, B, N, ld, part, nchunks, s)
+             : bwd2_stats_impl<float>(G, dz, wf, out, t, mean, invstd, B, N, ld, part, nchunks, s);
+}
+
+template <typename T>
+static dcnr_status bwd2_apply_impl(const void* G, const float* dz, const float* wf,
+                                   const void* out, const void* t, const float* mean,
+                                   const float* invstd, const float* coef, int64_t B, int N,
+                                   int ld, void* dt, void* du, float* part, int* nc,
+                                   hipStream_t s) {
+  Bwd2ApplyOp<T> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, coef, ld, N,
+                    (T*)dt, (T*)du};
+  return run_rowcol<T, 1>(op, B, N, part, nc, s);
+}
+dcnr_status bwd_bn2_apply2(int precision, const void* G, const float* dz, const float* wf,
+                           const void* out, const void* t, const float* mean, const float* invstd,
+                           const float* coef, int64_t B, int N, int ld, void* dt, void* du,
+                           float* part, int* nchunks, hipStream_t s) {
+  return precision == DCNR_PREC_BF16
+             ? bwd2_apply_impl<bf16>(G, dz, wf, out, t, mean, invstd, coef, B, N, ld, dt, du,
+                                     part, nchunks, s)
+             : bwd2_apply_impl<float>(G, dz, wf, out, t, mean, invstd, coef, B, N, ld, dt, du,
+                                      part, nchunks, s);
+}
+
+template <typename T>
+static dcnr_status bwd1_stats_impl(void* da, const void* t, const float* sc, const float* sh,
+                                   const float* mean, const float* invstd, int64_t B, int N,
+                                   int ld, float p, uint64_t seed, int layer, float* part, int* nc,
+                                   hipStream_t s) {
+  Bwd1StatsOp<T> op{(T*)da, (const T*)t, sc, sh, mean, invstd, ld,
+                    p > 0.f ? 1.f / (1.f - p) : 1.f,
+                    (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0), seed, layer,
+                    p > 0.f};
+  return run_rowcol<T, 2>(op, B, N, part, nc, s);
+}
+dcnr_status bwd_bn1_stats(int precision, void* da_dr, const void* t, const float* scale,
+                          const float* shift, const float* mean, const float* invstd, int64_t B,
+                          int N, int ld, float p, uint64_t seed, int layer, float* part,
+                          int* nchunks, hipStream_t s) {
+  return precision == DCNR_PREC_BF16
+             ? bwd1_stats_impl<bf16>(da_dr, t, scale, shift, mean, invstd, B, N, ld, p, seed,
+                                     layer, part, nchunks, s)
+             : bwd1_stats_impl<float>(da_dr, t, scale, shift, mean, invstd, B, N, ld, p, seed,
+                                      layer, part, nchunks, s);
+}
+
+template <typename T>
+static dcnr_status bwd1_apply_impl(const void* dr, const void* t, const float* mean,
+                                   const float* invstd, const float* coef, int64_t B, int N,
+                                   int ld, void* dt, float* part, int* nc, hipStream_t s) {
+  Bwd1ApplyOp<T> op{(const T*)dr, (const T*)t, mean, invstd, coef, ld, N, (T*)dt};
+  return run_rowcol<T, 1>(op, B, N, part, nc, s);
+}
+dcnr_status bwd_bn1_apply2(int precision, const void* dr, const void* t, const float* mean,
+                           const float* invstd, const float* coef, int64_t B, int N, int ld,
+                           void* dt, float* part, int* nchunks, hipStream_t s) {
+  return precision == DCNR_PREC_BF16
+             ? bwd1_apply_impl<bf16>(dr, t, mean, invstd, coef, B, N, ld, dt, part, nchunks, s)
+             : bwd1_apply_impl<float>(dr, t, mean, invstd, coef, B, N, ld, dt, part, nchunks, s);
+}
+
+dcnr_status sums_to_grad(const double* sums, int N, float* out, int accumulate, hipStream_t s) {
+  if (N <= 0) return DCNR_OK;
+  hipLaunchKernelGGL(sums_to_grad_kernel, dim3((unsigned)cdiv(N, NT)), dim3(NT), 0, s, sums, N,
+                     out, accumulate);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status splitk_reduce(const float* slab, int splits, int64_t slab_stride, int ld_slab, int N,
+                          int K, float* out, int accumulate, hipStream_t s) {
+  int64_t tot = (int64_t)N * K;
+  if (tot <= 0) return DCNR_OK;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)cdiv(tot, NT)), dim3(NT), 0, s, slab,
+                     splits, slab_stride, ld_slab, N, K, out, accumulate);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status fill_zero(void* p, size_t bytes, hipStream_t s) {
+  if (!bytes) return DCNR_OK;
+  DCNR_HIP(hipMemsetAsync(p, 0, bytes, s));
+  return DCNR_OK;
+}
+
+}  // namespace dcnr

@@ -1,0 +1,161 @@
+// Logit head and BCE loss (train.py:169-170, 206, 224), and the fused
+// multi-tensor Adam/AdamW step (train.py:201-204, 226).
+#include "dcnr_internal.h"
+
+#include <cmath>
+#include <type_traits>
+
+namespace dcnr {
+namespace {
+constexpr int NT = 256;
+
+// zdeep[b] = sum_n X[b][n] * w[n]   (deep half of final_linear), wave per row
+template <typename T>
+__global__ __launch_bounds__(NT) void row_dot_kernel(const T* X, int ld, int N, const float* w,
+                                                     int64_t B, float* out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * (NT / WAVE);
+  for (int64_t b = (int64_t)blockIdx.x * (NT / WAVE) + (threadIdx.x >> 6); b < B; b += nw) {
+    float s = 0.f;
+    for (int n = lane; n < N; n += WAVE) s += St<T>::ld(X + b * ld + n) * w[n];
+    s = wave_sum(s);
+    if (lane == 0) out[b] = s;
+  }
+}
+
+__global__ void logits_kernel(const float* zdeep, const float* zc, const float* bf, int64_t B,
+                              float* z) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < B) z[i] = (zdeep[i] + zc[i]) + bf[0];
+}
+
+// stage 1: per block partial sum of the BCE terms (+ dz); stage 2: fixed-order sum
+__global__ __launch_bounds__(NT) void bce_kernel(const float* z, const float* y, int64_t B,
+                                                 float* dz, float scale, double* part) {
+  __shared__ double red[NT];
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * NT + threadIdx.x; i < B; i += (int64_t)gridDim.x * NT) {
+    float zz = z[i], yy = y[i];
+    // max(z,0) - z*y + log1p(exp(-|z|))   (torch's binary_cross_entropy_with_logits)
+    float l = fmaxf(zz, 0.f) - zz * yy + log1pf(expf(-fabsf(zz)));
+    acc += (double)l;
+    if (dz) dz[i] = scale * (1.f / (1.f + expf(-zz)) - yy) / (float)B;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = NT / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void bce_final_kernel(const double* part, int n, int64_t B, float* loss) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < n; ++i) s += part[i];
+    loss[0] = (float)(s / (double)B);
+  }
+}
+
+constexpr int MAXT = 64;
+struct AdamBatch {
+  float* p[MAXT]; const float* g[MAXT]; float* m[MAXT]; float* v[MAXT];
+  int64_t n[MAXT]; int64_t blk0[MAXT + 1];
+  int nt;
+};
+
+// torch.optim._functional single-tensor Adam/AdamW algorithm, fp32:
+//   AdamW: p *= 1 - lr*wd ; Adam: g += wd*p
+//   m = lerp(m, g, 1-b1) ; v = b2*v + (1-b2)*g*g
+//   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+__global__ __launch_bounds__(NT) void adam_kernel(AdamBatch ab, float lr, float b1, float b2,
+                                                  float eps, float wd, float step_size,
+                                                  float bc2_sqrt, int decoupled) {
+  int t = 0;
+  while (t + 1 < ab.nt && (int64_t)blockIdx.x >= ab.blk0[t + 1]) ++t;
+  const int64_t base = ((int64_t)blockIdx.x - ab.blk0[t]) * (NT * 4);
+  float* p = ab.p[t];
+  const float* g = ab.g[t];
+  float* m = ab.m[t];
+  float* v = ab.v[t];
+  const int64_t n = ab.n[t];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    int64_t i = base + u * NT + threadIdx.x;
+    if (i >= n) break;
+    float pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+    if (decoupled) pp = pp * (1.f - lr * wd);
+    else if (wd != 0.f) gg = gg + wd * pp;
+    mm = mm + (1.f - b1) * (gg - mm);
+    vv = vv * b2 + (1.f - b2) * gg * gg;
+    float denom = sqrtf(vv) / bc2_sqrt + eps;
+    pp = pp - step_size * (mm / denom);
+    p[i] = pp; m[i] = mm; v[i] = vv;
+  }
+}
+
+}  // namespace
+
+dcnr_status row_dot(int precision, const void* X, int ld, int N, const float* w, int64_t B,
+                    float* out, hipStream_t s) {
+  if (B <= 0) return DCNR_OK;
+  int64_t blocks = std::min<int64_t>(cdiv(B, NT / WAVE), 4096);
+  if (precision == DCNR_PREC_BF16)
+    hipLaunchKernelGGL(row_dot_kernel<bf16>, dim3((unsigned)blocks), dim3(NT), 0, s,
+                       (const bf16*)X, ld, N, w, B, out);
+  else
+    hipLaunchKernelGGL(row_dot_kernel<float>, dim3((unsigned)blocks), dim3(NT), 0, s,
+                       (const float*)X, ld, N, w, B, out);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status head_logits(const float* zdeep, const float* zc, const float* bf, int64_t B,
+                        float* logits, hipStream_t s) {
+  if (B <= 0) return DCNR_OK;
+  hipLaunchKernelGGL(logits_kernel, dim3((unsigned)cdiv(B, NT)), dim3(NT), 0, s, zdeep, zc, bf, B,
+                     logits);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+constexpr int BCE_BLOCKS = 512;
+size_t bce_ws_bytes() { return BCE_BLOCKS * sizeof(double); }
+
+dcnr_status bce(const float* z, const float* y, int64_t B, float* loss, float* dz, float scale,
+                double* part, hipStream_t s) {
+  int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(BCE_BLOCKS, cdiv(B, NT)));
+  hipLaunchKernelGGL(bce_kernel, dim3(blocks), dim3(NT), 0, s, z, y, B, dz, scale, part);
+  DCNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bce_final_kernel, dim3(1), dim3(64), 0, s, part, blocks, B, loss);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status adam(int n, float* const* p, const float* const* g, float* const* m, float* const* v,
+                 const int64_t* numel, float lr, float b1, float b2, float eps, float wd,
+                 int64_t step, int decoupled, hipStream_t s) {
+  double bc1 = 1.0 - std::pow((double)b1, (double)step);
+  double bc2 = 1.0 - std::pow((double)b2, (double)step);
+  float step_size = (float)(lr / bc1);
+  float bc2_sqrt = (float)std::sqrt(bc2);
+  for (int off = 0; off < n; off += MAXT) {
+    AdamBatch ab;
+    ab.nt = std::min(MAXT, n - off);
+    ab.blk0[0] = 0;
+    for (int i = 0; i < ab.nt; ++i) {
+      ab.p[i] = p[off + i]; ab.g[i] = g[off + i]; ab.m[i] = m[off + i]; ab.v[i] = v[off + i];
+      ab.n[i] = numel[off + i];
+      ab.blk0[i + 1] = ab.blk0[i] + cdiv(ab.n[i], NT * 4);
+    }
+    int64_t blocks = ab.blk0[ab.nt];
+    if (blocks == 0) continue;
+    hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(NT), 0, s, ab, lr, b1, b2, eps,
+                       wd, step_size, bc2_sqrt, decoupled);
+    DCNR_LAUNCH_CHECK();
+  }
+  return DCNR_OK;
+}
+
+}  // namespace dcnr

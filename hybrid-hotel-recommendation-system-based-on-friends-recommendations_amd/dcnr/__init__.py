@@ -1,0 +1,19 @@
+"""dcnr -- MI355X-native (gfx950 HIP) DCN-R ranking path.
+
+Drop-in surfaces of the reference (Krist-Marrakesh/Hybrid-Hotel-Recommendation-
+System-Based-on-Friends-Recommendations):
+
+  DCN_RecSys, CrossLayer, ResBlock   train.py:90-170 / main.py:61-127
+  BCEWithLogitsLoss                  train.py:206
+  AdamW, Adam                        train.py:201-204
+  NearestNeighbors (cosine, brute)   main.py:268-270
+  FusedTrainer                       the train.py:219-226 inner-loop step
+
+All compute runs in libdcnr.so (C ABI: include/dcnr.h) on the HIP device.
+"""
+from .model import CrossLayer, DCN_RecSys, ResBlock  # noqa: F401
+from .ops import Adam, AdamW, BCEWithLogitsLoss, bce_with_logits  # noqa: F401
+from .knn import NearestNeighbors  # noqa: F401
+from .train import FusedTrainer  # noqa: F401
+
+__version__ = "0.1.0"

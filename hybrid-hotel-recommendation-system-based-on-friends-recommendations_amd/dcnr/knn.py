@@ -1,0 +1,79 @@
+"""Cosine nearest neighbours on libdcnr: drop-in for the
+``sklearn.neighbors.NearestNeighbors(metric='cosine', algorithm='brute')``
+index the reference builds at startup (main.py:268-270) and queries per
+positive hotel (main.py:200) and per /similar_items request (main.py:300).
+
+``kneighbors`` keeps sklearn's contract (numpy in, numpy ``(dist, idx)`` out,
+ascending distance, the query row itself included when it is in the index --
+callers drop position 0 as main.py does).  Ties are ordered by row index
+(sklearn's argsort order among exactly equal distances is unspecified).
+``kneighbors_device`` takes/returns device tensors for batched callers.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+
+
+class NearestNeighbors:
+    def __init__(self, n_neighbors=5, metric='cosine', algorithm='brute', device='cuda'):
+        if metric != 'cosine':
+            raise NotImplementedError("dcnr.NearestNeighbors implements metric='cosine' only "
+                                      "(the reference's only use, main.py:268)")
+        if algorithm not in ('brute', 'auto'):
+            raise NotImplementedError("dcnr.NearestNeighbors is a brute-force index")
+        self.n_neighbors = n_neighbors
+        self.metric = metric
+        self.algorithm = algorithm
+        self.device = torch.device(device)
+        self._table = None
+        self._inv = None
+
+    def fit(self, X, y=None):
+        t = torch.as_tensor(np.asarray(X, dtype=np.float32) if not torch.is_tensor(X) else X)
+        t = t.to(self.device, torch.float32).contiguous()
+        if t.dim() != 2:
+            raise ValueError("Expected 2D array")
+        if self.device.type != 'cuda':
+            raise RuntimeError("dcnr.NearestNeighbors runs on the HIP device only")
+        self._table = t
+        self._inv = torch.empty(t.shape[0], dtype=torch.float32, device=self.device)
+        lib = _lib.load()
+        _lib.check(lib.dcnr_row_inv_norms(t.data_ptr(), t.shape[0], t.shape[1], self._inv.data_ptr(),
+                                          _lib.stream_ptr(self.device)), "dcnr_row_inv_norms")
+        self.n_samples_fit_ = t.shape[0]
+        self.n_features_in_ = t.shape[1]
+        return self
+
+    def kneighbors_device(self, q: torch.Tensor, k: int):
+        if self._table is None:
+            raise RuntimeError("This NearestNeighbors instance is not fitted yet")
+        lib = _lib.load()
+        q = q.to(self.device, torch.float32).reshape(-1, self._table.shape[1]).contiguous()
+        Q = q.shape[0]
+        N, d = self._table.shape
+        if k > N:
+            raise ValueError(f"Expected n_neighbors <= n_samples_fit, but n_neighbors = {k}, "
+                             f"n_samples_fit = {N}, n_samples = {Q}")
+        idx = torch.empty((Q, k), dtype=torch.int64, device=self.device)
+        dist = torch.empty((Q, k), dtype=torch.float32, device=self.device)
+        nb = int(lib.dcnr_cosine_topk_workspace_size(N, Q, k))
+        ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=self.device)
+        _lib.check(lib.dcnr_cosine_topk(self._table.data_ptr(), self._inv.data_ptr(), N, d,
+                                        q.data_ptr(), Q, k, idx.data_ptr(), dist.data_ptr(),
+                                        ws.data_ptr(), ws.numel(), _lib.stream_ptr(self.device)),
+                   "dcnr_cosine_topk")
+        return dist, idx
+
+    def kneighbors(self, X=None, n_neighbors=None, return_distance=True):
+        k = self.n_neighbors if n_neighbors is None else int(n_neighbors)
+        if k <= 0:
+            raise ValueError(f"Expected n_neighbors > 0. Got {k}")
+        q = torch.as_tensor(np.asarray(X, dtype=np.float32)) if not torch.is_tensor(X) else X
+        dist, idx = self.kneighbors_device(q, k)
+        idx_np = idx.cpu().numpy()
+        if return_distance:
+            return dist.cpu().numpy(), idx_np
+        return idx_np

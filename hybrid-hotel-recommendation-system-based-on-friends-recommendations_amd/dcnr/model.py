@@ -1,0 +1,259 @@
+"""Drop-in ``DCN_RecSys`` whose forward/backward run on libdcnr (gfx950 HIP).
+
+Mirrors the reference module (train.py:90-170, duplicated in main.py:61-127):
+same constructor signature, same submodules in the same order (so
+``torch.manual_seed(s)`` yields the *same* initial weights as the reference),
+same ``state_dict`` keys and shapes, same forward signature and
+``.squeeze()`` semantics, and ``loss.backward()`` / ``torch.optim`` work
+unchanged.  The whole forward (gathers, cross stack, deep tower, head) is one
+native call (``dcnr_forward``); the backward is one native call
+(``dcnr_backward``).  There is no CPU path: calling forward with CPU tensors
+raises.
+
+Extra keyword (not in the reference): ``precision`` -- ``"fp32"`` (default,
+f32 MFMA, parity with the reference) or ``"bf16"`` (bf16 MFMA deep tower with
+fp32 accumulation and fp32 master weights).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from . import _lib
+
+
+class CrossLayer(nn.Module):
+    """train.py:90-99.  Holds the parameters; the fused path in
+    DCN_RecSys.forward never calls this forward (kept for API parity and for
+    standalone use): x + x*(x.w) + b."""
+
+    def __init__(self, input_dim):
+        super().__init__()
+        self.w = nn.Linear(input_dim, 1, bias=False)
+        self.b = nn.Parameter(torch.zeros(input_dim))
+
+    def forward(self, x):
+        return x + x * self.w(x) + self.b
+
+
+class ResBlock(nn.Module):
+    """train.py:102-122 (parameter container; fused in DCN_RecSys.forward)."""
+
+    def __init__(self, hidden_dim, dropout):
+        super().__init__()
+        self.layer1 = nn.Linear(hidden_dim, hidden_dim)
+        self.bn1 = nn.BatchNorm1d(hidden_dim)
+        self.relu = nn.ReLU()
+        self.dropout = nn.Dropout(dropout)
+        self.layer2 = nn.Linear(hidden_dim, hidden_dim)
+        self.bn2 = nn.BatchNorm1d(hidden_dim)
+
+    def forward(self, x):
+        identity = x
+        out = self.dropout(self.relu(self.bn1(self.layer1(x))))
+        out = self.bn2(self.layer2(out))
+        out = out + identity
+        return self.relu(out)
+
+
+_PRECISIONS = {"fp32": _lib.PREC_FP32, "bf16": _lib.PREC_BF16}
+
+
+class DCN_RecSys(nn.Module):
+    """Deep & Cross Network with residual deep tower (train.py:125-170)."""
+
+    def __init__(self, n_users, n_items, cat_dims, n_num_features, params, precision="fp32",
+                 check_indices=False):
+        super().__init__()
+        emb_dim = params['emb_dim']
+        hidden_dim = params['hidden_dim']
+        n_cross_layers = params['n_cross_layers']
+        dropout = params['dropout']
+        n_res_blocks = params.get('n_res_blocks', 2)
+
+        self.user_embedding = nn.Embedding(n_users, emb_dim)
+        self.item_embedding = nn.Embedding(n_items, emb_dim)
+        self.cat_embeddings = nn.ModuleList([
+            nn.Embedding(n_cat, int(np.sqrt(n_cat)) + 1) for n_cat in cat_dims.values()])
+        cat_emb_sum_dim = sum([int(np.sqrt(n_cat)) + 1 for n_cat in cat_dims.values()])
+        input_dim = emb_dim * 2 + cat_emb_sum_dim + n_num_features
+        self.initial_deep_layer = nn.Linear(input_dim, hidden_dim)
+        self.res_blocks = nn.ModuleList([ResBlock(hidden_dim, dropout) for _ in range(n_res_blocks)])
+        self.cross_network = nn.ModuleList([CrossLayer(input_dim) for _ in range(n_cross_layers)])
+        final_dim = hidden_dim + input_dim
+        self.final_linear = nn.Linear(final_dim, 1)
+
+        if precision not in _PRECISIONS:
+            raise ValueError(f"precision must be one of {list(_PRECISIONS)}")
+        self.precision = precision
+        self.check_indices = bool(check_indices)
+        self._cat_rows = (ctypes.c_int64 * max(1, len(cat_dims)))(*[int(n) for n in cat_dims.values()])
+        self._dims = dict(n_users=n_users, n_items=n_items, cat_dims=list(cat_dims.values()),
+                          n_num=n_num_features, emb_dim=emb_dim, hidden=hidden_dim,
+                          n_cross=n_cross_layers, n_res=n_res_blocks, dropout=float(dropout),
+                          input_dim=input_dim)
+        self.bn_allreduce = None   # set by dcnr.parallel for SyncBN
+        self._flat = None
+
+    # ------------------------------------------------------------ native glue
+    def desc(self) -> _lib.ModelDesc:
+        d = self._dims
+        desc = _lib.ModelDesc()
+        desc.n_users = d['n_users']
+        desc.n_items = d['n_items']
+        desc.n_cat = len(d['cat_dims'])
+        desc.cat_rows = ctypes.cast(self._cat_rows, ctypes.POINTER(ctypes.c_int64))
+        desc.emb_dim = d['emb_dim']
+        desc.n_num = d['n_num']
+        desc.hidden = d['hidden']
+        desc.n_cross = d['n_cross']
+        desc.n_res = d['n_res']
+        desc.dropout = d['dropout']
+        desc.precision = _PRECISIONS[self.precision]
+        desc.flags = _lib.FLAG_CHECK_INDICES if self.check_indices else 0
+        if self.bn_allreduce is not None:
+            desc.bn_allreduce = self.bn_allreduce
+        return desc
+
+    def state_tensors(self) -> List[torch.Tensor]:
+        """All state_dict tensors in state_dict order (params + BN buffers)."""
+        return [t for t in self.state_dict(keep_vars=True).values()]
+
+    def param_tensors(self) -> List[torch.Tensor]:
+        return [p for _, p in self.named_parameters()]
+
+    def workspace_bytes(self, B: int, mode: int) -> int:
+        lib = _lib.load()
+        n = ctypes.c_size_t(0)
+        desc = self.desc()
+        _lib.check(lib.dcnr_workspace_size(ctypes.byref(desc), int(B), int(mode), ctypes.byref(n)),
+                   "dcnr_workspace_size")
+        return int(n.value)
+
+    def _check_device(self, *tensors):
+        dev = self.final_linear.weight.device
+        if dev.type != 'cuda':
+            raise RuntimeError("dcnr.DCN_RecSys runs on the HIP device only (libdcnr, gfx950); "
+                               "move the model to 'cuda' -- there is no CPU path")
+        for t in tensors:
+            if t.device != dev:
+                raise RuntimeError(f"input on {t.device} but model on {dev}")
+        for t in self.state_tensors():
+            if t.dtype not in (torch.float32, torch.int64) or not t.is_contiguous():
+                raise RuntimeError("dcnr requires fp32 contiguous parameters")
+        return dev
+
+    def forward(self, user_ids, item_ids, cat_features, num_features):
+        dev = self._check_device(user_ids, item_ids, cat_features, num_features)
+        user_ids = user_ids.reshape(-1).to(torch.int64).contiguous()
+        item_ids = item_ids.reshape(-1).to(torch.int64).contiguous()
+        B = user_ids.shape[0]
+        K, F = len(self._dims['cat_dims']), self._dims['n_num']
+        if cat_features.numel() != B * K or num_features.numel() != B * F or \
+                item_ids.shape[0] != B:
+            raise RuntimeError("input shapes do not match the model")
+        cat_features = cat_features.to(torch.int64).reshape(B, K).contiguous()
+        num_features = num_features.to(torch.float32).reshape(B, F).contiguous()
+        train = self.training
+        if train and B == 1:
+            raise ValueError("Expected more than 1 value per channel when training, "
+                             "got input size torch.Size([1, %d])" % self._dims['hidden'])
+        params = self.param_tensors()
+        needs_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if train else 0
+        if needs_grad:
+            logits = _DCNRFunction.apply(self, train, seed, user_ids, item_ids, cat_features,
+                                         num_features, *params)
+        else:
+            logits, _ = run_forward(self, train, seed, user_ids, item_ids, cat_features,
+                                    num_features)
+        return logits.squeeze()
+
+    # ----------------------------------------------------------- flat storage
+    def flatten_(self):
+        """Move every parameter into one contiguous fp32 buffer (views keep the
+        state_dict API) and give each a ``.grad`` view into one flat gradient
+        buffer: lets the fused optimizer and the DP all-reduce run as single
+        launches.  Returns (flat_params, flat_grads)."""
+        params = self.param_tensors()
+        dev = params[0].device
+        sizes = [((p.numel() + 63) // 64) * 64 for p in params]
+        total = sum(sizes)
+        flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        gflat = torch.zeros(total, dtype=torch.float32, device=dev)
+        off = 0
+        for p, sz in zip(params, sizes):
+            n = p.numel()
+            flat[off:off + n].copy_(p.detach().reshape(-1))
+            p.data = flat[off:off + n].view_as(p)
+            p.grad = gflat[off:off + n].view_as(p)
+            off += sz
+        self._flat = (flat, gflat)
+        return flat, gflat
+
+
+def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
+                ws: Optional[torch.Tensor] = None):
+    lib = _lib.load()
+    B = user.shape[0]
+    dev = user.device
+    mode = _lib.TRAIN if train else _lib.EVAL
+    nbytes = model.workspace_bytes(B, mode)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    logits = torch.empty(B, dtype=torch.float32, device=dev)
+    state = _lib.ptr_array(model.state_tensors())
+    desc = model.desc()
+    st = lib.dcnr_forward(ctypes.byref(desc), state, user.data_ptr(), item.data_ptr(),
+                          cat.data_ptr() if cat.numel() else None,
+                          num.data_ptr() if num.numel() else None, B, mode, seed,
+                          logits.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev))
+    _lib.check(st, "dcnr_forward")
+    if model.check_indices:
+        _lib.check(lib.dcnr_check_errors(ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)),
+                   "embedding")
+    return logits, ws
+
+
+def run_backward(model: DCN_RecSys, user, item, cat, num, dlogits, ws, grads: List[torch.Tensor],
+                 accumulate=False):
+    lib = _lib.load()
+    B = user.shape[0]
+    desc = model.desc()
+    st = lib.dcnr_backward(ctypes.byref(desc), _lib.ptr_array(model.state_tensors()),
+                           _lib.ptr_array(grads), user.data_ptr(), item.data_ptr(),
+                           cat.data_ptr() if cat.numel() else None,
+                           num.data_ptr() if num.numel() else None, B,
+                           dlogits.data_ptr(), 1 if accumulate else 0, ws.data_ptr(), ws.numel(),
+                           _lib.stream_ptr(user.device))
+    _lib.check(st, "dcnr_backward")
+
+
+class _DCNRFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, train, seed, user, item, cat, num, *params):
+        logits, ws = run_forward(model, train, seed, user, item, cat, num)
+        ctx.model = model
+        ctx.train = train
+        ctx.ws = ws
+        ctx.save_for_backward(user, item, cat, num)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        if not ctx.train:
+            raise NotImplementedError("dcnr: backward through an eval-mode forward is not "
+                                      "supported (call model.train() for training)")
+        user, item, cat, num = ctx.saved_tensors
+        model = ctx.model
+        params = model.param_tensors()
+        grads = [torch.empty_like(p) for p in params]
+        dl = dlogits.reshape(-1).to(torch.float32).contiguous()
+        run_backward(model, user, item, cat, num, dl, ctx.ws, grads)
+        ctx.ws = None
+        out = [g if p.requires_grad else None for g, p in zip(grads, params)]
+        return (None, None, None, None, None, None, None, *out)

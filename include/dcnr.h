@@ -1,0 +1,171 @@
+/*
+ * dcnr.h -- C ABI of libdcnr.so, the MI355X (gfx950) DCN-R ranking hot path.
+ *
+ * Drop-in boundary for the reference's DCN-R path.  The reference
+ * (Krist-Marrakesh/Hybrid-Hotel-Recommendation-System-Based-on-Friends-
+ * Recommendations) has no FFI of its own: its boundary is the PyTorch module
+ * DCN_RecSys and its callers.  Each entry point below replaces one reference
+ * interface (file:line in the reference repository):
+ *
+ *   dcnr_forward          DCN_RecSys.forward            train.py:155-170 (dup main.py:114-127)
+ *                         incl. ResBlock.forward          train.py:112-122
+ *                         and CrossLayer.forward          train.py:96-99
+ *   dcnr_backward         loss.backward() through the model   train.py:225
+ *   dcnr_bce_with_logits  nn.BCEWithLogitsLoss()(preds, y)    train.py:206,224,233,376
+ *   dcnr_adam_step        torch.optim.AdamW/Adam(...).step()  train.py:201-204,226
+ *   dcnr_cosine_topk      NearestNeighbors(metric='cosine', algorithm='brute')
+ *                         .kneighbors(vec, n_neighbors=k)      main.py:196-203,268-270,300
+ *   dcnr_row_inv_norms    the row normalisation inside sklearn's cosine metric
+ *
+ * Conventions
+ *  - All tensor pointers are DEVICE pointers owned by the caller; the
+ *    library allocates nothing on the hot path (workspace is caller-owned,
+ *    size from dcnr_workspace_size / dcnr_cosine_topk_workspace_size).
+ *  - Parameter tables are HOST arrays of device pointers:
+ *      params: in the reference's state_dict() order (train.py:136-153):
+ *        user_embedding.weight, item_embedding.weight,
+ *        cat_embeddings.{k}.weight (k < n_cat),
+ *        initial_deep_layer.weight [H,D], initial_deep_layer.bias [H],
+ *        for j < n_res: res_blocks.{j}.{layer1.weight, layer1.bias,
+ *            bn1.weight, bn1.bias, bn1.running_mean, bn1.running_var,
+ *            bn1.num_batches_tracked (int64 scalar), layer2.weight,
+ *            layer2.bias, bn2.weight, bn2.bias, bn2.running_mean,
+ *            bn2.running_var, bn2.num_batches_tracked},
+ *        for l < n_cross: cross_network.{l}.b [D], cross_network.{l}.w.weight [1,D],
+ *        final_linear.weight [1,H+D], final_linear.bias [1]
+ *      grads: in named_parameters() order (the same list without the BN
+ *        running_mean / running_var / num_batches_tracked buffers).
+ *    Every floating tensor is fp32, contiguous, row-major.
+ *  - Index tensors are int64 (torch.long) like the reference; indices are
+ *    clamped in-kernel (never an out-of-bounds access) and, with
+ *    DCNR_FLAG_CHECK_INDICES, an out-of-range index is reported as
+ *    DCNR_INDEX_OOB by dcnr_check_errors (torch raises IndexError there).
+ *  - Everything is stream-ordered and asynchronous on `stream` (a
+ *    hipStream_t); functions return after enqueueing.  No entry point
+ *    synchronises except dcnr_check_errors.
+ *  - Status codes are returned, never thrown or aborted across the ABI;
+ *    dcnr_last_error() gives a thread-local message for the last failure.
+ *  - Eval-mode forward is re-entrant (no shared scratch); train-mode forward
+ *    mutates BN running statistics and must be serialised by the caller.
+ */
+#ifndef DCNR_H
+#define DCNR_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DCNR_ABI_VERSION 1
+
+typedef void* dcnr_stream_t; /* hipStream_t */
+
+typedef enum {
+  DCNR_OK = 0,
+  DCNR_BAD_ARG = 1,
+  DCNR_INDEX_OOB = 2,
+  DCNR_HIP_ERROR = 3,
+  DCNR_UNSUPPORTED_SHAPE = 4,
+  DCNR_WORKSPACE_TOO_SMALL = 5
+} dcnr_status;
+
+typedef enum { DCNR_PREC_FP32 = 0, DCNR_PREC_BF16 = 1 } dcnr_precision;
+typedef enum { DCNR_EVAL = 0, DCNR_TRAIN = 1 } dcnr_mode;
+
+#define DCNR_FLAG_CHECK_INDICES 1u
+
+/* Optional collective hook for SyncBN across data-parallel ranks: called
+ * (stream-ordered, from the calling thread) with a device buffer of `count`
+ * fp64 values that must be summed over all ranks in place before the call
+ * returns or is stream-ordered before later work on `stream`.  NULL = local
+ * BN (each rank normalises with its own batch statistics). */
+typedef int (*dcnr_allreduce_fn)(void* ctx, double* device_buf, int64_t count, dcnr_stream_t stream);
+
+typedef struct {
+  int64_t n_users;          /* user_embedding rows      (train.py:136) */
+  int64_t n_items;          /* item_embedding rows      (train.py:137) */
+  int32_t n_cat;            /* number of categorical tables (len(cat_dims)) */
+  const int64_t* cat_rows;  /* HOST array [n_cat]: cat_dims.values() (train.py:138-139) */
+  int32_t emb_dim;          /* params['emb_dim'] */
+  int32_t n_num;            /* n_num_features */
+  int32_t hidden;           /* params['hidden_dim'] */
+  int32_t n_cross;          /* params['n_cross_layers'] */
+  int32_t n_res;            /* params.get('n_res_blocks', 2) */
+  float dropout;            /* params['dropout'] (applied in train mode only) */
+  int32_t precision;        /* dcnr_precision of the deep-tower GEMMs/activations */
+  uint32_t flags;           /* DCNR_FLAG_* */
+  dcnr_allreduce_fn bn_allreduce; /* SyncBN hook or NULL */
+  void* bn_allreduce_ctx;
+} dcnr_model_desc;
+
+int dcnr_abi_version(void);
+const char* dcnr_last_error(void);
+
+/* Input dim D = 2*emb_dim + sum(int(sqrt(n_cat_k))+1) + n_num (train.py:139-141). */
+int64_t dcnr_input_dim(const dcnr_model_desc* desc);
+
+/* Workspace bytes for a batch of B in `mode`.  A train-mode workspace holds
+ * the saved activations that dcnr_backward consumes. */
+dcnr_status dcnr_workspace_size(const dcnr_model_desc* desc, int64_t B, int mode, size_t* bytes);
+
+/* DCN_RecSys.forward: logits[B] (fp32, device).  mode = DCNR_TRAIN uses
+ * batch statistics (B >= 2), updates BN running stats and
+ * num_batches_tracked in `params`, applies dropout with `dropout_seed`, and
+ * keeps the activations backward needs in `ws`. */
+dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
+                         const int64_t* user_ids, const int64_t* item_ids,
+                         const int64_t* cat_features /* [B,n_cat] */,
+                         const float* num_features /* [B,n_num] */, int64_t B, int mode,
+                         uint64_t dropout_seed, float* logits, void* ws, size_t ws_bytes,
+                         dcnr_stream_t stream);
+
+/* Backward of the last train-mode dcnr_forward on `ws`: given dL/dlogits
+ * [B], writes dL/dparam for every parameter into `grads`.  accumulate = 0
+ * overwrites (embedding grads are zeroed first, then scatter-added, i.e.
+ * embedding_dense_backward semantics); accumulate = 1 adds into grads. */
+dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void* const* grads,
+                          const int64_t* user_ids, const int64_t* item_ids,
+                          const int64_t* cat_features, const float* num_features, int64_t B,
+                          const float* dlogits, int accumulate, void* ws, size_t ws_bytes,
+                          dcnr_stream_t stream);
+
+size_t dcnr_bce_workspace_size(void);
+
+/* BCEWithLogitsLoss (mean): loss[0] = mean(max(z,0) - z*y + log1p(exp(-|z|)));
+ * if dlogits != NULL also writes dlogits = grad_scale * (sigmoid(z) - y) / B.
+ * Deterministic (fixed-order fp64 reduction through `ws`). */
+dcnr_status dcnr_bce_with_logits(const float* logits, const float* labels, int64_t B,
+                                 float* loss, float* dlogits, float grad_scale, void* ws,
+                                 size_t ws_bytes, dcnr_stream_t stream);
+
+/* One torch.optim.AdamW (decoupled = 1) or Adam (decoupled = 0) step over
+ * n_tensors tensors (host arrays of device pointers + element counts).
+ * `step` is the 1-based step number after increment (torch's state['step']). */
+dcnr_status dcnr_adam_step(int32_t n_tensors, float* const* params, const float* const* grads,
+                           float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
+                           float lr, float beta1, float beta2, float eps, float weight_decay,
+                           int64_t step, int decoupled, dcnr_stream_t stream);
+
+/* 1/||row|| for each row of table [N,d] (0-norm rows -> 1, as sklearn's normalize). */
+dcnr_status dcnr_row_inv_norms(const float* table, int64_t N, int32_t d, float* inv_norms,
+                               dcnr_stream_t stream);
+
+size_t dcnr_cosine_topk_workspace_size(int64_t N, int64_t Q, int32_t k);
+
+/* k nearest rows of `table` [N,d] to each query [Q,d] by cosine distance
+ * dist = clip(1 - <q/|q|, x/|x|>, 0, 2) (fp32), ascending; ties by lower
+ * row index.  idx int64 [Q,k], dist fp32 [Q,k].  1 <= k <= 64. */
+dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t N, int32_t d,
+                             const float* queries, int64_t Q, int32_t k, int64_t* idx,
+                             float* dist, void* ws, size_t ws_bytes, dcnr_stream_t stream);
+
+/* Synchronises `stream` and reports kernel-side errors recorded in ws
+ * (DCNR_INDEX_OOB when DCNR_FLAG_CHECK_INDICES saw an out-of-range id). */
+dcnr_status dcnr_check_errors(void* ws, size_t ws_bytes, dcnr_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DCNR_H */

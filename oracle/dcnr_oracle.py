@@ -1,0 +1,301 @@
+"""CPU oracle for the DCN-R ranking hot path -- TEST INFRASTRUCTURE ONLY.
+
+This module is a plain-numpy restatement of the reference algorithm, used as
+the *checker* in ``tests/``, ``__graft_entry__.smoke()`` and the
+``cpu_baseline`` leg of ``bench.py``.  Nothing in the product path
+(``dcnr`` package, ``libdcnr.so``) imports, calls or links it; the product
+path fails loudly when the HIP library is missing.
+
+Parity pinning: this restatement is pinned against golden vectors produced by
+importing the reference itself in the build container
+(``tests/golden/make_golden.py`` -> ``tests/golden/*.npz``; checked by
+``tests/test_oracle_golden.py``).
+
+Every function cites the reference lines it restates (paths relative to the
+reference repository root):
+
+* ``train.py:136-141``  table widths ``int(np.sqrt(n_cat)) + 1`` and input dim
+* ``train.py:155-170``  ``DCN_RecSys.forward`` (gathers, concat order, deep
+  tower, cross stack, ``cat([deep, cross])``, final linear, squeeze)
+* ``train.py:96-99``    ``CrossLayer.forward``: ``x + x*(x.w) + b`` (uses the
+  *current* layer input, not x0)
+* ``train.py:112-122``  ``ResBlock.forward``: L1 -> BN1 -> ReLU -> Dropout ->
+  L2 -> BN2 -> += identity -> ReLU
+* ``train.py:206,224``  ``BCEWithLogitsLoss`` (mean reduction)
+* ``train.py:201-204,226`` ``torch.optim.AdamW`` / ``Adam`` single step
+* ``main.py:268-270,300`` sklearn ``NearestNeighbors(metric='cosine',
+  algorithm='brute').kneighbors`` (third party: scikit-learn 1.7.2,
+  ``sklearn/metrics/pairwise.py`` cosine_distances and
+  ``sklearn/neighbors/_base.py`` ``_kneighbors_reduce_func``: argpartition
+  then argsort)
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+BN_EPS = 1e-5          # nn.BatchNorm1d default eps (train.py:106,110)
+BN_MOMENTUM = 0.1      # nn.BatchNorm1d default momentum
+
+
+def cat_width(n_cat: int) -> int:
+    """Categorical table width rule, train.py:139-140."""
+    return int(np.sqrt(n_cat)) + 1
+
+
+def input_dim(emb_dim: int, cat_dims: Sequence[int], n_num: int) -> int:
+    """train.py:140-141."""
+    return emb_dim * 2 + sum(cat_width(n) for n in cat_dims) + n_num
+
+
+@dataclass
+class ModelSpec:
+    n_users: int
+    n_items: int
+    cat_dims: List[int]
+    n_num: int
+    emb_dim: int
+    hidden: int
+    n_cross: int
+    n_res: int
+    dropout: float = 0.0
+
+    @property
+    def D(self) -> int:
+        return input_dim(self.emb_dim, self.cat_dims, self.n_num)
+
+
+def spec_from_params(n_users, n_items, cat_dims: Dict[str, int], n_num, params) -> ModelSpec:
+    """Mirror of the ctor argument handling at train.py:126-134."""
+    return ModelSpec(n_users, n_items, list(cat_dims.values()), n_num,
+                     params['emb_dim'], params['hidden_dim'], params['n_cross_layers'],
+                     params.get('n_res_blocks', 2), params['dropout'])
+
+
+# --------------------------------------------------------------------------
+# forward
+# --------------------------------------------------------------------------
+@dataclass
+class Cache:
+    x0: np.ndarray = None
+    h_in: List[np.ndarray] = field(default_factory=list)     # block inputs
+    t1: List[np.ndarray] = field(default_factory=list)
+    xh1: List[np.ndarray] = field(default_factory=list)
+    r1: List[np.ndarray] = field(default_factory=list)
+    a1: List[np.ndarray] = field(default_factory=list)
+    t2: List[np.ndarray] = field(default_factory=list)
+    xh2: List[np.ndarray] = field(default_factory=list)
+    u: List[np.ndarray] = field(default_factory=list)
+    inv1: List[np.ndarray] = field(default_factory=list)
+    inv2: List[np.ndarray] = field(default_factory=list)
+    masks: List[Optional[np.ndarray]] = field(default_factory=list)
+    h_out: np.ndarray = None
+    xs: List[np.ndarray] = field(default_factory=list)        # cross inputs x_l
+    ss: List[np.ndarray] = field(default_factory=list)        # s_l = x_l . w_l
+    xL: np.ndarray = None
+    train: bool = False
+    B: int = 0
+
+
+def _bn(t, p, prefix, train, dt):
+    """nn.BatchNorm1d forward (train: biased batch var for normalisation,
+    running stats updated with momentum 0.1 and the unbiased var)."""
+    g = p[prefix + '.weight'].astype(dt)
+    b = p[prefix + '.bias'].astype(dt)
+    if train:
+        mu = t.mean(axis=0)
+        var = t.var(axis=0)  # biased
+        n = t.shape[0]
+        rm = p[prefix + '.running_mean']
+        rv = p[prefix + '.running_var']
+        p[prefix + '.running_mean'] = ((1 - BN_MOMENTUM) * rm + BN_MOMENTUM * mu).astype(rm.dtype)
+        p[prefix + '.running_var'] = ((1 - BN_MOMENTUM) * rv + BN_MOMENTUM * var * n / (n - 1)).astype(rv.dtype)
+        p[prefix + '.num_batches_tracked'] = np.asarray(p[prefix + '.num_batches_tracked']) + 1
+    else:
+        mu = p[prefix + '.running_mean'].astype(dt)
+        var = p[prefix + '.running_var'].astype(dt)
+    inv = (1.0 / np.sqrt(var + BN_EPS)).astype(dt)
+    xh = (t - mu) * inv
+    return xh * g + b, xh, inv
+
+
+def gather_x0(p, spec: ModelSpec, user, item, cat, num, dt=np.float64):
+    """Embedding gathers + concat, train.py:156-159 (bit-exact in fp32)."""
+    parts = [p['user_embedding.weight'][user], p['item_embedding.weight'][item]]
+    for k in range(len(spec.cat_dims)):
+        parts.append(p[f'cat_embeddings.{k}.weight'][cat[:, k]])
+    parts.append(num)
+    return np.concatenate([np.asarray(a, dtype=dt) for a in parts], axis=1)
+
+
+def cross_layer(x, w, b):
+    """CrossLayer.forward, train.py:96-99: x + x*(x.w) + b."""
+    s = x @ w
+    return x + x * s[:, None] + b, s
+
+
+def forward(p: Dict[str, np.ndarray], spec: ModelSpec, user, item, cat, num, train=False,
+            dropout_masks: Optional[List[np.ndarray]] = None, dt=np.float64):
+    """DCN_RecSys.forward (train.py:155-170).  ``p`` is a dict of numpy
+    arrays keyed like the reference state_dict; in train mode the BN running
+    statistics in ``p`` are updated in place (as nn.BatchNorm1d does).
+    Returns (logits[B], cache)."""
+    if train and user.shape[0] == 1:
+        raise ValueError("Expected more than 1 value per channel when training")
+    c = Cache(train=train, B=user.shape[0])
+    W = lambda k: np.asarray(p[k], dtype=dt)
+    x0 = gather_x0(p, spec, user, item, cat, num, dt)
+    c.x0 = x0
+    h = x0 @ W('initial_deep_layer.weight').T + W('initial_deep_layer.bias')
+    pdrop = spec.dropout if train else 0.0
+    for j in range(spec.n_res):
+        pre = f'res_blocks.{j}'
+        c.h_in.append(h)
+        t1 = h @ W(pre + '.layer1.weight').T + W(pre + '.layer1.bias')
+        r1, xh1, inv1 = _bn(t1, p, pre + '.bn1', train, dt)
+        a1 = np.maximum(r1, 0)
+        m = None
+        if pdrop > 0:
+            m = dropout_masks[j].astype(dt) / (1.0 - pdrop)
+            a1 = a1 * m
+        t2 = a1 @ W(pre + '.layer2.weight').T + W(pre + '.layer2.bias')
+        r2, xh2, inv2 = _bn(t2, p, pre + '.bn2', train, dt)
+        u = r2 + h
+        h = np.maximum(u, 0)
+        for lst, v in ((c.t1, t1), (c.xh1, xh1), (c.r1, r1), (c.a1, a1), (c.t2, t2),
+                       (c.xh2, xh2), (c.u, u), (c.inv1, inv1), (c.inv2, inv2), (c.masks, m)):
+            lst.append(v)
+    c.h_out = h
+    x = x0
+    for l in range(spec.n_cross):
+        c.xs.append(x)
+        x, s = cross_layer(x, W(f'cross_network.{l}.w.weight')[0], W(f'cross_network.{l}.b'))
+        c.ss.append(s)
+    c.xL = x
+    fin = np.concatenate([h, x], axis=1)            # deep first (train.py:169)
+    z = fin @ W('final_linear.weight')[0] + W('final_linear.bias')[0]
+    return z, c
+
+
+def bce_with_logits(z, y):
+    """BCEWithLogitsLoss (mean), train.py:206/224; returns (loss, dL/dz)."""
+    z = np.asarray(z, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    loss = np.mean(np.maximum(z, 0) - z * y + np.log1p(np.exp(-np.abs(z))))
+    dz = (1.0 / (1.0 + np.exp(-z)) - y) / z.shape[0]
+    return loss, dz
+
+
+def backward(p, spec: ModelSpec, c: Cache, dz, user, item, cat, dt=np.float64):
+    """Autograd backward of forward() (loss.backward(), train.py:225).
+    Returns dict name -> grad, embedding grads dense (embedding_dense_backward)."""
+    W = lambda k: np.asarray(p[k], dtype=dt)
+    g = {}
+    dz = np.asarray(dz, dtype=dt)
+    H = spec.hidden
+    wf = W('final_linear.weight')[0]
+    g['final_linear.weight'] = (np.concatenate([c.h_out, c.xL], axis=1).T @ dz)[None, :]
+    g['final_linear.bias'] = np.array([dz.sum()], dtype=dt)
+    dh = dz[:, None] * wf[:H][None, :]
+    dx = dz[:, None] * wf[H:][None, :]
+    # cross stack (reverse)
+    for l in reversed(range(spec.n_cross)):
+        xl, s = c.xs[l], c.ss[l]
+        wl = W(f'cross_network.{l}.w.weight')[0]
+        g[f'cross_network.{l}.b'] = dx.sum(axis=0)
+        gx = (dx * xl).sum(axis=1)
+        g[f'cross_network.{l}.w.weight'] = (gx[:, None] * xl).sum(axis=0)[None, :]
+        dx = dx * (1.0 + s)[:, None] + gx[:, None] * wl[None, :]
+    dx0_cross = dx
+    B = c.B
+
+    def bn_back(dr, xh, inv, prefix):
+        gam = W(prefix + '.weight')
+        g[prefix + '.weight'] = (dr * xh).sum(axis=0)
+        g[prefix + '.bias'] = dr.sum(axis=0)
+        if c.train:
+            return gam * inv / B * (B * dr - dr.sum(axis=0) - xh * (dr * xh).sum(axis=0))
+        return dr * gam * inv
+
+    for j in reversed(range(spec.n_res)):
+        pre = f'res_blocks.{j}'
+        du = dh * (c.u[j] > 0)
+        dh_in = du.copy()
+        dt2 = bn_back(du, c.xh2[j], c.inv2[j], pre + '.bn2')
+        g[pre + '.layer2.weight'] = dt2.T @ c.a1[j]
+        g[pre + '.layer2.bias'] = dt2.sum(axis=0)
+        da = dt2 @ W(pre + '.layer2.weight')
+        if c.masks[j] is not None:
+            da = da * c.masks[j]
+        dr1 = da * (c.r1[j] > 0)
+        dt1 = bn_back(dr1, c.xh1[j], c.inv1[j], pre + '.bn1')
+        g[pre + '.layer1.weight'] = dt1.T @ c.h_in[j]
+        g[pre + '.layer1.bias'] = dt1.sum(axis=0)
+        dh = dh_in + dt1 @ W(pre + '.layer1.weight')
+    g['initial_deep_layer.weight'] = dh.T @ c.x0
+    g['initial_deep_layer.bias'] = dh.sum(axis=0)
+    dx0 = dh @ W('initial_deep_layer.weight') + dx0_cross
+    # embedding_dense_backward: scatter-add slices of dx0
+    e = spec.emb_dim
+    off = 0
+
+    def scatter(name, idx, width):
+        nonlocal off
+        gt = np.zeros(np.asarray(p[name]).shape, dtype=dt)
+        np.add.at(gt, idx, dx0[:, off:off + width])
+        off += width
+        g[name] = gt
+
+    scatter('user_embedding.weight', user, e)
+    scatter('item_embedding.weight', item, e)
+    for k, n in enumerate(spec.cat_dims):
+        scatter(f'cat_embeddings.{k}.weight', cat[:, k], cat_width(n))
+    return g
+
+
+# --------------------------------------------------------------------------
+# optimizer (train.py:201-204, 226)
+# --------------------------------------------------------------------------
+def adam_step(param, grad, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8,
+              weight_decay=0.0, decoupled=True):
+    """One torch.optim.AdamW (decoupled=True) / Adam (decoupled=False) step,
+    single-tensor algorithm; returns new (param, m, v).  ``step`` is the
+    1-based step count after increment."""
+    param = param.astype(np.float64)
+    grad = grad.astype(np.float64)
+    if decoupled:
+        param = param * (1 - lr * weight_decay)
+    elif weight_decay != 0:
+        grad = grad + weight_decay * param
+    m = beta1 * m + (1 - beta1) * grad
+    v = beta2 * v + (1 - beta2) * grad * grad
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    denom = np.sqrt(v) / math.sqrt(bc2) + eps
+    param = param - (lr / bc1) * m / denom
+    return param, m, v
+
+
+# --------------------------------------------------------------------------
+# candidate generation: cosine kNN (main.py:268-270, 196-203, 299-302)
+# --------------------------------------------------------------------------
+def cosine_kneighbors(table: np.ndarray, queries: np.ndarray, k: int):
+    """sklearn NearestNeighbors(metric='cosine', algorithm='brute').kneighbors
+    restated: normalise rows, dist = clip(1 - q.x, 0, 2) (fp32), then
+    argpartition(k-1) + argsort.  Ties are ordered by index here (stable),
+    where sklearn's argsort is unstable; tests compare modulo ties."""
+    t = np.asarray(table, dtype=np.float32)
+    q = np.asarray(queries, dtype=np.float32)
+
+    def normalize(a):
+        n = np.sqrt(np.einsum('ij,ij->i', a, a))
+        n[n == 0.0] = 1.0
+        return a / n[:, None]
+
+    s = normalize(q) @ normalize(t).T
+    d = np.clip(1.0 - s, 0.0, 2.0).astype(np.float32)
+    idx = np.argsort(d, axis=1, kind='stable')[:, :k]
+    return np.take_along_axis(d, idx, axis=1), idx

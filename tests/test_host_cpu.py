@@ -1,0 +1,81 @@
+"""CPU-only tests of the host side: the C-ABI library loads and exports every
+symbol include/dcnr.h declares (no compute calls), shape/workspace queries,
+module construction parity with the reference (state_dict keys, shapes and
+initial weights), and loud failure without a HIP device."""
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+import golden_common as gc
+from conftest import ROOT, golden
+from helpers import check_checksums, our_model
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "dcnr.h")).read()
+    return sorted(set(re.findall(r"\b(dcnr_[a-z0-9_]+)\s*\(", txt)) - {"dcnr_allreduce_fn"})
+
+
+def test_library_exports_header_symbols():
+    from dcnr import _lib
+    lib = _lib.load()
+    syms = header_symbols()
+    assert len(syms) >= 12
+    for s in syms:
+        assert hasattr(lib, s), f"libdcnr.so does not export {s}"
+    assert sorted(_lib.exported_symbols()) == syms
+    assert lib.dcnr_abi_version() == 1
+
+
+def test_input_dim_and_workspace_queries():
+    import dcnr
+    m = our_model(gc.CFG3R)
+    lib = dcnr._lib.load()
+    import ctypes
+    desc = m.desc()
+    assert lib.dcnr_input_dim(ctypes.byref(desc)) == 456
+    ev = m.workspace_bytes(131072, 0)
+    tr = m.workspace_bytes(131072, 1)
+    assert 0 < ev < tr
+    # train workspace holds >= 3 activations per res block + x0 (bf16 halves it)
+    mb = our_model(gc.CFG3R, precision="bf16")
+    assert mb.workspace_bytes(131072, 1) < tr
+
+
+@pytest.mark.parametrize("fname,cfg", [("f1_cfg1_eval.npz", gc.CFG1), ("f3_cfg3r_train.npz", gc.CFG3R),
+                                       ("f3b_odd_train.npz", gc.CFG_ODD)])
+def test_same_init_and_state_dict_as_reference(fname, cfg):
+    check_checksums(our_model(cfg), golden(fname))
+
+
+def test_width_rule_matches_reference():
+    import dcnr
+    fx = golden("f5_width_rule.npz")
+    for n, w in zip(fx["n"], fx["width"]):
+        m = dcnr.DCN_RecSys(3, 3, {"a": int(n)}, 1, dict(emb_dim=4, hidden_dim=8, n_cross_layers=1,
+                                                          n_res_blocks=1, dropout=0.0))
+        assert m.cat_embeddings[0].weight.shape[1] == w
+        import ctypes
+        desc = m.desc()
+        assert m._dims["input_dim"] == 8 + w + 1
+        assert dcnr._lib.load().dcnr_input_dim(ctypes.byref(desc)) == 8 + w + 1
+
+
+def test_cpu_model_raises():
+    import dcnr
+    cfg = gc.CFG_ODD
+    m = dcnr.DCN_RecSys(cfg["n_users"], cfg["n_items"], cfg["cat_dims"], cfg["n_num"],
+                        dict(cfg["params"]))
+    u, i, c, n, _ = gc.make_inputs(cfg, 4, 3)
+    with pytest.raises(RuntimeError):
+        m(*[torch.from_numpy(a) for a in (u, i, c, n)])
+
+
+def test_bad_precision_rejected():
+    import dcnr
+    with pytest.raises(ValueError):
+        dcnr.DCN_RecSys(3, 3, {}, 1, dict(emb_dim=4, hidden_dim=8, n_cross_layers=1, dropout=0.0),
+                        precision="fp8")
