@@ -1,0 +1,239 @@
+#!/usr/bin/env python
+"""bench.py -- DCN-R training step on MI355X (BASELINE.json configs[2] / [3]).
+
+One step = one pass of the hot path over one synthetic batch per GPU:
+    forward (train-mode BN, dropout 0.6) -> BCEWithLogits -> backward
+    -> [RCCL all-reduce of the flat gradient when N > 1] -> fused AdamW
+Workload (BASELINE.json configs[2]): 1M users x 100k hotels, 12 categorical
+tables of 1000 rows (width 32), 8 dense features, emb_dim 32, 3 cross layers,
+4 x 512 residual deep tower, batch 131072 per GPU, bf16 MFMA deep tower with
+fp32 accumulation / fp32 master weights.  N > 1 is configs[3] (data parallel,
+weak scaling: per-GPU batch fixed).  Inputs are pre-generated on the device
+(fresh ids every step from a pool), weights seed 42, inputs seed 0 (+rank).
+
+Run: python bench.py [--gpus N --steps K --warmup W]; N > 1 under
+torch.distributed.run (one process per GPU, RCCL).
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd")
+sys.path.insert(0, PKG)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+CFG = dict(n_users=1_000_000, n_items=100_000, cat_dims={f"c{k}": 1000 for k in range(12)},
+           n_num=8, params=dict(emb_dim=32, hidden_dim=512, n_cross_layers=3, n_res_blocks=4,
+                                dropout=0.6))
+D, H, R = 456, 512, 4
+GEMM_FLOP = {  # algorithmic FLOPs per sample per step (13.98 MFLOP fwd+bwd)
+    "gemm_fwd": 2 * (D * H + 2 * R * H * H),
+    "gemm_dx": 2 * (2 * R * H * H + H * D),
+    "gemm_dw": 2 * (2 * R * H * H + H * D),
+}
+# gather + x0 + 3 cross: 14 idx x 8 B + 14 rows x 128 B + 8 x 4 B read; x0 bf16 + zc written
+GATHER_BYTES = 14 * 8 + 14 * 32 * 4 + 8 * 4 + D * 2 + 4
+PEAK_BF16 = 2.5e15     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM = 8.0e12
+
+
+def make_batch(gen, B, dev):
+    ids = lambda n: torch.randint(0, n, (B,), generator=gen, device=dev, dtype=torch.int64)
+    user = ids(CFG["n_users"])
+    item = ids(CFG["n_items"])
+    cat = torch.randint(0, 1000, (B, 12), generator=gen, device=dev, dtype=torch.int64)
+    num = torch.rand((B, 8), generator=gen, device=dev, dtype=torch.float32)
+    y = (torch.rand((B,), generator=gen, device=dev) < 0.5).float()
+    return user, item, cat, num, y
+
+
+def cpu_baseline(B_cpu=8192, steps=2):
+    """The oracle (numpy fp32 restatement of train.py:155-226) timed on the
+    host: forward + BCE + backward + AdamW on a bounded sample of the same
+    workload.  Reported only; not the optimisation target."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import dcnr_oracle as orc
+    import dcnr
+    torch.manual_seed(42)
+    m = dcnr.DCN_RecSys(CFG["n_users"], CFG["n_items"], CFG["cat_dims"], CFG["n_num"],
+                        dict(CFG["params"], dropout=0.0))
+    sd = {k: v.detach().numpy().astype(np.float32) for k, v in m.state_dict().items()}
+    del m
+    spec = orc.spec_from_params(CFG["n_users"], CFG["n_items"], CFG["cat_dims"], CFG["n_num"],
+                                dict(CFG["params"], dropout=0.0))
+    rng = np.random.default_rng(0)
+    names = [k for k in sd if "running" not in k and "num_batches" not in k]
+    mom = {k: (np.zeros_like(sd[k]), np.zeros_like(sd[k])) for k in names}
+    t0 = time.perf_counter()
+    for s in range(steps):
+        u = rng.integers(0, CFG["n_users"], B_cpu)
+        i = rng.integers(0, CFG["n_items"], B_cpu)
+        c = rng.integers(0, 1000, (B_cpu, 12))
+        n = rng.random((B_cpu, 8), dtype=np.float32)
+        y = (rng.random(B_cpu) < 0.5).astype(np.float32)
+        z, cache = orc.forward(sd, spec, u, i, c, n, train=True, dt=np.float32)
+        _, dz = orc.bce_with_logits(z, y)
+        g = orc.backward(sd, spec, cache, dz.astype(np.float32), u, i, c, dt=np.float32)
+        for k in names:
+            p, mm, vv = orc.adam_step(sd[k], g[k], *mom[k], s + 1, 1e-3, weight_decay=1e-4)
+            sd[k] = p.astype(np.float32)
+            mom[k] = (mm, vv)
+    el = time.perf_counter() - t0
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": steps * B_cpu / el, "unit": "samples/s", "cores": cores, "kind": "port",
+            "sample": f"{steps} train steps (fwd+BCE+bwd+AdamW) at batch {B_cpu} of the same "
+                      f"model/tables, numpy fp32 oracle, {el:.1f} s"}
+
+
+def pmc_traffic(kernel_class):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        return json.load(open(p)).get(kernel_class)
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=131072)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--pool", type=int, default=8)
+    ap.add_argument("--eval-steps", type=int, default=10)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    import dcnr
+    from dcnr import _lib
+
+    B = args.batch
+    torch.manual_seed(42)
+    model = dcnr.DCN_RecSys(CFG["n_users"], CFG["n_items"], CFG["cat_dims"], CFG["n_num"],
+                            dict(CFG["params"]), precision=args.precision).to(dev)
+    trainer = dcnr.FusedTrainer(model, lr=1e-3, weight_decay=1e-4, optimizer_name="AdamW")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 * rank)
+    pool = [make_batch(gen, B, dev) for _ in range(max(1, args.pool))]
+
+    for k in range(args.warmup):
+        trainer.step(*pool[k % len(pool)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    _lib.profile_enable(True)
+    _lib.profile_collect()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        loss = trainer.step(*pool[k % len(pool)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    _lib.profile_enable(False)
+    prof = _lib.profile_collect()
+    el_t = torch.tensor([el], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+    el = float(el_t.item())
+    final_loss = float(loss.item())
+
+    # scored pairs/s: eval-mode forward (running-stat BN, no dropout) per GPU
+    model.eval()
+    with torch.no_grad():
+        for k in range(2):
+            model(*pool[k % len(pool)][:4])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for k in range(args.eval_steps):
+            model(*pool[k % len(pool)][:4])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        ev = torch.tensor([time.perf_counter() - t1], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(ev, op=dist.ReduceOp.MAX)
+    pairs_per_s = world * B * args.eval_steps / float(ev.item())
+
+    if rank == 0:
+        samples = world * B * args.steps
+        per_step_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1]}
+        launches = {k: v[1] / args.steps for k, v in prof.items() if v[1]}
+        gemm_cls = max(GEMM_FLOP, key=lambda k: prof[k][0])
+        ms, cnt = prof[gemm_cls]
+        flop_launch = GEMM_FLOP[gemm_cls] * B * args.steps / cnt
+        achieved = flop_launch / (ms / cnt / 1e3) / 1e12
+        g_ms, g_cnt = prof["gather_cross"]
+        gather_gbs = GATHER_BYTES * B * args.steps / g_cnt / (g_ms / g_cnt / 1e3) / 1e9
+        traffic = pmc_traffic(gemm_cls)
+        out = {
+            "metric": "fwd+bwd samples/sec (DCN-R train step) + scored (user,hotel) pairs/sec",
+            "value": samples / el,
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": args.precision,
+            "data": "synthetic (uniform ids, U[0,1) dense, Bernoulli labels; weights seed 42, "
+                    "torch default init)",
+            "config": {"workload": "DCN-R train step: fwd (train BN, dropout 0.6) + BCE + bwd + "
+                                   "AdamW (+grad all-reduce), BASELINE configs[2]/[3]",
+                       "batch_per_gpu": B, "global_batch": world * B,
+                       "tables": "1M x 32 users, 100k x 32 hotels, 12 x 1000 x 32 cat, 8 dense",
+                       "deep": "3 cross + 4 x 512 residual", "parallelism": f"dp{world}"},
+            "scored_pairs_per_sec": pairs_per_s,
+            "final_loss": final_loss,
+            "roofline": {"bound": "mfma", "kernel": gemm_cls, "achieved": achieved / 1.0,
+                         "peak": PEAK_BF16 / 1e12 if args.precision == "bf16" else 157.3,
+                         "unit": "TFLOP/s",
+                         "frac": achieved / ((PEAK_BF16 / 1e12) if args.precision == "bf16"
+                                             else 157.3),
+                         "traffic": traffic,
+                         "flop_per_launch": flop_launch,
+                         "avg_launch_ms": ms / cnt},
+            "roofline_gather": {"bound": "hbm", "kernel": "gather_cross", "achieved": gather_gbs,
+                                "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                                "frac": gather_gbs / (PEAK_HBM / 1e9),
+                                "bytes_per_sample": GATHER_BYTES, "avg_launch_ms": g_ms / g_cnt},
+            "kernel_ms_per_step": per_step_ms,
+            "kernel_launches_per_step": launches,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

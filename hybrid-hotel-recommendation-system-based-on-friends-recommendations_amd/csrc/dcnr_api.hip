@@ -16,6 +16,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 namespace dcnr {
@@ -29,10 +30,50 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+
+// ------------------------------------------------------------ profiling
+// Optional per-launch HIP-event timing by kernel class (dcnr_profile_*).
+struct ProfRec { int cat; hipEvent_t a, b; };
+static std::mutex g_pm;
+static bool g_prof = false;
+static std::vector<ProfRec> g_recs;
+static std::vector<hipEvent_t> g_pool;
+
+static hipEvent_t prof_event() {
+  if (!g_pool.empty()) { hipEvent_t e = g_pool.back(); g_pool.pop_back(); return e; }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+struct ProfScope {
+  int cat; hipStream_t s; hipEvent_t a = nullptr;
+  ProfScope(int c, hipStream_t st) : cat(c), s(st) {
+    if (!g_prof) return;
+    std::lock_guard<std::mutex> lk(g_pm);
+    a = prof_event();
+    (void)hipEventRecord(a, s);
+  }
+  ~ProfScope() {
+    if (!a) return;
+    std::lock_guard<std::mutex> lk(g_pm);
+    hipEvent_t b = prof_event();
+    (void)hipEventRecord(b, s);
+    g_recs.push_back(ProfRec{cat, a, b});
+  }
+};
+
 namespace {
 
 #define TRY(x)                       \
   do {                               \
+    dcnr_status st_ = (x);           \
+    if (st_ != DCNR_OK) return st_;  \
+  } while (0)
+// TRY with the launch attributed to a kernel class (stream `s` in scope)
+#define TRYP(cat, x)                 \
+  do {                               \
+    ProfScope ps_(cat, s);           \
     dcnr_status st_ = (x);           \
     if (st_ != DCNR_OK) return st_;  \
   } while (0)
@@ -299,13 +340,13 @@ dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train
     PackBatch pb;
     pb.n = (int)std::min<size_t>(MAX_PACK, v.size() - o);
     for (int i = 0; i < pb.n; ++i) pb.d[i] = v[o + i];
-    TRY(pack_weights(d.prec, pb, s));
+    TRYP(DCNR_K_PACK, pack_weights(d.prec, pb, s));
   }
   for (size_t o = 0; o < vb.size(); o += MAX_PACK) {
     PackBatch pb;
     pb.n = (int)std::min<size_t>(MAX_PACK, vb.size() - o);
     for (int i = 0; i < pb.n; ++i) pb.d[i] = vb[o + i];
-    TRY(pack_weights(DCNR_PREC_FP32, pb, s));
+    TRYP(DCNR_K_PACK, pack_weights(DCNR_PREC_FP32, pb, s));
   }
   return DCNR_OK;
 }
@@ -338,8 +379,9 @@ dcnr_status linear_dw(const Dims& d, const Layout& L, const void* dY, int ldy, i
   g.A = dY; g.lda = ldy; g.B = X; g.ldb = ldx;
   g.C = L.slab; g.ldc = Kc;
   g.M = N; g.N = Kc; g.K = B; g.k_per_split = kps; g.slab_stride = (int64_t)N * Kc;
-  TRY(gemm(d.prec, true, true, EPI_SPLITK, g, (int)S, s));
-  return splitk_reduce(L.slab, (int)S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s);
+  TRYP(DCNR_K_GEMM_DW, gemm(d.prec, true, true, EPI_SPLITK, g, (int)S, s));
+  TRYP(DCNR_K_REDUCE, splitk_reduce(L.slab, (int)S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s));
+  return DCNR_OK;
 }
 
 dcnr_status hook(const dcnr_model_desc* desc, const Dims& d, const Layout& L, hipStream_t s) {
@@ -359,11 +401,12 @@ dcnr_status bn_layer_fwd(const dcnr_model_desc* desc, const Dims& d, const Layou
   BnFinal f{gamma, beta, rm, rv, nbt, bb.scale, bb.shift, bb.mean, bb.invstd};
   if (train) {
     int nc = 0;
-    TRY(col_stats(d.prec, t, B, d.Hp, d.Hp, L.part, &nc, s));
-    TRY(reduce_partials_nk(L.part, nc, 2, d.Hp, L.sums, (double)B, s));
+    TRYP(DCNR_K_ROWWISE, col_stats(d.prec, t, B, d.Hp, d.Hp, L.part, &nc, s));
+    TRYP(DCNR_K_REDUCE, reduce_stats(d.prec, L.part, nc, d.Hp, L.sums, (double)B, t, s));
     TRY(hook(desc, d, L, s));
   }
-  return bn_finalize2(L.sums, d.Hp, d.H, train ? 1 : 0, f, s);
+  TRYP(DCNR_K_REDUCE, bn_finalize2(L.sums, d.Hp, d.H, train ? 1 : 0, f, s));
+  return DCNR_OK;
 }
 
 }  // namespace
@@ -417,35 +460,35 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   Params P = map_params(d, params);
   TRY(pack_all(d, P, L, train, s));
   const int check = (desc->flags & DCNR_FLAG_CHECK_INDICES) ? 1 : 0;
-  if (check) TRY(fill_zero(L.err, 4, s));
+  if (check) TRYP(DCNR_K_PACK, fill_zero(L.err, 4, s));
   GatherDesc g = make_gather(d, P, desc->n_num);
   CrossParams cp = make_cross(d, P);
-  TRY(gather_cross_fwd(d.prec, g, cp, user_ids, item_ids, cat_features, num_features, B, L.x0,
+  TRYP(DCNR_K_GATHER_CROSS, gather_cross_fwd(d.prec, g, cp, user_ids, item_ids, cat_features, num_features, B, L.x0,
                        d.Dp, L.zc, L.err, check, s));
-  TRY(linear_fwd(d, L.x0, d.Dp, L.W0p, d.Dp, L.b0p, L.h[0], B, s));
+  TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.x0, d.Dp, L.W0p, d.Dp, L.b0p, L.h[0], B, s));
   const float p = train ? d.dropout : 0.f;
   for (int j = 0; j < d.R; ++j) {
     const auto& Bk = P.blk[j];
-    TRY(linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
+    TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
     TRY(bn_layer_fwd(desc, d, L, L.t1[j], B, train, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
                      L.bn[2 * j], s));
-    TRY(bn_relu_drop(d.prec, L.t1[j], L.a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
+    TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], L.a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
                      dropout_seed, j, s));
-    TRY(linear_fwd(d, L.a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
+    TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
     TRY(bn_layer_fwd(desc, d, L, L.t2[j], B, train, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
                      L.bn[2 * j + 1], s));
-    TRY(bn_add_relu2(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp, L.bn[2 * j + 1].scale,
+    TRYP(DCNR_K_ROWWISE, bn_add_relu2(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp, L.bn[2 * j + 1].scale,
                      L.bn[2 * j + 1].shift, s));
   }
-  TRY(row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
-  TRY(head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
+  TRYP(DCNR_K_HEAD, row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
+  TRYP(DCNR_K_HEAD, head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
   return DCNR_OK;
 }
 
 dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void* const* grads,
                           const int64_t* user_ids, const int64_t* item_ids,
                           const int64_t* cat_features, const float* num_features, int64_t B,
-                          const float* dlogits, int accumulate, void* ws, size_t ws_bytes,
+                          const float* dlogits, uint64_t dropout_seed, int accumulate, void* ws, size_t ws_bytes,
                           dcnr_stream_t stream) {
   Dims d;
   TRY(make_dims(desc, &d));
@@ -466,7 +509,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   const float p = d.dropout;
   if (!accumulate)
     for (int t = 0; t < 2 + d.K; ++t)
-      TRY(fill_zero(Gr.tab[t], (size_t)d.rows[t] * d.widths[t] * 4, s));
+      TRYP(DCNR_K_PACK, fill_zero(Gr.tab[t], (size_t)d.rows[t] * d.widths[t] * 4, s));
 
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   for (int j = d.R - 1; j >= 0; --j) {
@@ -476,40 +519,40 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     const BnBufs& bn2 = L.bn[2 * j + 1];
     int nc = 0;
     // ---- out = relu(BN2(t2) + h_j):  du, BN2 backward
-    TRY(bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, B, Hp,
+    TRYP(DCNR_K_ROWWISE, bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, B, Hp,
                        Hp, L.part, &nc, s));
-    TRY(reduce_partials_nk(L.part, nc, 3, Hp, L.sums, (double)B, s));
-    if (!Gin) TRY(sums_to_grad(L.sums + 2 * Hp, H, Gr.wf, accumulate, s));  // dW_f[:H]
-    TRY(sums_to_grad(L.sums + Hp, H, Gk.g2, accumulate, s));               // dgamma2
-    TRY(sums_to_grad(L.sums, H, Gk.be2, accumulate, s));                   // dbeta2
+    TRYP(DCNR_K_REDUCE, reduce_partials_nk(L.part, nc, 3, Hp, L.sums, (double)B, s));
+    if (!Gin) TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums + 2 * Hp, H, Gr.wf, accumulate, s));  // dW_f[:H]
+    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums + Hp, H, Gk.g2, accumulate, s));               // dgamma2
+    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, Gk.be2, accumulate, s));                   // dbeta2
     TRY(hook(desc, d, L, s));
-    TRY(bn_bwd_coef(L.sums, Hp, H, Bk.g2, bn2.invstd, L.coef, 1, s));
-    TRY(bwd_bn2_apply2(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, L.coef,
+    TRYP(DCNR_K_REDUCE, bn_bwd_coef(L.sums, Hp, H, Bk.g2, bn2.invstd, L.coef, 1, s));
+    TRYP(DCNR_K_ROWWISE, bwd_bn2_apply2(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, L.coef,
                        B, Hp, Hp, L.dt2, L.du, L.part, &nc, s));
-    TRY(reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
-    TRY(sums_to_grad(L.sums, H, Gk.b2, accumulate, s));                    // dbias2
+    TRYP(DCNR_K_REDUCE, reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
+    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, Gk.b2, accumulate, s));                    // dbias2
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
-    TRY(bn_relu_drop(d.prec, L.t1[j], L.a1, B, Hp, Hp, bn1.scale, bn1.shift, p, 0, j, s));
+    TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], L.a1, B, Hp, Hp, bn1.scale, bn1.shift, p, dropout_seed, j, s));
     TRY(linear_dw(d, L, L.dt2, Hp, Hp, L.a1, Hp, Hp, B, Gk.w2, H, H, accumulate, s));
     {
       GemmArgs g;
       memset(&g, 0, sizeof(g));
       g.A = L.dt2; g.lda = Hp; g.B = L.W2t[j]; g.ldb = Hp; g.C = L.da; g.ldc = Hp;
       g.M = B; g.N = Hp; g.K = Hp; g.k_per_split = Hp;
-      TRY(gemm(d.prec, false, false, EPI_STORE, g, 1, s));
+      TRYP(DCNR_K_GEMM_DX, gemm(d.prec, false, false, EPI_STORE, g, 1, s));
     }
     // ---- relu/dropout + BN1 backward
-    TRY(bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean, bn1.invstd, B, Hp, Hp,
-                      p, 0, j, L.part, &nc, s));
-    TRY(reduce_partials_nk(L.part, nc, 2, Hp, L.sums, (double)B, s));
-    TRY(sums_to_grad(L.sums + Hp, H, Gk.g1, accumulate, s));
-    TRY(sums_to_grad(L.sums, H, Gk.be1, accumulate, s));
+    TRYP(DCNR_K_ROWWISE, bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean, bn1.invstd, B, Hp, Hp,
+                      p, dropout_seed, j, L.part, &nc, s));
+    TRYP(DCNR_K_REDUCE, reduce_partials_nk(L.part, nc, 2, Hp, L.sums, (double)B, s));
+    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums + Hp, H, Gk.g1, accumulate, s));
+    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, Gk.be1, accumulate, s));
     TRY(hook(desc, d, L, s));
-    TRY(bn_bwd_coef(L.sums, Hp, H, Bk.g1, bn1.invstd, L.coef, 1, s));
-    TRY(bwd_bn1_apply2(d.prec, L.da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, L.a1,
+    TRYP(DCNR_K_REDUCE, bn_bwd_coef(L.sums, Hp, H, Bk.g1, bn1.invstd, L.coef, 1, s));
+    TRYP(DCNR_K_ROWWISE, bwd_bn1_apply2(d.prec, L.da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, L.a1,
                        L.part, &nc, s));
-    TRY(reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
-    TRY(sums_to_grad(L.sums, H, Gk.b1, accumulate, s));
+    TRYP(DCNR_K_REDUCE, reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
+    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, Gk.b1, accumulate, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
     TRY(linear_dw(d, L, L.a1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s));
     {
@@ -518,22 +561,22 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       g.A = L.a1; g.lda = Hp; g.B = L.W1t[j]; g.ldb = Hp; g.C = L.G; g.ldc = Hp;
       g.resid = L.du; g.ldr = Hp;
       g.M = B; g.N = Hp; g.K = Hp; g.k_per_split = Hp;
-      TRY(gemm(d.prec, false, false, EPI_STORE_RESID, g, 1, s));
+      TRYP(DCNR_K_GEMM_DX, gemm(d.prec, false, false, EPI_STORE_RESID, g, 1, s));
     }
     Gin = L.G;
   }
   // ---- initial layer
   int nc = 0;
-  TRY(col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
-  TRY(reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
-  TRY(sums_to_grad(L.sums, H, Gr.b0, accumulate, s));
+  TRYP(DCNR_K_ROWWISE, col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
+  TRYP(DCNR_K_REDUCE, reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
+  TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, Gr.b0, accumulate, s));
   TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s));
   {
     GemmArgs g;
     memset(&g, 0, sizeof(g));
     g.A = L.G; g.lda = Hp; g.B = L.W0t; g.ldb = Hp; g.C = L.dx0; g.ldc = d.Dp; g.out_f32 = 1;
     g.M = B; g.N = d.Dp; g.K = Hp; g.k_per_split = Hp;
-    TRY(gemm(d.prec, false, false, EPI_STORE, g, 1, s));
+    TRYP(DCNR_K_GEMM_DX, gemm(d.prec, false, false, EPI_STORE, g, 1, s));
   }
   // ---- cross stack + head bias + embedding scatter
   GatherDesc g = make_gather(d, P, desc->n_num);
@@ -544,7 +587,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   cb.dwf_cross = Gr.wf + H;
   cb.dbf = Gr.bf;
   for (int t = 0; t < 2 + d.K; ++t) cb.emb_grad[t] = Gr.tab[t];
-  TRY(cross_bwd_scatter(g, cb, user_ids, item_ids, cat_features, num_features, dz, B, L.dx0, d.Dp,
+  TRYP(DCNR_K_CROSS_BWD, cross_bwd_scatter(g, cb, user_ids, item_ids, cat_features, num_features, dz, B, L.dx0, d.Dp,
                         L.cpart, L.cpart_elems, accumulate, s));
   return DCNR_OK;
 }
@@ -562,7 +605,9 @@ dcnr_status dcnr_bce_with_logits(const float* logits, const float* labels, int64
     set_error("dcnr_bce_with_logits: workspace too small");
     return DCNR_WORKSPACE_TOO_SMALL;
   }
-  return bce(logits, labels, B, loss, dlogits, grad_scale, (double*)ws, (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  TRYP(DCNR_K_HEAD, bce(logits, labels, B, loss, dlogits, grad_scale, (double*)ws, s));
+  return DCNR_OK;
 }
 
 dcnr_status dcnr_adam_step(int32_t n_tensors, float* const* params, const float* const* grads,
@@ -574,8 +619,10 @@ dcnr_status dcnr_adam_step(int32_t n_tensors, float* const* params, const float*
     set_error("dcnr_adam_step: bad argument");
     return DCNR_BAD_ARG;
   }
-  return adam(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, lr, beta1, beta2, eps,
-              weight_decay, step, decoupled, (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  TRYP(DCNR_K_ADAM, adam(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, lr, beta1, beta2,
+                         eps, weight_decay, step, decoupled, s));
+  return DCNR_OK;
 }
 
 dcnr_status dcnr_row_inv_norms(const float* table, int64_t N, int32_t d, float* inv_norms,
@@ -603,8 +650,38 @@ dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t
               k, (long long)N);
     return DCNR_BAD_ARG;
   }
-  return cosine_topk(table, inv_norms, N, d, queries, Q, k, idx, dist, ws, ws_bytes,
-                     (hipStream_t)stream);
+  hipStream_t s = (hipStream_t)stream;
+  TRYP(DCNR_K_KNN, cosine_topk(table, inv_norms, N, d, queries, Q, k, idx, dist, ws, ws_bytes, s));
+  return DCNR_OK;
+}
+
+void dcnr_profile_enable(int on) {
+  std::lock_guard<std::mutex> lk(g_pm);
+  g_prof = on != 0;
+}
+
+dcnr_status dcnr_profile_collect(double* ms, int64_t* launches, int32_t n) {
+  std::vector<ProfRec> recs;
+  {
+    std::lock_guard<std::mutex> lk(g_pm);
+    recs.swap(g_recs);
+  }
+  for (int i = 0; i < n; ++i) { if (ms) ms[i] = 0.0; if (launches) launches[i] = 0; }
+  dcnr_status st = DCNR_OK;
+  for (auto& r : recs) {
+    float t = 0.f;
+    if (hipEventSynchronize(r.b) != hipSuccess || hipEventElapsedTime(&t, r.a, r.b) != hipSuccess) {
+      set_error("profile: event query failed");
+      st = DCNR_HIP_ERROR;
+    }
+    if (r.cat >= 0 && r.cat < n) {
+      if (ms) ms[r.cat] += t;
+      if (launches) launches[r.cat] += 1;
+    }
+  }
+  std::lock_guard<std::mutex> lk(g_pm);
+  for (auto& r : recs) { g_pool.push_back(r.a); g_pool.push_back(r.b); }
+  return st;
 }
 
 dcnr_status dcnr_check_errors(void* ws, size_t ws_bytes, dcnr_stream_t stream) {

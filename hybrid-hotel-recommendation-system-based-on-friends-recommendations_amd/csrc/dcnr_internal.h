@@ -147,6 +147,10 @@ dcnr_status col_sum(int precision, const void* x, int64_t B, int N, int ld, floa
                     int* nchunks, hipStream_t s);                    // NK=1
 dcnr_status reduce_partials_nk(const float* part, int nchunks, int NK, int N, double* sums,
                                double count, hipStream_t s);
+// BN batch statistics: col_stats partials are shifted by K = t[0][n]; this
+// reduces them and converts to unshifted fp64 [sum t, sum t^2] + count.
+dcnr_status reduce_stats(int precision, const float* part, int nchunks, int N, double* sums,
+                         double count, const void* t, hipStream_t s);
 
 struct BnFinal {   // per BN layer
   const float* gamma; const float* beta; float* rmean; float* rvar; int64_t* nbt;

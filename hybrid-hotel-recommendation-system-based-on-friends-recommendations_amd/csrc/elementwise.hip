@@ -1,11 +1,15 @@
 // Row-major [B][ld] activation kernels of the deep tower: BatchNorm statistics,
-// BN/ReLU/dropout application, residual add, and their backward; all HBM
-// streaming with 16-byte accesses (8 bf16 or 4 fp32 per thread), column
-// partial sums reduced deterministically (fixed order, fp64) -- no atomics.
+// BN/ReLU/dropout application, residual add, and their backward.  All are HBM
+// streams with 16-byte accesses (8 bf16 or 4 fp32 per thread), U rows in
+// flight per thread (loads for U rows issued before any use), per-column
+// constants held in registers, and column partial sums reduced
+// deterministically (fixed order, fp64) -- no atomics.
 //
 // Reference semantics: ResBlock.forward (train.py:112-122), nn.BatchNorm1d
 // (train: biased batch var for normalisation, running stats with momentum 0.1
 // and unbiased var; eval: running stats), nn.ReLU, nn.Dropout.
+// Batch variance is computed from sums shifted by the batch's first row
+// (K = t[0]), so var = E[(t-K)^2] - E[t-K]^2 does not cancel when |mean| >> std.
 #include "dcnr_internal.h"
 
 #include <cmath>
@@ -15,8 +19,10 @@ namespace dcnr {
 namespace {
 
 constexpr int NT = 256;
+constexpr int UNROLL = 4;
 constexpr float BN_EPS = 1e-5f;
 constexpr double BN_MOM = 0.1;
+constexpr int TARGET_CHUNKS = 2048;  // 8 blocks/CU in flight for HBM latency hiding
 
 template <typename T> constexpr int VE = 16 / (int)sizeof(T);
 
@@ -45,32 +51,48 @@ __device__ __forceinline__ void stv(T* p, const float (&o)[VE<T>]) {
   }
   *reinterpret_cast<uint4*>(p) = u;
 }
+template <int V>
+__device__ __forceinline__ void ldc(const float* p, float (&o)[V]) {
+#pragma unroll
+  for (int v = 0; v < V; ++v) o[v] = p[v];
+}
 
-struct Geo {            // thread -> (row sub-index, column group)
-  int tcols, rpp, rsub, cg;
-  __device__ Geo(int N, int V) {
-    tcols = (N + V - 1) / V;
-    rpp = NT / tcols;
-    rsub = threadIdx.x / tcols;
-    cg = threadIdx.x % tcols;
-  }
-};
-
-// Generic row x column-group driver with NK per-column partial sums per chunk.
+// Generic row x column-group driver.  Each thread owns V consecutive columns
+// (c0 = cg*V) and walks rows rsub, rsub+rpp, ... of its block's chunk, U rows
+// per step (all loads first).  NK > 0: per-column partial sums per chunk.
 template <typename T, int NK, class Op>
 __global__ __launch_bounds__(NT) void rowcol_kernel(Op op, int64_t B, int N, int rows_per_chunk,
                                                     float* part) {
   constexpr int V = VE<T>;
-  Geo g(N, V);
-  float acc[NK > 0 ? NK : 1][V];
+  constexpr int NKA = NK > 0 ? NK : 1;
+  const int tcols = (N + V - 1) / V;
+  const int rpp = NT / tcols;
+  const int rsub = threadIdx.x / tcols, cg = threadIdx.x % tcols;
+  const int c0 = cg * V;
+  float acc[NKA][V];
 #pragma unroll
-  for (int k = 0; k < (NK > 0 ? NK : 1); ++k)
+  for (int k = 0; k < NKA; ++k)
 #pragma unroll
     for (int v = 0; v < V; ++v) acc[k][v] = 0.f;
   const int64_t r0 = (int64_t)blockIdx.x * rows_per_chunk;
   const int64_t r1 = min(B, r0 + rows_per_chunk);
-  if (g.rsub < g.rpp)
-    for (int64_t r = r0 + g.rsub; r < r1; r += g.rpp) op(r, g.cg * V, acc);
+  if (rsub < rpp) {
+    typename Op::Cst cst;
+    op.prep(c0, cst);
+    for (int64_t r = r0 + rsub; r < r1; r += (int64_t)UNROLL * rpp) {
+      typename Op::Reg q[UNROLL];
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        int64_t rr = r + (int64_t)u * rpp;
+        if (rr < r1) op.load(rr, c0, q[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        int64_t rr = r + (int64_t)u * rpp;
+        if (rr < r1) op.apply(rr, c0, cst, q[u], acc);
+      }
+    }
+  }
   if constexpr (NK > 0) {
     __shared__ float red[NT * NK * V];
 #pragma unroll
@@ -78,13 +100,13 @@ __global__ __launch_bounds__(NT) void rowcol_kernel(Op op, int64_t B, int N, int
 #pragma unroll
       for (int v = 0; v < V; ++v) red[(threadIdx.x * NK + k) * V + v] = acc[k][v];
     __syncthreads();
-    if (g.rsub == 0) {
+    if (rsub == 0) {
       for (int k = 0; k < NK; ++k)
         for (int v = 0; v < V; ++v) {
-          int c = g.cg * V + v;
+          int c = c0 + v;
           if (c >= N) continue;
           float s = 0.f;
-          for (int rs = 0; rs < g.rpp; ++rs) s += red[((rs * g.tcols + g.cg) * NK + k) * V + v];
+          for (int rs = 0; rs < rpp; ++rs) s += red[((rs * tcols + cg) * NK + k) * V + v];
           part[((int64_t)blockIdx.x * NK + k) * N + c] = s;
         }
     }
@@ -98,8 +120,7 @@ dcnr_status run_rowcol(const Op& op, int64_t B, int N, float* part, int* nchunks
     set_error("rowcol: unsupported width %d", N);
     return DCNR_UNSUPPORTED_SHAPE;
   }
-  int64_t want = 2048;
-  int rows = (int)std::max<int64_t>(16, cdiv(B, want));
+  int rows = (int)std::max<int64_t>(32, cdiv(B, TARGET_CHUNKS));
   int nc = (int)cdiv(B, rows);
   if (nchunks) *nchunks = nc;
   if (B <= 0) return DCNR_OK;
@@ -108,99 +129,133 @@ dcnr_status run_rowcol(const Op& op, int64_t B, int N, float* part, int* nchunks
   return DCNR_OK;
 }
 
+struct NoCst {};
+
 // ---------------------------------------------------------------- ops
-template <typename T> struct StatsOp {   // sum t, sum t^2
+// sums of (t-K) and (t-K)^2 with K = t[0] (the batch's first row)
+template <typename T> struct StatsOp {
   const T* t; int ld;
-  __device__ void operator()(int64_t r, int c, float (&acc)[2][VE<T>]) const {
-    float x[VE<T>]; ldv<T>(t + r * ld + c, x);
+  struct Cst { float k[VE<T>]; };
+  struct Reg { float x[VE<T>]; };
+  __device__ void prep(int c, Cst& q) const { ldv<T>(t + c, q.k); }
+  __device__ void load(int64_t r, int c, Reg& q) const { ldv<T>(t + r * ld + c, q.x); }
+  __device__ void apply(int64_t, int, const Cst& k, Reg& q, float (&acc)[2][VE<T>]) const {
 #pragma unroll
-    for (int v = 0; v < VE<T>; ++v) { acc[0][v] += x[v]; acc[1][v] += x[v] * x[v]; }
+    for (int v = 0; v < VE<T>; ++v) {
+      float d = q.x[v] - k.k[v];
+      acc[0][v] += d;
+      acc[1][v] += d * d;
+    }
   }
 };
 
 template <typename T> struct ColSumOp {
   const T* x; int ld;
-  __device__ void operator()(int64_t r, int c, float (&acc)[1][VE<T>]) const {
-    float a[VE<T>]; ldv<T>(x + r * ld + c, a);
+  typedef NoCst Cst;
+  struct Reg { float a[VE<T>]; };
+  __device__ void prep(int, Cst&) const {}
+  __device__ void load(int64_t r, int c, Reg& q) const { ldv<T>(x + r * ld + c, q.a); }
+  __device__ void apply(int64_t, int, const Cst&, Reg& q, float (&acc)[1][VE<T>]) const {
 #pragma unroll
-    for (int v = 0; v < VE<T>; ++v) acc[0][v] += a[v];
+    for (int v = 0; v < VE<T>; ++v) acc[0][v] += q.a[v];
   }
 };
 
 template <typename T> struct BnReluDropOp {  // a = dropout(relu(t*sc+sh))
   const T* t; T* a; int ld; const float* sc; const float* sh;
   float inv_keep; uint32_t thresh; uint64_t seed; int layer; int drop;
-  __device__ void operator()(int64_t r, int c, float (&)[1][VE<T>]) const {
-    float x[VE<T>]; ldv<T>(t + r * ld + c, x);
+  struct Cst { float sc[VE<T>], sh[VE<T>]; };
+  struct Reg { float x[VE<T>]; };
+  __device__ void prep(int c, Cst& q) const { ldc(sc + c, q.sc); ldc(sh + c, q.sh); }
+  __device__ void load(int64_t r, int c, Reg& q) const { ldv<T>(t + r * ld + c, q.x); }
+  __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&)[1][VE<T>]) const {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      float y = fmaxf(x[v] * sc[c + v] + sh[c + v], 0.f);
+      float y = fmaxf(q.x[v] * k.sc[v] + k.sh[v], 0.f);
       if (drop) y = dropout_keep(seed, layer, r, c + v, thresh) ? y * inv_keep : 0.f;
-      x[v] = y;
+      q.x[v] = y;
     }
-    stv<T>(a + r * ld + c, x);
+    stv<T>(a + r * ld + c, q.x);
   }
 };
 
 template <typename T> struct BnAddReluOp {   // out = relu(t*sc+sh + x)
   const T* t; const T* x; T* out; int ld; const float* sc; const float* sh;
-  __device__ void operator()(int64_t r, int c, float (&)[1][VE<T>]) const {
-    float a[VE<T>], b[VE<T>]; ldv<T>(t + r * ld + c, a); ldv<T>(x + r * ld + c, b);
+  struct Cst { float sc[VE<T>], sh[VE<T>]; };
+  struct Reg { float a[VE<T>], b[VE<T>]; };
+  __device__ void prep(int c, Cst& q) const { ldc(sc + c, q.sc); ldc(sh + c, q.sh); }
+  __device__ void load(int64_t r, int c, Reg& q) const {
+    ldv<T>(t + r * ld + c, q.a);
+    ldv<T>(x + r * ld + c, q.b);
+  }
+  __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&)[1][VE<T>]) const {
 #pragma unroll
-    for (int v = 0; v < VE<T>; ++v) a[v] = fmaxf(a[v] * sc[c + v] + sh[c + v] + b[v], 0.f);
-    stv<T>(out + r * ld + c, a);
+    for (int v = 0; v < VE<T>; ++v) q.a[v] = fmaxf(q.a[v] * k.sc[v] + k.sh[v] + q.b[v], 0.f);
+    stv<T>(out + r * ld + c, q.a);
   }
 };
 
-// backward of out = relu(BN2(t2) + x): du = g*[out>0]
+// backward of out = relu(BN2(t2) + x): du = g*[out>0]; g = G or dz (x) wf
 template <typename T> struct Bwd2StatsOp {
   const T* G; const float* dz; const float* wf; const T* out; const T* t;
   const float* mean; const float* invstd; int ld;
-  __device__ void operator()(int64_t r, int c, float (&acc)[3][VE<T>]) const {
-    float o[VE<T>], tt[VE<T>], g[VE<T>];
-    ldv<T>(out + r * ld + c, o); ldv<T>(t + r * ld + c, tt);
-    if (G) ldv<T>(G + r * ld + c, g);
-    else {
-      float d = dz[r];
-#pragma unroll
-      for (int v = 0; v < VE<T>; ++v) g[v] = d * wf[c + v];
-    }
+  struct Cst { float wf[VE<T>], mu[VE<T>], is[VE<T>]; };
+  struct Reg { float o[VE<T>], t[VE<T>], g[VE<T>]; float d; };
+  __device__ void prep(int c, Cst& q) const {
+    if (!G) ldc(wf + c, q.wf);
+    ldc(mean + c, q.mu); ldc(invstd + c, q.is);
+  }
+  __device__ void load(int64_t r, int c, Reg& q) const {
+    ldv<T>(out + r * ld + c, q.o);
+    ldv<T>(t + r * ld + c, q.t);
+    if (G) ldv<T>(G + r * ld + c, q.g);
+    else q.d = dz[r];
+  }
+  __device__ void apply(int64_t, int, const Cst& k, Reg& q, float (&acc)[3][VE<T>]) const {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      float du = o[v] > 0.f ? g[v] : 0.f;
-      float xh = (tt[v] - mean[c + v]) * invstd[c + v];
+      float g = G ? q.g[v] : q.d * k.wf[v];
+      float du = q.o[v] > 0.f ? g : 0.f;
+      float xh = (q.t[v] - k.mu[v]) * k.is[v];
       acc[0][v] += du;
       acc[1][v] += du * xh;
-      if (!G) acc[2][v] += dz[r] * o[v];
+      if (!G) acc[2][v] += q.d * q.o[v];
     }
   }
 };
 
-// dt = kA*du - kB*xh - kC ; writes dt, du ; partial sum of dt (bias grad)
+// dt = c0*du - c1*xh - c2 ; writes dt, du ; partial sum of dt (bias grad)
 template <typename T> struct Bwd2ApplyOp {
   const T* G; const float* dz; const float* wf; const T* out; const T* t;
   const float* mean; const float* invstd; const float* coef; int ld, N;
   T* dt; T* du_out;
-  __device__ void operator()(int64_t r, int c, float (&acc)[1][VE<T>]) const {
-    float o[VE<T>], tt[VE<T>], g[VE<T>], d[VE<T>];
-    ldv<T>(out + r * ld + c, o); ldv<T>(t + r * ld + c, tt);
-    if (G) ldv<T>(G + r * ld + c, g);
-    else {
-      float dd = dz[r];
-#pragma unroll
-      for (int v = 0; v < VE<T>; ++v) g[v] = dd * wf[c + v];
-    }
+  struct Cst { float wf[VE<T>], mu[VE<T>], is[VE<T>], k0[VE<T>], k1[VE<T>], k2[VE<T>]; };
+  struct Reg { float o[VE<T>], t[VE<T>], g[VE<T>]; float d; };
+  __device__ void prep(int c, Cst& q) const {
+    if (!G) ldc(wf + c, q.wf);
+    ldc(mean + c, q.mu); ldc(invstd + c, q.is);
+    ldc(coef + c, q.k0); ldc(coef + N + c, q.k1); ldc(coef + 2 * N + c, q.k2);
+  }
+  __device__ void load(int64_t r, int c, Reg& q) const {
+    ldv<T>(out + r * ld + c, q.o);
+    ldv<T>(t + r * ld + c, q.t);
+    if (G) ldv<T>(G + r * ld + c, q.g);
+    else q.d = dz[r];
+  }
+  __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[1][VE<T>]) const {
+    float d[VE<T>];
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      float du = o[v] > 0.f ? g[v] : 0.f;
-      float xh = (tt[v] - mean[c + v]) * invstd[c + v];
-      float y = coef[c + v] * du - coef[N + c + v] * xh - coef[2 * N + c + v];
-      g[v] = du;
+      float g = G ? q.g[v] : q.d * k.wf[v];
+      float du = q.o[v] > 0.f ? g : 0.f;
+      float xh = (q.t[v] - k.mu[v]) * k.is[v];
+      float y = k.k0[v] * du - k.k1[v] * xh - k.k2[v];
+      q.g[v] = du;
       d[v] = y;
       acc[0][v] += y;
     }
     stv<T>(dt + r * ld + c, d);
-    stv<T>(du_out + r * ld + c, g);
+    stv<T>(du_out + r * ld + c, q.g);
   }
 };
 
@@ -208,53 +263,95 @@ template <typename T> struct Bwd2ApplyOp {
 template <typename T> struct Bwd1StatsOp {
   T* da; const T* t; const float* sc; const float* sh; const float* mean; const float* invstd;
   int ld; float inv_keep; uint32_t thresh; uint64_t seed; int layer; int drop;
-  __device__ void operator()(int64_t r, int c, float (&acc)[2][VE<T>]) const {
-    float a[VE<T>], tt[VE<T>];
-    ldv<T>(da + r * ld + c, a); ldv<T>(t + r * ld + c, tt);
+  struct Cst { float sc[VE<T>], sh[VE<T>], mu[VE<T>], is[VE<T>]; };
+  struct Reg { float a[VE<T>], t[VE<T>]; };
+  __device__ void prep(int c, Cst& q) const {
+    ldc(sc + c, q.sc); ldc(sh + c, q.sh); ldc(mean + c, q.mu); ldc(invstd + c, q.is);
+  }
+  __device__ void load(int64_t r, int c, Reg& q) const {
+    ldv<T>(da + r * ld + c, q.a);
+    ldv<T>(t + r * ld + c, q.t);
+  }
+  __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[2][VE<T>]) const {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      float pre = tt[v] * sc[c + v] + sh[c + v];
-      float dr = pre > 0.f ? a[v] : 0.f;
+      float pre = q.t[v] * k.sc[v] + k.sh[v];
+      float dr = pre > 0.f ? q.a[v] : 0.f;
       if (drop) dr = dropout_keep(seed, layer, r, c + v, thresh) ? dr * inv_keep : 0.f;
-      float xh = (tt[v] - mean[c + v]) * invstd[c + v];
-      a[v] = dr;
+      float xh = (q.t[v] - k.mu[v]) * k.is[v];
+      q.a[v] = dr;
       acc[0][v] += dr;
       acc[1][v] += dr * xh;
     }
-    stv<T>(da + r * ld + c, a);
+    stv<T>(da + r * ld + c, q.a);
   }
 };
 
 template <typename T> struct Bwd1ApplyOp {
   const T* dr; const T* t; const float* mean; const float* invstd; const float* coef; int ld, N;
   T* dt;
-  __device__ void operator()(int64_t r, int c, float (&acc)[1][VE<T>]) const {
-    float a[VE<T>], tt[VE<T>];
-    ldv<T>(dr + r * ld + c, a); ldv<T>(t + r * ld + c, tt);
+  struct Cst { float mu[VE<T>], is[VE<T>], k0[VE<T>], k1[VE<T>], k2[VE<T>]; };
+  struct Reg { float a[VE<T>], t[VE<T>]; };
+  __device__ void prep(int c, Cst& q) const {
+    ldc(mean + c, q.mu); ldc(invstd + c, q.is);
+    ldc(coef + c, q.k0); ldc(coef + N + c, q.k1); ldc(coef + 2 * N + c, q.k2);
+  }
+  __device__ void load(int64_t r, int c, Reg& q) const {
+    ldv<T>(dr + r * ld + c, q.a);
+    ldv<T>(t + r * ld + c, q.t);
+  }
+  __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[1][VE<T>]) const {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      float xh = (tt[v] - mean[c + v]) * invstd[c + v];
-      float y = coef[c + v] * a[v] - coef[N + c + v] * xh - coef[2 * N + c + v];
-      a[v] = y;
+      float xh = (q.t[v] - k.mu[v]) * k.is[v];
+      float y = k.k0[v] * q.a[v] - k.k1[v] * xh - k.k2[v];
+      q.a[v] = y;
       acc[0][v] += y;
     }
-    stv<T>(dt + r * ld + c, a);
+    stv<T>(dt + r * ld + c, q.a);
   }
 };
 
 // ------------------------------------------------------------ small kernels
-// part [nchunks][NK][N] f32 -> sums [3][N] f64 (components >= NK zeroed) + count at [3N]
-__global__ void reduce_partials_kernel(const float* part, int nchunks, int NK, int N, double* sums,
-                                       double count) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < 3 * N) {
-    int k = i / N, n = i % N;
-    double s = 0.0;
-    if (k < NK)
-      for (int c = 0; c < nchunks; ++c) s += (double)part[((int64_t)c * NK + k) * N + n];
-    sums[i] = s;
+// part [nchunks][NK][N] f32 -> sums [3][N] f64 (components >= NK zeroed) + count
+// at [3N].  Block = 8 columns x 32 chunk-lanes, all NK components of a column in
+// one block; fixed-order tree -> deterministic.  With `shift` (the stats pass's
+// K = t[0]) the shifted sums S0' = sum(t-K), S1' = sum((t-K)^2) are converted
+// to S0 = S0' + nK, S1 = S1' + 2K S0' + nK^2 (fp64), so SyncBN can add them.
+template <typename T>
+__global__ __launch_bounds__(NT) void reduce_partials_kernel(const float* part, int nchunks, int NK,
+                                                             int N, double* sums, double count,
+                                                             const T* shift) {
+  __shared__ double red[3][32][8];
+  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+  const int n = blockIdx.x * 8 + tx;
+  double s[3] = {0.0, 0.0, 0.0};
+  if (n < N)
+    for (int c = ty; c < nchunks; c += 32)
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+        if (k < NK) s[k] += (double)part[((int64_t)c * NK + k) * N + n];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) red[k][ty][tx] = s[k];
+  __syncthreads();
+  for (int o = 16; o > 0; o >>= 1) {
+    if (ty < o)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) red[k][ty][tx] += red[k][ty + o][tx];
+    __syncthreads();
   }
-  if (i == 0) sums[3 * N] = count;
+  if (ty == 0 && n < N) {
+    double v0 = red[0][0][tx], v1 = red[1][0][tx], v2 = red[2][0][tx];
+    if (shift) {
+      double K = (double)(float)shift[n];
+      v1 = v1 + 2.0 * K * v0 + count * K * K;
+      v0 = v0 + count * K;
+    }
+    sums[n] = v0;
+    sums[N + n] = v1;
+    sums[2 * N + n] = v2;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) sums[3 * N] = count;
 }
 
 __global__ void bn_finalize_kernel(const double* sums, int N, int Nr, int train, BnFinal f) {
@@ -342,12 +439,18 @@ __global__ void pack_kernel(PackBatch pb) {
   }
 }
 
+template <typename T>
+dcnr_status launch_reduce(const float* part, int nchunks, int NK, int N, double* sums,
+                          double count, const T* shift, hipStream_t s) {
+  hipLaunchKernelGGL(reduce_partials_kernel<T>, dim3((unsigned)cdiv(std::max(N, 1), 8)),
+                     dim3(NT), 0, s, part, nchunks, NK, N, sums, count, shift);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
 }  // namespace
 
 // ================================================================== API
-#define DISPATCH_T(prec, ...) \
-  ((prec) == DCNR_PREC_BF16 ? __VA_ARGS__##_impl<bf16> : __VA_ARGS__##_impl<float>)
-
 dcnr_status pack_weights(int precision, const PackBatch& pb, hipStream_t s) {
   if (pb.n == 0) return DCNR_OK;
   dim3 grid(64, pb.n);
@@ -369,6 +472,13 @@ dcnr_status col_stats(int precision, const void* t, int64_t B, int N, int ld, fl
                                      : col_stats_impl<float>(t, B, N, ld, part, nchunks, s);
 }
 
+dcnr_status reduce_stats(int precision, const float* part, int nchunks, int N, double* sums,
+                         double count, const void* t, hipStream_t s) {
+  return precision == DCNR_PREC_BF16
+             ? launch_reduce<bf16>(part, nchunks, 2, N, sums, count, (const bf16*)t, s)
+             : launch_reduce<float>(part, nchunks, 2, N, sums, count, (const float*)t, s);
+}
+
 template <typename T>
 static dcnr_status col_sum_impl(const void* x, int64_t B, int N, int ld, float* part, int* nc,
                                 hipStream_t s) {
@@ -383,11 +493,7 @@ dcnr_status col_sum(int precision, const void* x, int64_t B, int N, int ld, floa
 
 dcnr_status reduce_partials_nk(const float* part, int nchunks, int NK, int N, double* sums,
                                double count, hipStream_t s) {
-  int tot = 3 * N;
-  hipLaunchKernelGGL(reduce_partials_kernel, dim3((unsigned)cdiv(std::max(tot, 1), NT)), dim3(NT),
-                     0, s, part, nchunks, NK, N, sums, count);
-  DCNR_LAUNCH_CHECK();
-  return DCNR_OK;
+  return launch_reduce<float>(part, nchunks, NK, N, sums, count, nullptr, s);
 }
 
 dcnr_status bn_finalize2(const double* sums, int N, int Nr, int train, const BnFinal& f,
@@ -406,13 +512,16 @@ dcnr_status bn_bwd_coef(const double* sums, int N, int Nr, const float* gamma, c
   return DCNR_OK;
 }
 
+static uint32_t drop_thresh(float p) {
+  return (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0);
+}
+
 template <typename T>
 static dcnr_status bn_relu_drop_impl(const void* t, void* a, int64_t B, int N, int ld,
                                      const float* sc, const float* sh, float p, uint64_t seed,
                                      int layer, hipStream_t s) {
   BnReluDropOp<T> op{(const T*)t, (T*)a, ld, sc, sh, p > 0.f ? 1.f / (1.f - p) : 1.f,
-                     (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0), seed, layer,
-                     p > 0.f};
+                     drop_thresh(p), seed, layer, p > 0.f};
   return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
 }
 dcnr_status bn_relu_drop(int precision, const void* t, void* a, int64_t B, int N, int ld,
@@ -478,9 +587,7 @@ static dcnr_status bwd1_stats_impl(void* da, const void* t, const float* sc, con
                                    int ld, float p, uint64_t seed, int layer, float* part, int* nc,
                                    hipStream_t s) {
   Bwd1StatsOp<T> op{(T*)da, (const T*)t, sc, sh, mean, invstd, ld,
-                    p > 0.f ? 1.f / (1.f - p) : 1.f,
-                    (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0), seed, layer,
-                    p > 0.f};
+                    p > 0.f ? 1.f / (1.f - p) : 1.f, drop_thresh(p), seed, layer, p > 0.f};
   return run_rowcol<T, 2>(op, B, N, part, nc, s);
 }
 dcnr_status bwd_bn1_stats(int precision, void* da_dr, const void* t, const float* scale,

@@ -242,36 +242,56 @@ __global__ __launch_bounds__(NT) void cross_bwd_kernel(GatherDesc g, CrossBwdPar
       }
     }
   }
-  const int64_t stride = (int64_t)(2 * L + 1) * D + 1;
-  float* mp = part + wid * stride;
+  // block-level partial: the 4 waves add into LDS in fixed wave order
+  // (deterministic), then one coalesced store per block
+  const int stride = (2 * L + 1) * D + 1;
+  float* red = swf + D;   // [stride] after the weight region
+  const int w = threadIdx.x >> 6;
+  for (int ww = 0; ww < WPB; ++ww) {
+    if (w == ww) {
 #pragma unroll
-  for (int r = 0; r < RM; ++r) {
-    int e = lane + WAVE * r;
-    if (e >= D) continue;
+      for (int r = 0; r < RM; ++r) {
+        int e = lane + WAVE * r;
+        if (e >= D) continue;
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-      mp[l * D + e] = dwa[l][r];
-      mp[(L + l) * D + e] = dba[l][r];
+        for (int l = 0; l < L; ++l) {
+          red[l * D + e] = (ww ? red[l * D + e] : 0.f) + dwa[l][r];
+          red[(L + l) * D + e] = (ww ? red[(L + l) * D + e] : 0.f) + dba[l][r];
+        }
+        red[2 * L * D + e] = (ww ? red[2 * L * D + e] : 0.f) + dwfa[r];
+      }
+      if (lane == 0) red[(2 * L + 1) * D] = (ww ? red[(2 * L + 1) * D] : 0.f) + dbf;
     }
-    mp[2 * L * D + e] = dwfa[r];
+    __syncthreads();
   }
-  if (lane == 0) mp[(2 * L + 1) * D] = dbf;
+  float* mp = part + (int64_t)blockIdx.x * stride;
+  for (int i = threadIdx.x; i < stride; i += NT) mp[i] = red[i];
 }
 
-// reduce per-wave partials -> grads
-__global__ void cross_reduce_kernel(const float* part, int64_t nw, int D, int L, CrossBwdParams p,
-                                    int accumulate) {
-  int64_t stride = (int64_t)(2 * L + 1) * D + 1;
-  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= stride) return;
+// reduce per-block partials -> grads (8 elements x 32 lanes per block, fixed order)
+__global__ __launch_bounds__(NT) void cross_reduce_kernel(const float* part, int64_t nb, int D,
+                                                          int L, CrossBwdParams p, int accumulate) {
+  __shared__ float red[32][8];
+  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+  const int64_t stride = (int64_t)(2 * L + 1) * D + 1;
+  const int64_t i = (int64_t)blockIdx.x * 8 + tx;
   float s = 0.f;
-  for (int64_t w = 0; w < nw; ++w) s += part[w * stride + i];
+  if (i < stride)
+    for (int64_t w = ty; w < nb; w += 32) s += part[w * stride + i];
+  red[ty][tx] = s;
+  __syncthreads();
+  for (int o = 16; o > 0; o >>= 1) {
+    if (ty < o) red[ty][tx] += red[ty + o][tx];
+    __syncthreads();
+  }
+  if (ty != 0 || i >= stride) return;
+  s = red[0][tx];
   float* dst;
   if (i < (int64_t)L * D) dst = p.dw[i / D] + i % D;
   else if (i < (int64_t)2 * L * D) dst = p.db[(i - L * D) / D] + (i - L * D) % D;
   else if (i < stride - 1) dst = p.dwf_cross + (i - 2 * L * D);
   else dst = p.dbf;
-  if (dst) *dst = accumulate ? *dst + s : s;
+  *dst = accumulate ? *dst + s : s;
 }
 
 template <typename T, int RM>
@@ -291,8 +311,8 @@ dcnr_status launch_bwd(const GatherDesc& g, const CrossBwdParams& p, const int64
                        const int64_t* item, const int64_t* cat, const float* num, const float* dz,
                        int64_t B, const float* dx0, int ld_dx, float* part, int64_t nw,
                        hipStream_t s) {
-  size_t lds = (size_t)(2 * L + 1) * g.D * sizeof(float);
-  hipLaunchKernelGGL((cross_bwd_kernel<RM, L>), dim3((unsigned)(nw / WPB)), dim3(NT), lds, s, g, p,
+  size_t lds = (size_t)(2 * (2 * L + 1) * g.D + 1) * sizeof(float);
+  hipLaunchKernelGGL((cross_bwd_kernel<RM, L>), dim3((unsigned)nw), dim3(NT), lds, s, g, p,
                      user, item, cat, num, dz, B, dx0, ld_dx, part);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
@@ -313,11 +333,11 @@ dcnr_status dispatch_bwd_L(int L, const GatherDesc& g, const CrossBwdParams& p,
   return DCNR_UNSUPPORTED_SHAPE;
 }
 
-constexpr int64_t BWD_WAVES = 2048;
+constexpr int64_t BWD_BLOCKS = 2048;  // x4 waves: 32 waves/CU of latency hiding
 
 }  // namespace
 
-size_t cross_bwd_part_elems(int D, int L) { return (size_t)BWD_WAVES * ((2 * L + 1) * D + 1); }
+size_t cross_bwd_part_elems(int D, int L) { return (size_t)BWD_BLOCKS * ((2 * L + 1) * D + 1); }
 
 dcnr_status gather_cross_fwd(int precision, const GatherDesc& g, const CrossParams& cp,
                              const int64_t* user, const int64_t* item, const int64_t* cat,
@@ -351,13 +371,13 @@ dcnr_status cross_bwd_scatter(const GatherDesc& g, const CrossBwdParams& p, cons
   }
   dcnr_status st = D <= 8 * WAVE
                        ? dispatch_bwd_L<8>(L, g, p, user, item, cat, num, dz, B, dx0_deep, ld_dx,
-                                           part, BWD_WAVES, s)
+                                           part, BWD_BLOCKS, s)
                        : dispatch_bwd_L<16>(L, g, p, user, item, cat, num, dz, B, dx0_deep, ld_dx,
-                                            part, BWD_WAVES, s);
+                                            part, BWD_BLOCKS, s);
   if (st != DCNR_OK) return st;
   int64_t stride = (int64_t)(2 * L + 1) * D + 1;
-  hipLaunchKernelGGL(cross_reduce_kernel, dim3((unsigned)cdiv(stride, NT)), dim3(NT), 0, s, part,
-                     BWD_WAVES, D, L, p, accumulate);
+  hipLaunchKernelGGL(cross_reduce_kernel, dim3((unsigned)cdiv(stride, 8)), dim3(NT), 0, s, part,
+                     BWD_BLOCKS, D, L, p, accumulate);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }

@@ -57,7 +57,7 @@ _SIGS = {
     "dcnr_forward": (ctypes.c_int, [ctypes.POINTER(ModelDesc), _P, _P, _P, _P, _P, _I64,
                                     ctypes.c_int, ctypes.c_uint64, _P, _P, ctypes.c_size_t, _P]),
     "dcnr_backward": (ctypes.c_int, [ctypes.POINTER(ModelDesc), _P, _P, _P, _P, _P, _P, _I64, _P,
-                                     ctypes.c_int, _P, ctypes.c_size_t, _P]),
+                                     ctypes.c_uint64, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     "dcnr_bce_workspace_size": (ctypes.c_size_t, []),
     "dcnr_bce_with_logits": (ctypes.c_int, [_P, _P, _I64, _P, _P, ctypes.c_float, _P,
                                             ctypes.c_size_t, _P]),
@@ -69,7 +69,26 @@ _SIGS = {
     "dcnr_cosine_topk": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, _P, _I64, ctypes.c_int32,
                                         _P, _P, _P, ctypes.c_size_t, _P]),
     "dcnr_check_errors": (ctypes.c_int, [_P, ctypes.c_size_t, _P]),
+    "dcnr_profile_enable": (None, [ctypes.c_int]),
+    "dcnr_profile_collect": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
 }
+
+KERNEL_CLASSES = ["gather_cross", "gemm_fwd", "gemm_dx", "gemm_dw", "rowwise", "reduce",
+                  "cross_bwd", "head", "adam", "knn", "pack"]
+
+
+def profile_enable(on: bool):
+    load().dcnr_profile_enable(1 if on else 0)
+
+
+def profile_collect():
+    """{class: (total_ms, launches)} since the last collect (synchronises)."""
+    n = len(KERNEL_CLASSES)
+    ms = (ctypes.c_double * n)()
+    cnt = (ctypes.c_int64 * n)()
+    check(load().dcnr_profile_collect(ctypes.cast(ms, ctypes.c_void_p),
+                                      ctypes.cast(cnt, ctypes.c_void_p), n), "profile")
+    return {k: (ms[i], cnt[i]) for i, k in enumerate(KERNEL_CLASSES)}
 
 _lib = None
 _lock = threading.Lock()

@@ -220,7 +220,8 @@ def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
 
 
 def run_backward(model: DCN_RecSys, user, item, cat, num, dlogits, ws, grads: List[torch.Tensor],
-                 accumulate=False):
+                 seed: int, accumulate=False):
+    """``seed`` must be the dropout seed of the train-mode forward that filled ws."""
     lib = _lib.load()
     B = user.shape[0]
     desc = model.desc()
@@ -228,8 +229,8 @@ def run_backward(model: DCN_RecSys, user, item, cat, num, dlogits, ws, grads: Li
                            _lib.ptr_array(grads), user.data_ptr(), item.data_ptr(),
                            cat.data_ptr() if cat.numel() else None,
                            num.data_ptr() if num.numel() else None, B,
-                           dlogits.data_ptr(), 1 if accumulate else 0, ws.data_ptr(), ws.numel(),
-                           _lib.stream_ptr(user.device))
+                           dlogits.data_ptr(), int(seed), 1 if accumulate else 0, ws.data_ptr(),
+                           ws.numel(), _lib.stream_ptr(user.device))
     _lib.check(st, "dcnr_backward")
 
 
@@ -239,6 +240,7 @@ class _DCNRFunction(torch.autograd.Function):
         logits, ws = run_forward(model, train, seed, user, item, cat, num)
         ctx.model = model
         ctx.train = train
+        ctx.seed = seed
         ctx.ws = ws
         ctx.save_for_backward(user, item, cat, num)
         return logits
@@ -253,7 +255,7 @@ class _DCNRFunction(torch.autograd.Function):
         params = model.param_tensors()
         grads = [torch.empty_like(p) for p in params]
         dl = dlogits.reshape(-1).to(torch.float32).contiguous()
-        run_backward(model, user, item, cat, num, dl, ctx.ws, grads)
+        run_backward(model, user, item, cat, num, dl, ctx.ws, grads, ctx.seed)
         ctx.ws = None
         out = [g if p.requires_grad else None for g, p in zip(grads, params)]
         return (None, None, None, None, None, None, None, *out)

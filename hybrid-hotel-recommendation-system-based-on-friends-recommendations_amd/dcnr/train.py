@@ -38,7 +38,7 @@ class FusedTrainer:
         self.world = dist.get_world_size(process_group) if (dist.is_available() and
                                                              dist.is_initialized()) else 1
         self._ws = None
-        self._params = model.param_tensors()
+        self._grads = [p.grad for p in model.param_tensors()]   # views into gflat
         if sync_bn and self.world > 1:
             from .parallel import install_sync_bn
             install_sync_bn(model, process_group)
@@ -52,7 +52,8 @@ class FusedTrainer:
         logits, self._ws = run_forward(model, True, seed, user, item, cat, num, self._ws)
         # grad_scale 1/world: the SUM all-reduce then yields the global mean gradient
         loss, dz = bce_with_logits(logits, y, True, 1.0 / self.world)
-        run_backward(model, user, item, cat, num, dz, self._ws, self._params, accumulate=False)
+        run_backward(model, user, item, cat, num, dz, self._ws, self._grads, seed,
+                     accumulate=False)
         if self.world > 1:
             dist.all_reduce(self.gflat, op=dist.ReduceOp.SUM, group=self.pg)
         self.optimizer_step()

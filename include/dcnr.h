@@ -128,7 +128,7 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
 dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void* const* grads,
                           const int64_t* user_ids, const int64_t* item_ids,
                           const int64_t* cat_features, const float* num_features, int64_t B,
-                          const float* dlogits, int accumulate, void* ws, size_t ws_bytes,
+                          const float* dlogits, uint64_t dropout_seed, int accumulate, void* ws, size_t ws_bytes,
                           dcnr_stream_t stream);
 
 size_t dcnr_bce_workspace_size(void);
@@ -160,6 +160,29 @@ size_t dcnr_cosine_topk_workspace_size(int64_t N, int64_t Q, int32_t k);
 dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t N, int32_t d,
                              const float* queries, int64_t Q, int32_t k, int64_t* idx,
                              float* dist, void* ws, size_t ws_bytes, dcnr_stream_t stream);
+
+/* Kernel-timing instrumentation (measurement only, off by default): when
+ * enabled, every launch the library makes is bracketed by HIP events on its
+ * stream and attributed to one of these classes. */
+typedef enum {
+  DCNR_K_GATHER_CROSS = 0, /* gather + x0 + cross forward                 */
+  DCNR_K_GEMM_FWD = 1,     /* deep-tower Linear forward (MFMA)             */
+  DCNR_K_GEMM_DX = 2,      /* deep-tower dX GEMMs (MFMA)                   */
+  DCNR_K_GEMM_DW = 3,      /* deep-tower dW split-K GEMMs (MFMA)           */
+  DCNR_K_ROWWISE = 4,      /* BN stats/apply, ReLU, dropout, residual      */
+  DCNR_K_REDUCE = 5,       /* partial-sum / split-K reductions, BN finalize */
+  DCNR_K_CROSS_BWD = 6,    /* cross backward + embedding-grad scatter      */
+  DCNR_K_HEAD = 7,         /* head dot, logits, BCE                         */
+  DCNR_K_ADAM = 8,         /* fused Adam/AdamW                              */
+  DCNR_K_KNN = 9,          /* cosine top-k                                  */
+  DCNR_K_PACK = 10,        /* weight packing / zero fills                  */
+  DCNR_K_COUNT = 11
+} dcnr_kernel_class;
+
+void dcnr_profile_enable(int on);
+/* Synchronises the recorded events and returns, per class, the summed kernel
+ * milliseconds and launch counts since the last collect (arrays of n). */
+dcnr_status dcnr_profile_collect(double* ms, int64_t* launches, int32_t n);
 
 /* Synchronises `stream` and reports kernel-side errors recorded in ws
  * (DCNR_INDEX_OOB when DCNR_FLAG_CHECK_INDICES saw an out-of-range id). */

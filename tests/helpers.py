@@ -63,3 +63,19 @@ def assert_grads_close(grads: dict, ref: dict, rtol=5e-3, atol=1e-7, names=None)
         if e > rtol:
             bad.append((k, e, float(np.abs(g - r).max())))
     assert not bad, f"grad mismatches: {bad}"
+
+
+def dropout_mask_np(seed: int, layer: int, B: int, H: int, p: float) -> np.ndarray:
+    """Host replica of libdcnr's counter-based dropout keep-test
+    (csrc/dcnr_internal.h dropout_keep): keep(seed, layer, row, col)."""
+    M = np.uint64
+    with np.errstate(over="ignore"):
+        x = M(seed) ^ (M(0x9E3779B97F4A7C15) * M(layer + 1))
+        rows = np.arange(B, dtype=np.uint64)[:, None]
+        cols = np.arange(H, dtype=np.uint64)[None, :]
+        x = x + rows * M(0x100000001B3) + cols * M(0xC2B2AE3D27D4EB4F)
+        x = x ^ (x >> M(30)); x = x * M(0xBF58476D1CE4E5B9)
+        x = x ^ (x >> M(27)); x = x * M(0x94D049BB133111EB)
+        x = x ^ (x >> M(31))
+    thresh = np.uint64(min(4294967295.0, float(np.float32(p)) * 4294967296.0))
+    return ((x >> M(32)) >= thresh).astype(np.float64)
