@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -351,6 +352,24 @@ dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train
   return DCNR_OK;
 }
 
+// C = A . B^T with k-contiguous operands: bf16 -> the weight-resident streaming
+// kernel (gemm_nt.hip) when the weight fits LDS; otherwise the generic tiled
+// MFMA kernel (fp32 parity path, K > 512).
+dcnr_status gemm_nn(int prec, int epi, const GemmArgs& g, int splits, hipStream_t s) {
+  if (prec == DCNR_PREC_BF16 && splits == 1 && gemm_nt_supported(g.K, g.N) &&
+      getenv("DCNR_DISABLE_GEMM_NT") == nullptr) {
+    NtArgs a;
+    memset(&a, 0, sizeof(a));
+    a.X = (const bf16*)g.A; a.ldx = g.lda; a.M = g.M; a.K = (int)g.K;
+    a.W = (const bf16*)g.B; a.ldw = g.ldb; a.N = (int)g.N;
+    a.C = g.C; a.ldc = g.ldc; a.bias = g.bias;
+    a.R = g.resid; a.ldr = g.ldr;
+    int ne = epi == EPI_STORE_RESID ? NT_EPI_RESID : (g.out_f32 ? NT_EPI_F32 : NT_EPI_BIAS);
+    return gemm_nt(ne, a, s);
+  }
+  return gemm(prec, false, false, epi, g, splits, s);
+}
+
 dcnr_status linear_fwd(const Dims& d, const void* A, int lda, const void* W, int K,
                        const float* bias, void* out, int64_t B, hipStream_t s) {
   GemmArgs g;
@@ -358,7 +377,7 @@ dcnr_status linear_fwd(const Dims& d, const void* A, int lda, const void* W, int
   g.A = A; g.lda = lda; g.B = W; g.ldb = K;
   g.C = out; g.ldc = d.Hp; g.bias = bias;
   g.M = B; g.N = d.Hp; g.K = K; g.k_per_split = K;
-  return gemm(d.prec, false, false, EPI_STORE, g, 1, s);
+  return gemm_nn(d.prec, EPI_STORE, g, 1, s);
 }
 
 // dW[N][Kc] = sum_b dY[b][n] X[b][k]   (real extents Nr x Kr written to out)
@@ -539,7 +558,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       memset(&g, 0, sizeof(g));
       g.A = L.dt2; g.lda = Hp; g.B = L.W2t[j]; g.ldb = Hp; g.C = L.da; g.ldc = Hp;
       g.M = B; g.N = Hp; g.K = Hp; g.k_per_split = Hp;
-      TRYP(DCNR_K_GEMM_DX, gemm(d.prec, false, false, EPI_STORE, g, 1, s));
+      TRYP(DCNR_K_GEMM_DX, gemm_nn(d.prec, EPI_STORE, g, 1, s));
     }
     // ---- relu/dropout + BN1 backward
     TRYP(DCNR_K_ROWWISE, bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean, bn1.invstd, B, Hp, Hp,
@@ -561,7 +580,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       g.A = L.a1; g.lda = Hp; g.B = L.W1t[j]; g.ldb = Hp; g.C = L.G; g.ldc = Hp;
       g.resid = L.du; g.ldr = Hp;
       g.M = B; g.N = Hp; g.K = Hp; g.k_per_split = Hp;
-      TRYP(DCNR_K_GEMM_DX, gemm(d.prec, false, false, EPI_STORE_RESID, g, 1, s));
+      TRYP(DCNR_K_GEMM_DX, gemm_nn(d.prec, EPI_STORE_RESID, g, 1, s));
     }
     Gin = L.G;
   }
@@ -576,7 +595,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     memset(&g, 0, sizeof(g));
     g.A = L.G; g.lda = Hp; g.B = L.W0t; g.ldb = Hp; g.C = L.dx0; g.ldc = d.Dp; g.out_f32 = 1;
     g.M = B; g.N = d.Dp; g.K = Hp; g.k_per_split = Hp;
-    TRYP(DCNR_K_GEMM_DX, gemm(d.prec, false, false, EPI_STORE, g, 1, s));
+    TRYP(DCNR_K_GEMM_DX, gemm_nn(d.prec, EPI_STORE, g, 1, s));
   }
   // ---- cross stack + head bias + embedding scatter
   GatherDesc g = make_gather(d, P, desc->n_num);

@@ -88,11 +88,29 @@ struct GemmArgs {
   int64_t k_per_split;   // split-K chunk (multiple of BK), = K when no split
   int64_t slab_stride;   // elements between split slabs (EPI_SPLITK)
   int out_f32;           // 1: C is float, 0: C is T
+  int xcd_split;         // set by gemm(): 1-D grid with a split's tiles on one XCD
 };
 
 // precision 0 = fp32 (f32 MFMA), 1 = bf16 (bf16 MFMA).
 dcnr_status gemm(int precision, bool a_t, bool b_t, int epi, const GemmArgs& a, int splits,
                  hipStream_t s);
+
+// bf16 weight-resident streaming GEMM (gemm_nt.hip): C[M,N] = X[M,K] W[N,K]^T
+enum NtEpi : int {
+  NT_EPI_BIAS = 0,    // C bf16 = acc + bias[n] (bias padded to N, may be null)
+  NT_EPI_F32 = 1,     // C f32  = acc
+  NT_EPI_RESID = 2,   // C bf16 = acc + R[m][n] (bf16)
+};
+struct NtArgs {
+  const bf16* X; int64_t ldx; int64_t M; int K;
+  const bf16* W; int64_t ldw; int N;
+  void* C; int64_t ldc;
+  const float* bias;
+  const void* R; int64_t ldr;
+  int nslices, groups; int64_t mtiles;   // filled by gemm_nt
+};
+bool gemm_nt_supported(int64_t K, int64_t N);
+dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ elementwise
 struct PackDesc {            // W [rows][cols] f32 -> dst T [rows_p][ld] (+ optional transpose)

@@ -196,57 +196,57 @@ template <typename T> struct BnAddReluOp {   // out = relu(t*sc+sh + x)
 };
 
 // backward of out = relu(BN2(t2) + x): du = g*[out>0]; g = G or dz (x) wf
-template <typename T> struct Bwd2StatsOp {
+template <typename T, bool HAS_G> struct Bwd2StatsOp {
   const T* G; const float* dz; const float* wf; const T* out; const T* t;
   const float* mean; const float* invstd; int ld;
   struct Cst { float wf[VE<T>], mu[VE<T>], is[VE<T>]; };
-  struct Reg { float o[VE<T>], t[VE<T>], g[VE<T>]; float d; };
+  struct Reg { float o[VE<T>], t[VE<T>], g[VE<T>]; float d = 0.f; };
   __device__ void prep(int c, Cst& q) const {
-    if (!G) ldc(wf + c, q.wf);
+    if (!HAS_G) ldc(wf + c, q.wf);
     ldc(mean + c, q.mu); ldc(invstd + c, q.is);
   }
   __device__ void load(int64_t r, int c, Reg& q) const {
     ldv<T>(out + r * ld + c, q.o);
     ldv<T>(t + r * ld + c, q.t);
-    if (G) ldv<T>(G + r * ld + c, q.g);
+    if constexpr (HAS_G) ldv<T>(G + r * ld + c, q.g);
     else q.d = dz[r];
   }
   __device__ void apply(int64_t, int, const Cst& k, Reg& q, float (&acc)[3][VE<T>]) const {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      float g = G ? q.g[v] : q.d * k.wf[v];
+      float g = HAS_G ? q.g[v] : q.d * k.wf[v];
       float du = q.o[v] > 0.f ? g : 0.f;
       float xh = (q.t[v] - k.mu[v]) * k.is[v];
       acc[0][v] += du;
       acc[1][v] += du * xh;
-      if (!G) acc[2][v] += q.d * q.o[v];
+      if (!HAS_G) acc[2][v] += q.d * q.o[v];
     }
   }
 };
 
 // dt = c0*du - c1*xh - c2 ; writes dt, du ; partial sum of dt (bias grad)
-template <typename T> struct Bwd2ApplyOp {
+template <typename T, bool HAS_G> struct Bwd2ApplyOp {
   const T* G; const float* dz; const float* wf; const T* out; const T* t;
   const float* mean; const float* invstd; const float* coef; int ld, N;
   T* dt; T* du_out;
   struct Cst { float wf[VE<T>], mu[VE<T>], is[VE<T>], k0[VE<T>], k1[VE<T>], k2[VE<T>]; };
-  struct Reg { float o[VE<T>], t[VE<T>], g[VE<T>]; float d; };
+  struct Reg { float o[VE<T>], t[VE<T>], g[VE<T>]; float d = 0.f; };
   __device__ void prep(int c, Cst& q) const {
-    if (!G) ldc(wf + c, q.wf);
+    if (!HAS_G) ldc(wf + c, q.wf);
     ldc(mean + c, q.mu); ldc(invstd + c, q.is);
     ldc(coef + c, q.k0); ldc(coef + N + c, q.k1); ldc(coef + 2 * N + c, q.k2);
   }
   __device__ void load(int64_t r, int c, Reg& q) const {
     ldv<T>(out + r * ld + c, q.o);
     ldv<T>(t + r * ld + c, q.t);
-    if (G) ldv<T>(G + r * ld + c, q.g);
+    if constexpr (HAS_G) ldv<T>(G + r * ld + c, q.g);
     else q.d = dz[r];
   }
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[1][VE<T>]) const {
     float d[VE<T>];
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      float g = G ? q.g[v] : q.d * k.wf[v];
+      float g = HAS_G ? q.g[v] : q.d * k.wf[v];
       float du = q.o[v] > 0.f ? g : 0.f;
       float xh = (q.t[v] - k.mu[v]) * k.is[v];
       float y = k.k0[v] * du - k.k1[v] * xh - k.k2[v];
@@ -549,7 +549,11 @@ template <typename T>
 static dcnr_status bwd2_stats_impl(const void* G, const float* dz, const float* wf, const void* out,
                                    const void* t, const float* mean, const float* invstd,
                                    int64_t B, int N, int ld, float* part, int* nc, hipStream_t s) {
-  Bwd2StatsOp<T> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, ld};
+  if (G) {
+    Bwd2StatsOp<T, true> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, ld};
+    return run_rowcol<T, 3>(op, B, N, part, nc, s);
+  }
+  Bwd2StatsOp<T, false> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, ld};
   return run_rowcol<T, 3>(op, B, N, part, nc, s);
 }
 dcnr_status bwd_bn2_stats3(int precision, const void* G, const float* dz, const float* wf,
@@ -566,8 +570,13 @@ static dcnr_status bwd2_apply_impl(const void* G, const float* dz, const float* 
                                    const float* invstd, const float* coef, int64_t B, int N,
                                    int ld, void* dt, void* du, float* part, int* nc,
                                    hipStream_t s) {
-  Bwd2ApplyOp<T> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, coef, ld, N,
-                    (T*)dt, (T*)du};
+  if (G) {
+    Bwd2ApplyOp<T, true> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, coef,
+                            ld, N, (T*)dt, (T*)du};
+    return run_rowcol<T, 1>(op, B, N, part, nc, s);
+  }
+  Bwd2ApplyOp<T, false> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, coef,
+                           ld, N, (T*)dt, (T*)du};
   return run_rowcol<T, 1>(op, B, N, part, nc, s);
 }
 dcnr_status bwd_bn2_apply2(int precision, const void* G, const float* dz, const float* wf,

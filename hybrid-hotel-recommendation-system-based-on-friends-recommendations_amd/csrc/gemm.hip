@@ -117,9 +117,21 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) T lds[2 * (LA::SIZE + LB::SIZE)];
 
   const int64_t ntl = (g.N + BN - 1) / BN;
-  const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
+  int64_t t;
+  int split;
+  if (g.xcd_split) {
+    // split-K over the batch: every output tile of one split runs on one XCD
+    // (blocks b, b+8, ... share an L2), so the split's rows of both operands
+    // are fetched from HBM once and re-read from L2 by the other tiles
+    const int64_t ntiles = ((g.M + BM - 1) / BM) * ntl;
+    const int64_t bid = blockIdx.x;
+    split = (int)((bid % 8) + 8 * (bid / (8 * ntiles)));
+    t = (bid / 8) % ntiles;
+  } else {
+    t = xcd_remap(blockIdx.x, gridDim.x);
+    split = blockIdx.y;
+  }
   const int64_t tm = t / ntl, tn = t % ntl;
-  const int split = blockIdx.y;
   const int64_t m0 = tm * BM, n0 = tn * BN;
   const int64_t kbeg = (int64_t)split * g.k_per_split;
   const int64_t kend = min(g.K, kbeg + g.k_per_split);
@@ -217,8 +229,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
 template <typename T, bool AT, bool BT, int EPI, typename TO>
 dcnr_status launch(const GemmArgs& a, int splits, hipStream_t s) {
   int64_t mt = cdiv(a.M, BM), ntl = cdiv(a.N, BN);
+  GemmArgs b = a;
   dim3 grid((unsigned)(mt * ntl), (unsigned)splits);
-  hipLaunchKernelGGL((gemm_kernel<T, AT, BT, EPI, TO>), grid, dim3(NT), 0, s, a);
+  b.xcd_split = 0;
+  if (EPI == EPI_SPLITK && splits % 8 == 0) {
+    b.xcd_split = 1;
+    grid = dim3((unsigned)(mt * ntl * splits), 1);
+  }
+  hipLaunchKernelGGL((gemm_kernel<T, AT, BT, EPI, TO>), grid, dim3(NT), 0, s, b);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }

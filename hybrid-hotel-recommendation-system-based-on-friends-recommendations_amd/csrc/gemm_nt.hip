@@ -1,0 +1,270 @@
+// Weight-resident streaming GEMM for the bf16 deep tower (gfx950):
+//
+//   C[M, N] = X[M, K] . W[N, K]^T  (+ bias | + residual),  K <= 512
+//
+// The deep tower's Linear layers (train.py:143,105,109) have a huge M (the
+// batch, 131072) and a small N x K weight (<= 512 x 512): the problem is one
+// pass over the activations.  Design:
+//  * each workgroup keeps a 128-row slice of W resident in LDS for its whole
+//    lifetime (128 x K bf16 <= 128 KiB, XOR-swizzled so the ds_read_b128
+//    fragment reads are bank-conflict free) -- one barrier, at the start;
+//  * each of the 4 waves owns 32 rows of every 128-row M-tile and loads its X
+//    fragments straight from HBM into registers (the 16x16x32 B-operand
+//    layout is 16 rows x 64 contiguous bytes per load), through a ring
+//    DEPTH k-steps deep that runs continuously across the wave's M-tiles:
+//    no LDS staging and no barrier in the main loop, counted vmcnt waits;
+//  * workgroups are grouped so the N-slices of one M-tile run on one XCD at
+//    the same time (blocks b, b+8, ... share an XCD's L2): X comes from HBM
+//    once and is re-read from L2 by the other slices;
+//  * v_mfma_f32_16x16x32_bf16 with W as the A operand and X as the B operand:
+//    each lane accumulates 4 consecutive output columns of one row, so the
+//    epilogue stores are 8-byte (bf16) / 16-byte (f32) row-contiguous;
+//  * all global accesses go through range-checked buffer descriptors
+//    (out-of-range loads read 0, stores are dropped): branch-free edges.
+#include "dcnr_internal.h"
+
+namespace dcnr {
+namespace {
+
+constexpr int NT = 256, TM = 128, TN = 128, BK = 32, WROWS = TM / 4;
+
+template <int KTP> struct NtCfg {
+  static constexpr int WCH = KTP * (BK / 8);                 // 16-B chunks per W row
+  static constexpr int DEPTH = KTP;                          // prefetch ring depth (k-steps)
+  static constexpr int W_LDS = TN * WCH;                     // uint4 units
+  static constexpr size_t LDS_BYTES = (size_t)W_LDS * 16;
+};
+
+template <int WCH>
+__device__ __forceinline__ int w_slot(int row, int ch) { return row * WCH + (ch ^ (row & 15)); }
+
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+constexpr int OOR = 0x7fffff00;  // a buffer offset past num_records: loads 0, stores dropped
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  bf16 x = (bf16)a, y = (bf16)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+}
+
+// X fragments of one k-step for this wave: rows r0 + i*16 + (lane&15), k = kt*32 + 8*(lane>>4)
+__device__ __forceinline__ void load_x(u32x4 (&f)[2], __amdgpu_buffer_rsrc_t xr, int64_t ldx,
+                                       int64_t M, int K, int64_t r0, int kt, int lane, bool valid) {
+  const int k = kt * BK + 8 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int64_t m = r0 + i * 16 + (lane & 15);
+    const bool ok = valid && m < M && k < K;
+    f[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (int)((m * ldx + k) * 2) : OOR, 0, 0);
+  }
+}
+
+template <int KTP, int EPI>
+__global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
+  using C = NtCfg<KTP>;
+  constexpr int DEPTH = C::DEPTH;
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+  uint4* Ws = lds;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nsl = a.nslices;
+  const int bid = blockIdx.x;
+  const int slice = (bid / 8) % nsl;
+  const int group = (bid % 8) + 8 * (bid / (8 * nsl));
+  const int groups = a.groups;
+  const int n0 = slice * TN;
+
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.X, (short)0, (int)(a.M * a.ldx * 2), 0x00020000);
+  const int es = EPI == NT_EPI_F32 ? 4 : 2;
+  const __amdgpu_buffer_rsrc_t cr =
+      __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, (int)(a.M * a.ldc * es), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr_ = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.R, (short)0, EPI == NT_EPI_RESID ? (int)(a.M * a.ldr * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.bias, (short)0, a.bias ? a.N * 4 : 0, 0x00020000);
+
+  // start the X stream before the W slice load so both are in flight
+  u32x4 ring[DEPTH][2];
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d)
+    load_x(ring[d], xr, a.ldx, a.M, a.K, (int64_t)group * TM + wave * WROWS, d, lane,
+           group < a.mtiles);
+
+  // resident W slice (rows n0..n0+127, zero-padded beyond N and K)
+  const int kch = a.K / 8;
+  for (int c = tid; c < C::W_LDS; c += NT) {
+    const int row = c / C::WCH, ch = c % C::WCH;
+    const int n = n0 + row;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < a.N && ch < kch) v = *reinterpret_cast<const uint4*>(a.W + (int64_t)n * a.ldw + ch * 8);
+    Ws[w_slot<C::WCH>(row, ch)] = v;
+  }
+
+  // per-column bias for this lane's output columns (loaded once)
+  float bias[8][4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int n = n0 + j * 16 + (lane >> 4) * 4;
+    u32x4 b4 = {0u, 0u, 0u, 0u};
+    if constexpr (EPI == NT_EPI_BIAS)
+      b4 = __builtin_amdgcn_raw_buffer_load_b128(br, n < a.N ? n * 4 : OOR, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[j][r] = __uint_as_float(b4[r]);
+  }
+  __syncthreads();
+
+  for (int64_t mt = group; mt < a.mtiles; mt += groups) {
+    const int64_t r0 = mt * TM + wave * WROWS;
+    // residual operand of this tile, issued ahead of the k-loop's refills so
+    // that waiting for it in the epilogue does not drain the prefetch ring
+    u32x2 resid[2][8];
+    if constexpr (EPI == NT_EPI_RESID) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int n = n0 + j * 16 + (lane >> 4) * 4;
+          const int64_t m = r0 + i * 16 + (lane & 15);
+          const bool ok = n < a.N && m < a.M;
+          resid[i][j] = __builtin_amdgcn_raw_buffer_load_b64(
+              rr_, ok ? (int)((m * a.ldr + n) * 2) : OOR, 0, 0);
+        }
+    }
+    f32x4 acc[2][8];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // W fragments double-buffered in registers: the ds_reads of k-step kt+1
+    // are issued ahead of k-step kt's MFMAs; sched_barrier pins one k-step per
+    // region so the compiler does not hoist the whole tile's reads (spills)
+    bf16x8 wf[2][8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      wf[0][j] = __builtin_bit_cast(bf16x8, Ws[w_slot<C::WCH>(j * 16 + (lane & 15), lane >> 4)]);
+#pragma unroll
+    for (int kt = 0; kt < KTP; ++kt) {
+      const int slot = kt % DEPTH;
+      const int cb = kt & 1;
+      if (kt + 1 < KTP) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          wf[cb ^ 1][j] = __builtin_bit_cast(
+              bf16x8, Ws[w_slot<C::WCH>(j * 16 + (lane & 15), (kt + 1) * 4 + (lane >> 4))]);
+      }
+      bf16x8 xf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) xf[i] = __builtin_bit_cast(bf16x8, ring[slot][i]);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][j], xf[i], acc[i][j], 0, 0, 0);
+      // refill the slot with the k-step DEPTH ahead (same or next M-tile)
+      {
+        const int kn = kt + DEPTH;
+        const int64_t mtn = mt + (kn >= KTP ? groups : 0);
+        load_x(ring[slot], xr, a.ldx, a.M, a.K, mtn * TM + wave * WROWS, kn % KTP, lane,
+               mtn < a.mtiles);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+
+    // epilogue: lane holds C[m][n..n+3] for each (i, j)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = n0 + j * 16 + (lane >> 4) * 4;
+      const bool nok = n < a.N;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int64_t m = r0 + i * 16 + (lane & 15);
+        const bool ok = nok && m < a.M;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[j][r];
+        if constexpr (EPI == NT_EPI_F32) {
+          u32x4 o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                     __float_as_uint(v[3])};
+          __builtin_amdgcn_raw_buffer_store_b128(o, cr, ok ? (int)((m * a.ldc + n) * 4) : OOR, 0, 0);
+        } else {
+          if constexpr (EPI == NT_EPI_RESID) {
+            const u32x2 rv = resid[i][j];
+            const bf16* rb = reinterpret_cast<const bf16*>(&rv);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += (float)rb[r];
+          }
+          u32x2 o = {pack2(v[0], v[1]), pack2(v[2], v[3])};
+          __builtin_amdgcn_raw_buffer_store_b64(o, cr, ok ? (int)((m * a.ldc + n) * 2) : OOR, 0, 0);
+        }
+      }
+    }
+  }
+}
+
+template <int KTP, int EPI>
+dcnr_status launch_nt(NtArgs a, hipStream_t s) {
+  using C = NtCfg<KTP>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    DCNR_HIP(hipFuncSetAttribute((const void*)gemm_nt_kernel<KTP, EPI>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES));
+    attr_set = true;
+  }
+  a.nslices = (int)cdiv(a.N, TN);
+  // 32-bit buffer offsets: launch in M-chunks of < 2^29 bytes per operand
+  const int64_t maxld = std::max<int64_t>({a.ldx, a.ldc * 2, a.R ? a.ldr : 0});
+  const int64_t mchunk = std::max<int64_t>(TM, ((int64_t(1) << 29) / (maxld * 2)) / TM * TM);
+  if (a.M > mchunk) {
+    for (int64_t m0 = 0; m0 < a.M; m0 += mchunk) {
+      NtArgs b = a;
+      b.M = std::min(mchunk, a.M - m0);
+      b.X = a.X + m0 * a.ldx;
+      b.C = (char*)a.C + m0 * a.ldc * (EPI == NT_EPI_F32 ? 4 : 2);
+      if (a.R) b.R = (const char*)a.R + m0 * a.ldr * 2;
+      dcnr_status st = launch_nt<KTP, EPI>(b, s);
+      if (st != DCNR_OK) return st;
+    }
+    return DCNR_OK;
+  }
+  a.mtiles = cdiv(a.M, TM);
+  // one workgroup per CU; grid a multiple of 8 * nslices (XCD grouping)
+  const int unit = 8 * a.nslices;
+  int grid = std::max(unit, (256 / unit) * unit);
+  const int64_t need = a.mtiles * a.nslices;
+  if (need < grid) grid = (int)(cdiv(need, unit) * unit);
+  a.groups = grid / a.nslices;
+  hipLaunchKernelGGL((gemm_nt_kernel<KTP, EPI>), dim3(grid), dim3(NT), C::LDS_BYTES, s, a);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+template <int EPI>
+dcnr_status dispatch_k(const NtArgs& a, hipStream_t s) {
+  if (a.K <= 128) return launch_nt<4, EPI>(a, s);
+  if (a.K <= 256) return launch_nt<8, EPI>(a, s);
+  return launch_nt<16, EPI>(a, s);
+}
+
+}  // namespace
+
+bool gemm_nt_supported(int64_t K, int64_t N) { return K <= 512 && K % 8 == 0 && N % 8 == 0; }
+
+dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N <= 0) return DCNR_OK;
+  if (!gemm_nt_supported(a.K, a.N) || a.ldx % 8 || a.ldw % 8 || a.ldc % 8 ||
+      (epi == NT_EPI_RESID && a.ldr % 8)) {
+    set_error("gemm_nt: unsupported K=%d N=%d", a.K, a.N);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  switch (epi) {
+    case NT_EPI_BIAS: return dispatch_k<NT_EPI_BIAS>(a, s);
+    case NT_EPI_F32: return dispatch_k<NT_EPI_F32>(a, s);
+    case NT_EPI_RESID: return dispatch_k<NT_EPI_RESID>(a, s);
+  }
+  set_error("gemm_nt: bad epilogue");
+  return DCNR_BAD_ARG;
+}
+
+}  // namespace dcnr
