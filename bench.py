@@ -56,7 +56,7 @@ def make_batch(gen, B, dev):
     return user, item, cat, num, y
 
 
-def cpu_baseline(B_cpu=8192, steps=2):
+def cpu_baseline(B_cpu=32768, steps=4):
     """The oracle (numpy fp32 restatement of train.py:155-226) timed on the
     host: forward + BCE + backward + AdamW on a bounded sample of the same
     workload.  Reported only; not the optimisation target."""
@@ -139,6 +139,19 @@ def main():
 
     for k in range(args.warmup):
         trainer.step(*pool[k % len(pool)])
+    # the same K steps without the per-launch HIP events (instrumentation cost check)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        trainer.step(*pool[k % len(pool)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el_plain = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el_plain, op=dist.ReduceOp.MAX)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -199,6 +212,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3,
+            "ms_per_step_uninstrumented": float(el_plain.item()) / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

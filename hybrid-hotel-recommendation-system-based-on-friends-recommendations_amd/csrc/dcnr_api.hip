@@ -171,6 +171,7 @@ struct Layout {
   float* zc; float* zdeep;
   BnBufs bn[2 * MAX_RES];
   float* part; double* sums; float* coef;
+  double* red2; int* red_cnt;   // reduce_fused scratch (counters zeroed by pack_all)
   // backward
   void* G; void* dt2; void* du; void* da;
   float* dx0; float* slab; int64_t slab_elems; float* cpart; size_t cpart_elems;
@@ -220,6 +221,8 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws) {
   L.part = (float*)b.take((size_t)PART_CHUNKS * 3 * d.Hp * 4);
   L.sums = (double*)b.take((size_t)(3 * d.Hp + 1) * 8);
   L.coef = (float*)b.take((size_t)3 * d.Hp * 4);
+  L.red2 = (double*)b.take((size_t)RED_G * 3 * d.Hp * 8);
+  L.red_cnt = (int*)b.take(RED_MAX_CGRP * 4);
   if (train) {
     L.G = b.take(act);
     L.dt2 = b.take(act);
@@ -336,6 +339,8 @@ dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train
     vb.push_back(p);
   };
   addb(P.b0, L.b0p);
+  // reduce_fused's column-group counters start at zero (a 1-row pack of 0 columns)
+  vb.push_back(PackDesc{P.b0, L.red_cnt, nullptr, 0, 0, RED_MAX_CGRP, 0, 1, 0});
   for (int j = 0; j < d.R; ++j) { addb(P.blk[j].b1, L.b1p[j]); addb(P.blk[j].b2, L.b2p[j]); }
   for (size_t o = 0; o < v.size(); o += MAX_PACK) {
     PackBatch pb;
@@ -413,6 +418,14 @@ dcnr_status hook(const dcnr_model_desc* desc, const Dims& d, const Layout& L, hi
   return DCNR_OK;
 }
 
+RedFinal red_init(const Layout& L, int mode, double count, int accumulate) {
+  RedFinal rf;
+  memset(&rf, 0, sizeof(rf));
+  rf.mode = mode; rf.count = count; rf.accumulate = accumulate;
+  rf.red2 = L.red2; rf.counter = L.red_cnt; rf.sums = L.sums;
+  return rf;
+}
+
 dcnr_status bn_layer_fwd(const dcnr_model_desc* desc, const Dims& d, const Layout& L,
                          const void* t, int64_t B, bool train, const float* gamma,
                          const float* beta, float* rm, float* rv, int64_t* nbt,
@@ -421,10 +434,50 @@ dcnr_status bn_layer_fwd(const dcnr_model_desc* desc, const Dims& d, const Layou
   if (train) {
     int nc = 0;
     TRYP(DCNR_K_ROWWISE, col_stats(d.prec, t, B, d.Hp, d.Hp, L.part, &nc, s));
-    TRYP(DCNR_K_REDUCE, reduce_stats(d.prec, L.part, nc, d.Hp, L.sums, (double)B, t, s));
+    if (!desc->bn_allreduce) {  // local BN: reduce + finalize in one launch
+      RedFinal rf = red_init(L, RED_BN_FWD, (double)B, 0);
+      rf.f = f;
+      TRYP(DCNR_K_REDUCE, reduce_fused(d.prec, L.part, nc, 2, d.Hp, d.H, t, rf, s));
+      return DCNR_OK;
+    }
+    RedFinal rf = red_init(L, RED_SUMS, (double)B, 0);
+    TRYP(DCNR_K_REDUCE, reduce_fused(d.prec, L.part, nc, 2, d.Hp, d.H, t, rf, s));
     TRY(hook(desc, d, L, s));
   }
   TRYP(DCNR_K_REDUCE, bn_finalize2(L.sums, d.Hp, d.H, train ? 1 : 0, f, s));
+  return DCNR_OK;
+}
+
+// BN backward reductions: part [nc][NK][Hp] -> dgamma, dbeta (+ dW_f deep half
+// when dwf != null) and coef.  Fused into one launch unless SyncBN must sum
+// the statistics across ranks first.
+dcnr_status bn_bwd_reduce(const dcnr_model_desc* desc, const Dims& d, const Layout& L, int nc,
+                          int NK, int64_t B, const float* gamma, const float* invstd,
+                          float* dgamma, float* dbeta, float* dwf, int accumulate, hipStream_t s) {
+  const int Hp = d.Hp, H = d.H;
+  if (!desc->bn_allreduce) {
+    RedFinal rf = red_init(L, RED_BN_BWD, (double)B, accumulate);
+    rf.gamma = gamma; rf.invstd = invstd; rf.dgamma = dgamma; rf.dbeta = dbeta; rf.dwf = dwf;
+    rf.coef = L.coef;
+    TRYP(DCNR_K_REDUCE, reduce_fused(DCNR_PREC_FP32, L.part, nc, NK, Hp, H, nullptr, rf, s));
+    return DCNR_OK;
+  }
+  RedFinal rf = red_init(L, RED_SUMS, (double)B, 0);
+  TRYP(DCNR_K_REDUCE, reduce_fused(DCNR_PREC_FP32, L.part, nc, NK, Hp, H, nullptr, rf, s));
+  if (dwf) TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums + 2 * Hp, H, dwf, accumulate, s));
+  TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums + Hp, H, dgamma, accumulate, s));
+  TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, dbeta, accumulate, s));
+  TRY(hook(desc, d, L, s));
+  TRYP(DCNR_K_REDUCE, bn_bwd_coef(L.sums, Hp, H, gamma, invstd, L.coef, 1, s));
+  return DCNR_OK;
+}
+
+// Bias gradient: part [nc][1][Hp] -> grad[H] (never needs the hook).
+dcnr_status bias_reduce(const Dims& d, const Layout& L, int nc, float* grad, int accumulate,
+                        hipStream_t s) {
+  RedFinal rf = red_init(L, RED_BIAS, 0.0, accumulate);
+  rf.grad = grad;
+  TRYP(DCNR_K_REDUCE, reduce_fused(DCNR_PREC_FP32, L.part, nc, 1, d.Hp, d.H, nullptr, rf, s));
   return DCNR_OK;
 }
 
@@ -540,16 +593,12 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     // ---- out = relu(BN2(t2) + h_j):  du, BN2 backward
     TRYP(DCNR_K_ROWWISE, bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, B, Hp,
                        Hp, L.part, &nc, s));
-    TRYP(DCNR_K_REDUCE, reduce_partials_nk(L.part, nc, 3, Hp, L.sums, (double)B, s));
-    if (!Gin) TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums + 2 * Hp, H, Gr.wf, accumulate, s));  // dW_f[:H]
-    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums + Hp, H, Gk.g2, accumulate, s));               // dgamma2
-    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, Gk.be2, accumulate, s));                   // dbeta2
-    TRY(hook(desc, d, L, s));
-    TRYP(DCNR_K_REDUCE, bn_bwd_coef(L.sums, Hp, H, Bk.g2, bn2.invstd, L.coef, 1, s));
+    // dbeta2, dgamma2 and (last block only) dW_f[:H]
+    TRY(bn_bwd_reduce(desc, d, L, nc, 3, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, Gin ? nullptr : Gr.wf,
+                      accumulate, s));
     TRYP(DCNR_K_ROWWISE, bwd_bn2_apply2(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, L.coef,
                        B, Hp, Hp, L.dt2, L.du, L.part, &nc, s));
-    TRYP(DCNR_K_REDUCE, reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
-    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, Gk.b2, accumulate, s));                    // dbias2
+    TRY(bias_reduce(d, L, nc, Gk.b2, accumulate, s));  // dbias2
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
     TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], L.a1, B, Hp, Hp, bn1.scale, bn1.shift, p, dropout_seed, j, s));
     TRY(linear_dw(d, L, L.dt2, Hp, Hp, L.a1, Hp, Hp, B, Gk.w2, H, H, accumulate, s));
@@ -563,15 +612,11 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     // ---- relu/dropout + BN1 backward
     TRYP(DCNR_K_ROWWISE, bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean, bn1.invstd, B, Hp, Hp,
                       p, dropout_seed, j, L.part, &nc, s));
-    TRYP(DCNR_K_REDUCE, reduce_partials_nk(L.part, nc, 2, Hp, L.sums, (double)B, s));
-    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums + Hp, H, Gk.g1, accumulate, s));
-    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, Gk.be1, accumulate, s));
-    TRY(hook(desc, d, L, s));
-    TRYP(DCNR_K_REDUCE, bn_bwd_coef(L.sums, Hp, H, Bk.g1, bn1.invstd, L.coef, 1, s));
+    TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, accumulate,
+                      s));
     TRYP(DCNR_K_ROWWISE, bwd_bn1_apply2(d.prec, L.da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, L.a1,
                        L.part, &nc, s));
-    TRYP(DCNR_K_REDUCE, reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
-    TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, Gk.b1, accumulate, s));
+    TRY(bias_reduce(d, L, nc, Gk.b1, accumulate, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
     TRY(linear_dw(d, L, L.a1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s));
     {
@@ -587,8 +632,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   // ---- initial layer
   int nc = 0;
   TRYP(DCNR_K_ROWWISE, col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
-  TRYP(DCNR_K_REDUCE, reduce_partials_nk(L.part, nc, 1, Hp, L.sums, (double)B, s));
-  TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, Gr.b0, accumulate, s));
+  TRY(bias_reduce(d, L, nc, Gr.b0, accumulate, s));
   TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s));
   {
     GemmArgs g;
@@ -671,6 +715,22 @@ dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t
   }
   hipStream_t s = (hipStream_t)stream;
   TRYP(DCNR_K_KNN, cosine_topk(table, inv_norms, N, d, queries, Q, k, idx, dist, ws, ws_bytes, s));
+  return DCNR_OK;
+}
+
+dcnr_status dcnr_linear_bf16(const void* X, int64_t ldx, int64_t M, int32_t K, const void* W,
+                             int64_t ldw, int32_t N, const float* bias, void* C, int64_t ldc,
+                             int out_f32, dcnr_stream_t stream) {
+  if (!X || !W || !C || M < 0 || K < 1 || N < 1) {
+    set_error("dcnr_linear_bf16: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  GemmArgs g;
+  memset(&g, 0, sizeof(g));
+  g.A = X; g.lda = ldx; g.B = W; g.ldb = ldw; g.C = C; g.ldc = ldc; g.bias = bias;
+  g.M = M; g.N = N; g.K = K; g.k_per_split = K; g.out_f32 = out_f32 ? 1 : 0;
+  TRYP(DCNR_K_GEMM_FWD, gemm_nn(DCNR_PREC_BF16, EPI_STORE, g, 1, s));
   return DCNR_OK;
 }
 

@@ -50,6 +50,42 @@ template <> struct St<bf16> {
   static __device__ __forceinline__ void st(bf16* p, float v) { *p = (bf16)v; }
 };
 
+// ------------------------------------------------ buffer loads / hand-off
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+constexpr int OOR = 0x7fffff00;  // a buffer offset past num_records: loads 0, stores dropped
+
+// Raw buffer descriptor over [p, p + bytes) (bytes < 2^31).  Out-of-range
+// offsets load 0 with no branch, so unrolled load batches stay branch-free.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, p ? (int)bytes : 0, 0x00020000);
+}
+
+// Split-reduction hand-off (cdna_hip_programming.md, "In-launch split-K
+// reduction"): every block stores its partial with plain stores and calls
+// this; it returns true in exactly one block, the last arriver, which may
+// then read all partials with plain loads.  `flag` is an int in the block's
+// LDS.  The counter is zero at rest (re-zeroed by the last arriver; zeroed
+// per forward by pack_all before first use).
+__device__ __forceinline__ bool last_arriver(int* counter, int n_arrivals, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int prev = __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = prev == n_arrivals - 1;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *flag = last;
+  }
+  __syncthreads();
+  return *flag != 0;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -163,12 +199,7 @@ dcnr_status col_stats(int precision, const void* t, int64_t B, int N, int ld, fl
                       int* nchunks, hipStream_t s);                  // NK=2: t, t^2
 dcnr_status col_sum(int precision, const void* x, int64_t B, int N, int ld, float* part,
                     int* nchunks, hipStream_t s);                    // NK=1
-dcnr_status reduce_partials_nk(const float* part, int nchunks, int NK, int N, double* sums,
-                               double count, hipStream_t s);
-// BN batch statistics: col_stats partials are shifted by K = t[0][n]; this
-// reduces them and converts to unshifted fp64 [sum t, sum t^2] + count.
-dcnr_status reduce_stats(int precision, const float* part, int nchunks, int N, double* sums,
-                         double count, const void* t, hipStream_t s);
+// (col_stats partials are shifted by K = t[0][n]; reduce_fused unshifts them.)
 
 struct BnFinal {   // per BN layer
   const float* gamma; const float* beta; float* rmean; float* rvar; int64_t* nbt;
@@ -178,6 +209,23 @@ struct BnFinal {   // per BN layer
 // N = padded width, Nr = real width (parameters have Nr entries; pads -> 0)
 dcnr_status bn_finalize2(const double* sums, int N, int Nr, int train, const BnFinal& f,
                          hipStream_t s);
+// Fused reduce + consumer (used when no SyncBN hook must see the sums)
+enum RedMode : int { RED_BN_FWD = 0, RED_BN_BWD = 1, RED_BIAS = 2, RED_SUMS = 3 };
+constexpr int RED_G = 32;          // chunk groups per column group
+constexpr int RED_MAX_CGRP = 64;   // column groups of 64 -> N <= 4096
+struct RedFinal {
+  int mode; int accumulate; double count;
+  double* red2;                                // workspace [RED_G][3][N] fp64
+  int* counter;                                // workspace [RED_MAX_CGRP], zero at rest
+  double* sums;                                // RED_SUMS: [3][N] + count
+
+  BnFinal f;                                   // RED_BN_FWD (train)
+  const float* gamma; const float* invstd;     // RED_BN_BWD
+  float* dgamma; float* dbeta; float* dwf; float* coef;
+  float* grad;                                 // RED_BIAS
+};
+dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, int N, int Nr,
+                         const void* shift, const RedFinal& rf, hipStream_t s);
 // coef[3][N] for dt = coef0*dy - coef1*xhat - coef2
 dcnr_status bn_bwd_coef(const double* sums, int N, int Nr, const float* gamma, const float* invstd,
                         float* coef, int train, hipStream_t s);

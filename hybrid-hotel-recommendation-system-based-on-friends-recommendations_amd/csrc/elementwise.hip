@@ -313,47 +313,6 @@ template <typename T> struct Bwd1ApplyOp {
 };
 
 // ------------------------------------------------------------ small kernels
-// part [nchunks][NK][N] f32 -> sums [3][N] f64 (components >= NK zeroed) + count
-// at [3N].  Block = 8 columns x 32 chunk-lanes, all NK components of a column in
-// one block; fixed-order tree -> deterministic.  With `shift` (the stats pass's
-// K = t[0]) the shifted sums S0' = sum(t-K), S1' = sum((t-K)^2) are converted
-// to S0 = S0' + nK, S1 = S1' + 2K S0' + nK^2 (fp64), so SyncBN can add them.
-template <typename T>
-__global__ __launch_bounds__(NT) void reduce_partials_kernel(const float* part, int nchunks, int NK,
-                                                             int N, double* sums, double count,
-                                                             const T* shift) {
-  __shared__ double red[3][32][8];
-  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
-  const int n = blockIdx.x * 8 + tx;
-  double s[3] = {0.0, 0.0, 0.0};
-  if (n < N)
-    for (int c = ty; c < nchunks; c += 32)
-#pragma unroll
-      for (int k = 0; k < 3; ++k)
-        if (k < NK) s[k] += (double)part[((int64_t)c * NK + k) * N + n];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) red[k][ty][tx] = s[k];
-  __syncthreads();
-  for (int o = 16; o > 0; o >>= 1) {
-    if (ty < o)
-#pragma unroll
-      for (int k = 0; k < 3; ++k) red[k][ty][tx] += red[k][ty + o][tx];
-    __syncthreads();
-  }
-  if (ty == 0 && n < N) {
-    double v0 = red[0][0][tx], v1 = red[1][0][tx], v2 = red[2][0][tx];
-    if (shift) {
-      double K = (double)(float)shift[n];
-      v1 = v1 + 2.0 * K * v0 + count * K * K;
-      v0 = v0 + count * K;
-    }
-    sums[n] = v0;
-    sums[N + n] = v1;
-    sums[2 * N + n] = v2;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) sums[3 * N] = count;
-}
-
 __global__ void bn_finalize_kernel(const double* sums, int N, int Nr, int train, BnFinal f) {
   int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
@@ -439,16 +398,150 @@ __global__ void pack_kernel(PackBatch pb) {
   }
 }
 
+// Column reduction of per-chunk partials part [nchunks][NK][N] (f32) in fp64,
+// fused with its consumer.  Grid = (N/64 column groups) x RED_G chunk groups:
+// each block sums its chunk range for 64 columns (256 B coalesced rows, 4
+// chunk lanes), writes an fp64 block partial to rf.red2 [RED_G][3][N], and the
+// last block of each column group (device-scope counter, self-resetting) adds
+// the RED_G partials in fixed order and finalises: deterministic, one launch.
+// With `shift` (the stats pass's K = t[0]) the shifted sums S0' = sum(t-K),
+// S1' = sum((t-K)^2) become S0 = S0' + nK, S1 = S1' + 2K S0' + nK^2.
 template <typename T>
-dcnr_status launch_reduce(const float* part, int nchunks, int NK, int N, double* sums,
-                          double count, const T* shift, hipStream_t s) {
-  hipLaunchKernelGGL(reduce_partials_kernel<T>, dim3((unsigned)cdiv(std::max(N, 1), 8)),
-                     dim3(NT), 0, s, part, nchunks, NK, N, sums, count, shift);
-  DCNR_LAUNCH_CHECK();
-  return DCNR_OK;
+__global__ __launch_bounds__(NT) void reduce_fused_kernel(const float* part, int nchunks, int NK,
+                                                          int N, int Nr, const T* shift,
+                                                          RedFinal rf) {
+  __shared__ double red[4 * 3 * 64 + 1];   // one LDS object (the hand-off flag lives in it)
+  int* flag = reinterpret_cast<int*>(&red[4 * 3 * 64]);
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int cgrp = blockIdx.x, g = blockIdx.y;
+  const int n = cgrp * 64 + tx;
+  const int per = (nchunks + RED_G - 1) / RED_G;
+  const int c0 = g * per, c1 = min(nchunks, c0 + per);
+  // stage 1: this block's chunk range, 8 chunk rows x NK loads in flight per
+  // lane; out-of-range elements come back as 0 from the buffer descriptor
+  // (no per-element branch, which would serialise the loads)
+  const __amdgpu_buffer_rsrc_t pr = buf_rsrc(part, (int64_t)nchunks * NK * N * 4);
+  constexpr int U = 8;
+  double s[3] = {0.0, 0.0, 0.0};
+  for (int c = c0 + ty; c < c1; c += 4 * U) {
+    float v[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int cc = c + 4 * u;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const bool ok = n < N && cc < c1 && k < NK;
+        v[u][k] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+            pr, ok ? ((cc * NK + k) * N + n) * 4 : OOR, 0, 0));
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) s[k] += (double)v[u][k];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) red[(ty * 3 + k) * 64 + tx] = s[k];
+  __syncthreads();
+  if (ty == 0 && n < N)
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+      rf.red2[((int64_t)g * 3 + k) * N + n] =
+          ((red[k * 64 + tx] + red[(3 + k) * 64 + tx]) + red[(6 + k) * 64 + tx]) + red[(9 + k) * 64 + tx];
+  if (!last_arriver(&rf.counter[cgrp], RED_G, flag)) return;
+  // stage 2 (last block of this column group): lane ty sums groups
+  // ty*QP .. ty*QP+QP-1 (all loads issued first), then a fixed-order combine
+  constexpr int QP = RED_G / 4;
+  const __amdgpu_buffer_rsrc_t r2r = buf_rsrc(rf.red2, (int64_t)RED_G * 3 * N * 8);
+  {
+    double w[QP][3];
+#pragma unroll
+    for (int q = 0; q < QP; ++q)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const bool ok = n < N && k < NK;
+        u32x2 raw = __builtin_amdgcn_raw_buffer_load_b64(
+            r2r, ok ? (((ty * QP + q) * 3 + k) * N + n) * 8 : OOR, 0, 0);
+        w[q][k] = __builtin_bit_cast(double, raw);
+      }
+    double t3[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < QP; ++q)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) t3[k] += w[q][k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 3; ++k) red[(ty * 3 + k) * 64 + tx] = t3[k];
+    __syncthreads();
+  }
+  if (ty != 0 || n >= N) return;
+  double v0 = ((red[0 * 64 + tx] + red[3 * 64 + tx]) + red[6 * 64 + tx]) + red[9 * 64 + tx];
+  double v1 = ((red[1 * 64 + tx] + red[4 * 64 + tx]) + red[7 * 64 + tx]) + red[10 * 64 + tx];
+  double v2 = ((red[2 * 64 + tx] + red[5 * 64 + tx]) + red[8 * 64 + tx]) + red[11 * 64 + tx];
+  const double cnt = rf.count;
+  const bool real = n < Nr;
+  if (shift) {  // unshift
+    double K = (double)(float)shift[n];
+    v1 = v1 + 2.0 * K * v0 + cnt * K * K;
+    v0 = v0 + cnt * K;
+  }
+  if (rf.mode == RED_SUMS) {  // raw sums for the SyncBN hook (+ count at [3N])
+    rf.sums[n] = v0;
+    rf.sums[N + n] = v1;
+    rf.sums[2 * N + n] = v2;
+    if (n == 0) rf.sums[3 * N] = cnt;
+  } else if (rf.mode == RED_BN_FWD) {
+    const BnFinal& f = rf.f;
+    if (!real) {
+      f.scale[n] = 0.f; f.shift[n] = 0.f; f.mean[n] = 0.f; f.invstd[n] = 0.f;
+      return;
+    }
+    double mean = v0 / cnt;
+    double var = v1 / cnt - mean * mean;
+    if (var < 0) var = 0;
+    f.rmean[n] = (float)((1.0 - BN_MOM) * (double)f.rmean[n] + BN_MOM * mean);
+    f.rvar[n] = (float)((1.0 - BN_MOM) * (double)f.rvar[n] + BN_MOM * var * cnt / (cnt - 1.0));
+    if (n == 0 && f.nbt) f.nbt[0] += 1;
+    float inv = (float)(1.0 / sqrt(var + (double)BN_EPS));
+    float sc = f.gamma[n] * inv;
+    f.scale[n] = sc;
+    f.shift[n] = f.beta[n] - (float)mean * sc;
+    f.mean[n] = (float)mean;
+    f.invstd[n] = inv;
+  } else if (rf.mode == RED_BN_BWD) {
+    // v0 = sum dy, v1 = sum dy*xhat, v2 = sum dz*out (deep half of dW_f)
+    const float a = real ? rf.gamma[n] * rf.invstd[n] : 0.f;
+    rf.coef[n] = a;
+    rf.coef[N + n] = (float)((double)a * v1 / cnt);
+    rf.coef[2 * N + n] = (float)((double)a * v0 / cnt);
+    if (real) {
+      rf.dgamma[n] = rf.accumulate ? rf.dgamma[n] + (float)v1 : (float)v1;
+      rf.dbeta[n] = rf.accumulate ? rf.dbeta[n] + (float)v0 : (float)v0;
+      if (rf.dwf) rf.dwf[n] = rf.accumulate ? rf.dwf[n] + (float)v2 : (float)v2;
+    }
+  } else {  // RED_BIAS
+    if (real) rf.grad[n] = rf.accumulate ? rf.grad[n] + (float)v0 : (float)v0;
+  }
 }
 
 }  // namespace
+
+dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, int N, int Nr,
+                         const void* shift, const RedFinal& rf, hipStream_t s) {
+  if (N <= 0 || N > 64 * RED_MAX_CGRP || NK < 1 || NK > 3) {
+    set_error("reduce: unsupported width %d / components %d", N, NK);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  dim3 grid((unsigned)cdiv(N, 64), RED_G);
+  if (precision == DCNR_PREC_BF16)
+    hipLaunchKernelGGL(reduce_fused_kernel<bf16>, grid, dim3(NT), 0, s, part, nchunks, NK, N, Nr,
+                       (const bf16*)shift, rf);
+  else
+    hipLaunchKernelGGL(reduce_fused_kernel<float>, grid, dim3(NT), 0, s, part, nchunks, NK, N, Nr,
+                       (const float*)shift, rf);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
 
 // ================================================================== API
 dcnr_status pack_weights(int precision, const PackBatch& pb, hipStream_t s) {
@@ -472,13 +565,6 @@ dcnr_status col_stats(int precision, const void* t, int64_t B, int N, int ld, fl
                                      : col_stats_impl<float>(t, B, N, ld, part, nchunks, s);
 }
 
-dcnr_status reduce_stats(int precision, const float* part, int nchunks, int N, double* sums,
-                         double count, const void* t, hipStream_t s) {
-  return precision == DCNR_PREC_BF16
-             ? launch_reduce<bf16>(part, nchunks, 2, N, sums, count, (const bf16*)t, s)
-             : launch_reduce<float>(part, nchunks, 2, N, sums, count, (const float*)t, s);
-}
-
 template <typename T>
 static dcnr_status col_sum_impl(const void* x, int64_t B, int N, int ld, float* part, int* nc,
                                 hipStream_t s) {
@@ -489,11 +575,6 @@ dcnr_status col_sum(int precision, const void* x, int64_t B, int N, int ld, floa
                     int* nchunks, hipStream_t s) {
   return precision == DCNR_PREC_BF16 ? col_sum_impl<bf16>(x, B, N, ld, part, nchunks, s)
                                      : col_sum_impl<float>(x, B, N, ld, part, nchunks, s);
-}
-
-dcnr_status reduce_partials_nk(const float* part, int nchunks, int NK, int N, double* sums,
-                               double count, hipStream_t s) {
-  return launch_reduce<float>(part, nchunks, NK, N, sums, count, nullptr, s);
 }
 
 dcnr_status bn_finalize2(const double* sums, int N, int Nr, int train, const BnFinal& f,

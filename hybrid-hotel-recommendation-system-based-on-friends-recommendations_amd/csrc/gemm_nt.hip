@@ -38,9 +38,6 @@ template <int KTP> struct NtCfg {
 template <int WCH>
 __device__ __forceinline__ int w_slot(int row, int ch) { return row * WCH + (ch ^ (row & 15)); }
 
-typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
-typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
-constexpr int OOR = 0x7fffff00;  // a buffer offset past num_records: loads 0, stores dropped
 
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
   bf16 x = (bf16)a, y = (bf16)b;
@@ -106,9 +103,8 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int n = n0 + j * 16 + (lane >> 4) * 4;
-    u32x4 b4 = {0u, 0u, 0u, 0u};
-    if constexpr (EPI == NT_EPI_BIAS)
-      b4 = __builtin_amdgcn_raw_buffer_load_b128(br, n < a.N ? n * 4 : OOR, 0, 0);
+    // null bias -> descriptor of 0 records -> the load returns zeros (any epilogue)
+    u32x4 b4 = __builtin_amdgcn_raw_buffer_load_b128(br, n < a.N ? n * 4 : OOR, 0, 0);
 #pragma unroll
     for (int r = 0; r < 4; ++r) bias[j][r] = __uint_as_float(b4[r]);
   }

@@ -97,6 +97,8 @@ class DCN_RecSys(nn.Module):
                           n_cross=n_cross_layers, n_res=n_res_blocks, dropout=float(dropout),
                           input_dim=input_dim)
         self.bn_allreduce = None   # set by dcnr.parallel for SyncBN
+        self._sync_bn_hook = None
+        self._active_ws = None
         self._flat = None
 
     # ------------------------------------------------------------ native glue
@@ -196,6 +198,13 @@ class DCN_RecSys(nn.Module):
         return flat, gflat
 
 
+def _hook_error(model):
+    hook = getattr(model, "_sync_bn_hook", None)
+    if hook is not None and hook.error is not None:
+        e, hook.error = hook.error, None
+        raise RuntimeError("SyncBN all-reduce hook failed") from e
+
+
 def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
                 ws: Optional[torch.Tensor] = None):
     lib = _lib.load()
@@ -208,10 +217,13 @@ def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
     logits = torch.empty(B, dtype=torch.float32, device=dev)
     state = _lib.ptr_array(model.state_tensors())
     desc = model.desc()
+    model._active_ws = ws          # the SyncBN hook (dcnr.parallel) maps pointers into it
     st = lib.dcnr_forward(ctypes.byref(desc), state, user.data_ptr(), item.data_ptr(),
                           cat.data_ptr() if cat.numel() else None,
                           num.data_ptr() if num.numel() else None, B, mode, seed,
                           logits.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev))
+    model._active_ws = None
+    _hook_error(model)
     _lib.check(st, "dcnr_forward")
     if model.check_indices:
         _lib.check(lib.dcnr_check_errors(ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)),
@@ -225,12 +237,15 @@ def run_backward(model: DCN_RecSys, user, item, cat, num, dlogits, ws, grads: Li
     lib = _lib.load()
     B = user.shape[0]
     desc = model.desc()
+    model._active_ws = ws
     st = lib.dcnr_backward(ctypes.byref(desc), _lib.ptr_array(model.state_tensors()),
                            _lib.ptr_array(grads), user.data_ptr(), item.data_ptr(),
                            cat.data_ptr() if cat.numel() else None,
                            num.data_ptr() if num.numel() else None, B,
                            dlogits.data_ptr(), int(seed), 1 if accumulate else 0, ws.data_ptr(),
                            ws.numel(), _lib.stream_ptr(user.device))
+    model._active_ws = None
+    _hook_error(model)
     _lib.check(st, "dcnr_backward")
 
 

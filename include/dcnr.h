@@ -161,6 +161,15 @@ dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t
                              const float* queries, int64_t Q, int32_t k, int64_t* idx,
                              float* dist, void* ws, size_t ws_bytes, dcnr_stream_t stream);
 
+/* The deep tower's Linear layer as a standalone bf16 call (nn.Linear forward,
+ * train.py:143,105,109): C[M,N] = X[M,K] . W[N,K]^T + bias, X/W bf16
+ * row-major (K, ldx, ldw multiples of 8), C bf16 (out_f32 = 0) or fp32.
+ * Used by the deep tower internally; exported for unit tests and kernel
+ * benchmarks. */
+dcnr_status dcnr_linear_bf16(const void* X, int64_t ldx, int64_t M, int32_t K, const void* W,
+                             int64_t ldw, int32_t N, const float* bias, void* C, int64_t ldc,
+                             int out_f32, dcnr_stream_t stream);
+
 /* Kernel-timing instrumentation (measurement only, off by default): when
  * enabled, every launch the library makes is bracketed by HIP events on its
  * stream and attributed to one of these classes. */

@@ -1,0 +1,178 @@
+"""Data-parallel path on CPU: world_size-2 gloo process groups (the GPU box runs
+the same code over RCCL).  Covers the batch split, the flat-gradient exchange
+convention (BCE grad pre-scaled by 1/world, SUM all-reduce == global mean) and
+the SyncBN hook (pointer -> workspace view -> all-reduce) including the
+statistics protocol libdcnr hands it (shifted sums unshifted, + count)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import dcnr_oracle as orc
+from dcnr import parallel
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+
+def _run(fn, world=2):
+    port = _free_port()
+    mp.spawn(fn, args=(world, port), nprocs=world, join=True)
+
+
+def test_shard_range():
+    assert parallel.shard_range(10, 0, 2) == (0, 5)
+    assert parallel.shard_range(10, 1, 2) == (5, 10)
+    assert parallel.shard_range(11, 1, 2) == (5, 10)   # ragged tail dropped
+    lo_hi = [parallel.shard_range(131072 * 8, r, 8) for r in range(8)]
+    assert lo_hi[0][0] == 0 and lo_hi[-1][1] == 131072 * 8
+    assert all(a[1] == b[0] for a, b in zip(lo_hi, lo_hi[1:]))
+    with pytest.raises(ValueError):
+        parallel.shard_range(4, 2, 2)
+
+
+class _FakeModel:
+    _active_ws = None
+    bn_allreduce = None
+
+
+def _hook_worker(rank, world, port):
+    _init(rank, world, port)
+    try:
+        model = _FakeModel()
+        hook = parallel.install_sync_bn(model)
+        ws = torch.zeros(4096, dtype=torch.uint8)
+        H = 24
+        off = 512  # 256-aligned like libdcnr's bump allocator
+        buf = ws[off:off + (3 * H + 1) * 8].view(torch.float64)
+        rng = np.random.default_rng(rank)
+        vals = rng.standard_normal(3 * H + 1)
+        buf.copy_(torch.from_numpy(vals))
+        model._active_ws = ws
+        # through the ctypes thunk exactly as libdcnr calls it
+        rc = hook.cfunc(None, ws.data_ptr() + off, 3 * H + 1, None)
+        assert rc == 0 and hook.error is None and hook.calls == 1
+        want = sum(np.random.default_rng(r).standard_normal(3 * H + 1) for r in range(world))
+        np.testing.assert_allclose(buf.numpy(), want, rtol=0, atol=1e-12)
+        # a pointer outside the active workspace is reported, not crashed on
+        rc = hook.cfunc(None, ws.data_ptr() + 8192, 4, None)
+        assert rc == 1 and isinstance(hook.error, RuntimeError)
+        model._active_ws = None
+        parallel.remove_sync_bn(model)
+        assert model.bn_allreduce is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sync_bn_hook_gloo_world2():
+    _run(_hook_worker)
+
+
+def _stats_worker(rank, world, port):
+    """SyncBN protocol: each rank produces [S0, S1, -, count] from ITS shard the
+    way libdcnr does (sums shifted by the shard's first row, unshifted in fp64);
+    after the hook's SUM the finalize (mean = S0/n, var = S1/n - mean^2) must
+    equal BatchNorm statistics of the concatenated global batch."""
+    _init(rank, world, port)
+    try:
+        B, H = 64, 16
+        rng = np.random.default_rng(7)
+        t_all = (rng.standard_normal((B * world, H)) * 0.3 + 50.0).astype(np.float32)
+        lo, hi = parallel.shard_range(B * world, rank, world)
+        t = t_all[lo:hi]
+        K = t[0].astype(np.float64)
+        d = t.astype(np.float64) - K
+        s0p, s1p = d.sum(0), (d * d).sum(0)
+        n = float(hi - lo)
+        s1 = s1p + 2 * K * s0p + n * K * K
+        s0 = s0p + n * K
+        buf = torch.from_numpy(np.concatenate([s0, s1, np.zeros(H), [n]]))
+        dist.all_reduce(buf)
+        v = buf.numpy()
+        cnt = v[3 * H]
+        mean = v[:H] / cnt
+        var = v[H:2 * H] / cnt - mean * mean
+        np.testing.assert_allclose(cnt, B * world)
+        np.testing.assert_allclose(mean, t_all.astype(np.float64).mean(0), rtol=1e-12)
+        np.testing.assert_allclose(var, t_all.astype(np.float64).var(0), rtol=1e-6)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_sync_bn_statistics_protocol_gloo_world2():
+    _run(_stats_worker)
+
+
+def _random_params(spec, rng):
+    """Random fp32 parameters keyed like the reference state_dict (train.py:136-153)."""
+    D = orc.input_dim(spec.emb_dim, spec.cat_dims, spec.n_num)
+    H = spec.hidden
+    r = lambda *s: (rng.standard_normal(s) * 0.3).astype(np.float32)
+    p = {"user_embedding.weight": r(spec.n_users, spec.emb_dim),
+         "item_embedding.weight": r(spec.n_items, spec.emb_dim)}
+    for k, n in enumerate(spec.cat_dims):
+        p[f"cat_embeddings.{k}.weight"] = r(n, orc.cat_width(n))
+    p["initial_deep_layer.weight"], p["initial_deep_layer.bias"] = r(H, D), r(H)
+    for j in range(spec.n_res):
+        for l in (1, 2):
+            pre = f"res_blocks.{j}"
+            p[f"{pre}.layer{l}.weight"], p[f"{pre}.layer{l}.bias"] = r(H, H), r(H)
+            p[f"{pre}.bn{l}.weight"], p[f"{pre}.bn{l}.bias"] = 1 + r(H), r(H)
+            p[f"{pre}.bn{l}.running_mean"] = r(H)
+            p[f"{pre}.bn{l}.running_var"] = (1 + np.abs(r(H))).astype(np.float32)
+            p[f"{pre}.bn{l}.num_batches_tracked"] = np.array(0)
+    for l in range(spec.n_cross):
+        p[f"cross_network.{l}.b"], p[f"cross_network.{l}.w.weight"] = r(D), r(1, D)
+    p["final_linear.weight"], p["final_linear.bias"] = r(1, H + D), r(1)
+    return p
+
+
+def _grad_worker(rank, world, port):
+    """Gradient exchange convention of FusedTrainer.step on the oracle model:
+    every rank backpropagates (1/world) * mean-BCE of its shard; the SUM
+    all-reduce of the flat gradient must equal the mean of the per-rank
+    gradients, and with BN in eval mode (no batch coupling) the gradient of
+    the global-batch loss."""
+    _init(rank, world, port)
+    try:
+        spec = orc.ModelSpec(n_users=50, n_items=40, cat_dims=[7, 30], n_num=3, emb_dim=4,
+                             hidden=16, n_cross=2, n_res=1, dropout=0.0)
+        params = _random_params(spec, np.random.default_rng(3))
+        rng = np.random.default_rng(11)
+        Bg = 32
+        user = rng.integers(0, 50, Bg); item = rng.integers(0, 40, Bg)
+        cat = np.stack([rng.integers(0, 7, Bg), rng.integers(0, 30, Bg)], 1)
+        num = rng.random((Bg, 3)); y = (rng.random(Bg) < 0.4).astype(np.float64)
+        lo, hi = parallel.shard_range(Bg, rank, world)
+
+        def grads(sl, scale):
+            z, cache = orc.forward(params, spec, user[sl], item[sl], cat[sl], num[sl], train=False)
+            _, dz = orc.bce_with_logits(z, y[sl])
+            g = orc.backward(params, spec, cache, dz * scale, user[sl], item[sl], cat[sl])
+            return np.concatenate([g[k].reshape(-1) for k in sorted(g)])
+
+        local = torch.from_numpy(grads(slice(lo, hi), 1.0 / world))
+        dist.all_reduce(local)
+        full = grads(slice(0, Bg), 1.0)
+        np.testing.assert_allclose(local.numpy(), full, rtol=1e-9, atol=1e-12)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_gradient_exchange_gloo_world2():
+    _run(_grad_worker)

@@ -356,3 +356,77 @@ def test_training_reduces_loss(dev, precision):
         losses.append(float(tr.step(u, i, c, n, y)))
     assert all(np.isfinite(losses))
     assert np.mean(losses[-5:]) < 0.7 * np.mean(losses[:5]), losses
+
+
+def test_sync_bn_hook_world1_matches_local_bn(dev):
+    """SyncBN path (hook between the BN reductions and their consumers, RCCL
+    all-reduce of the fp64 statistics) at world size 1 must reproduce local
+    BN: same logits, grads and running stats; 4 hook calls per residual block."""
+    import socket
+    import torch.distributed as dist
+    import dcnr
+    from dcnr import parallel
+    s = socket.socket(); s.bind(("127.0.0.1", 0)); port = s.getsockname()[1]; s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        cfg = gc.CFG3R
+        m1 = our_model(cfg).to(dev)
+        m2 = copy.deepcopy(m1)
+        hook = parallel.install_sync_bn(m2)
+        u, i, c, n, y = gc.make_inputs(cfg, 777, 31)
+        z1, l1, g1 = run_train(m1, dev, u, i, c, n, y)
+        z2, l2, g2 = run_train(m2, dev, u, i, c, n, y)
+        R = cfg["params"]["n_res_blocks"]
+        assert hook.calls == 4 * R
+        np.testing.assert_allclose(z2, z1, rtol=1e-6, atol=1e-6)
+        assert abs(l1 - l2) <= 1e-6
+        for k in g1:
+            np.testing.assert_allclose(g2[k], g1[k], rtol=1e-4, atol=1e-6, err_msg=k)
+        for (k, a), (_, b) in zip(m1.state_dict().items(), m2.state_dict().items()):
+            np.testing.assert_allclose(b.cpu().double().numpy(), a.cpu().double().numpy(),
+                                       rtol=1e-6, atol=1e-7, err_msg=k)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_cosine_knn_vs_sklearn_golden(dev):
+    """dcnr.NearestNeighbors (cosine, brute) vs the reference's sklearn index
+    (main.py:268-270, 200, 300) on the planted-ties table of F6."""
+    import dcnr
+    fx = golden("f6_knn.npz")
+    table, q_rows = gc.knn_table()
+    nn_ = dcnr.NearestNeighbors(metric="cosine", algorithm="brute").fit(table)
+    for k in (11, 51):
+        d, i = nn_.kneighbors(table[q_rows], n_neighbors=k)
+        np.testing.assert_allclose(d, fx[f"d{k}"], rtol=0, atol=2e-6)
+        for r in range(len(q_rows)):
+            ref_d, ref_i = fx[f"d{k}"][r], fx[f"i{k}"][r]
+            inner = ref_d < ref_d[-1] - 2e-6
+            assert set(ref_i[inner]) <= set(i[r].tolist())
+            # same position for every neighbour not within fp32 noise of another
+            near = np.diff(ref_d) <= 2e-6
+            isolated = np.ones(k, bool)
+            isolated[1:] &= ~near
+            isolated[:-1] &= ~near
+            np.testing.assert_array_equal(i[r][isolated], ref_i[isolated])
+
+
+@pytest.mark.parametrize("M,K,N,out_f32", [(4096, 512, 512, 0), (1000, 456, 512, 1),
+                                           (333, 64, 96, 0), (70000, 128, 256, 1)])
+def test_linear_bf16_vs_torch(dev, M, K, N, out_f32):
+    """dcnr_linear_bf16 (weight-resident streaming MFMA GEMM) vs a torch fp32
+    reference of the same bf16 operands; tolerance = bf16 output rounding."""
+    import ctypes
+    from dcnr import _lib
+    g = torch.Generator(device=dev).manual_seed(M + K + N)
+    X = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev, generator=g)
+    C = torch.empty(M, N, device=dev, dtype=torch.float32 if out_f32 else torch.bfloat16)
+    lib = _lib.load()
+    _lib.check(lib.dcnr_linear_bf16(X.data_ptr(), K, M, K, W.data_ptr(), K, N, b.data_ptr(),
+                                    C.data_ptr(), N, out_f32, _lib.stream_ptr(dev)), "linear")
+    ref = X.float() @ W.float().T + b
+    err = (C.float() - ref).abs().max().item()
+    tol = 1e-3 if out_f32 else 1.6e-2 * ref.abs().max().item()
+    assert err <= tol, err

@@ -1,0 +1,42 @@
+"""Kernel benchmark: the deep tower's Linear (dcnr_linear_bf16) at cfg3 shape
+vs torch's bf16 matmul (hipBLASLt) on the same device, same data."""
+import ctypes, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd"))
+import torch
+from dcnr import _lib
+
+def run(M=131072, K=512, N=512, iters=20):
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    X = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    W = (torch.randn(N, K, device=dev, generator=g) / K ** 0.5).to(torch.bfloat16)
+    b = torch.randn(N, device=dev, generator=g)
+    C = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+    lib = _lib.load()
+    s = _lib.stream_ptr(dev)
+    call = lambda: _lib.check(lib.dcnr_linear_bf16(X.data_ptr(), K, M, K, W.data_ptr(), K, N, b.data_ptr(),
+                                                   C.data_ptr(), N, 0, s), "linear")
+    call(); torch.cuda.synchronize()
+    ref = torch.addmm(b, X.float(), W.float().t())
+    err = ((C.float() - ref).norm() / ref.norm()).item()
+    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+    e0.record()
+    for _ in range(iters): call()
+    e1.record(); torch.cuda.synchronize()
+    t_ours = e0.elapsed_time(e1) / iters
+    Wt = W.t()
+    for _ in range(3): torch.addmm(b.to(torch.bfloat16), X, Wt)
+    e0.record()
+    for _ in range(iters): torch.addmm(b.to(torch.bfloat16), X, Wt)
+    e1.record(); torch.cuda.synchronize()
+    t_torch = e0.elapsed_time(e1) / iters
+    fl = 2 * M * N * K
+    print(f"M={M} K={K} N={N}: ours {t_ours*1e3:.1f} us ({fl/t_ours/1e9:.0f} TF/s, rel err {err:.2e}); "
+          f"torch/hipBLASLt {t_torch*1e3:.1f} us ({fl/t_torch/1e9:.0f} TF/s); "
+          f"HBM floor {(M*K*2+M*N*2)/6.3e12*1e6:.1f} us")
+
+if __name__ == "__main__":
+    for K in (512, 456):
+        run(K=K)
+    run(M=131072, K=512, N=128)
