@@ -139,39 +139,38 @@ def main():
 
     for k in range(args.warmup):
         trainer.step(*pool[k % len(pool)])
-    # the same K steps without the per-launch HIP events (instrumentation cost check)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        trainer.step(*pool[k % len(pool)])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el_plain = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(el_plain, op=dist.ReduceOp.MAX)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    _lib.profile_enable(True)
-    _lib.profile_collect()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        loss = trainer.step(*pool[k % len(pool)])
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    _lib.profile_enable(False)
-    prof = _lib.profile_collect()
-    el_t = torch.tensor([el], device=dev, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-    el = float(el_t.item())
+
+    def timed(instrumented):
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        if instrumented:
+            _lib.profile_enable(True)
+            _lib.profile_collect()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            last = trainer.step(*pool[k % len(pool)])
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        prof = None
+        if instrumented:
+            _lib.profile_enable(False)
+            prof = _lib.profile_collect()
+        el_t = torch.tensor([el], device=dev, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+        return float(el_t.item()), prof, last
+
+    # timed region: K plain steps (the reported value)
+    el, _, loss = timed(False)
+    # the same K steps again with every libdcnr launch bracketed by HIP events
+    # on its stream (per-kernel-class durations for the roofline); the events
+    # serialise launches, so this pass is not the throughput number
+    el_prof, prof, _ = timed(True)
     final_loss = float(loss.item())
 
     # scored pairs/s: eval-mode forward (running-stat BN, no dropout) per GPU
@@ -197,7 +196,7 @@ def main():
         samples = world * B * args.steps
         per_step_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1]}
         launches = {k: v[1] / args.steps for k, v in prof.items() if v[1]}
-        gemm_cls = max(GEMM_FLOP, key=lambda k: prof[k][0])
+        gemm_cls = "gemm_fwd"   # 9 launches/step, all gemm_nt_kernel<16,0> (the largest kernel)
         ms, cnt = prof[gemm_cls]
         flop_launch = GEMM_FLOP[gemm_cls] * B * args.steps / cnt
         achieved = flop_launch / (ms / cnt / 1e3) / 1e12
@@ -212,7 +211,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": el / args.steps * 1e3,
-            "ms_per_step_uninstrumented": float(el_plain.item()) / args.steps * 1e3,
+            "ms_per_step_instrumented": el_prof / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -226,7 +225,8 @@ def main():
                        "deep": "3 cross + 4 x 512 residual", "parallelism": f"dp{world}"},
             "scored_pairs_per_sec": pairs_per_s,
             "final_loss": final_loss,
-            "roofline": {"bound": "mfma", "kernel": gemm_cls, "achieved": achieved / 1.0,
+            "roofline": {"bound": "mfma",
+                         "kernel": "gemm_nt_kernel<16,0> (deep-tower Linear fwd, class gemm_fwd)", "achieved": achieved / 1.0,
                          "peak": PEAK_BF16 / 1e12 if args.precision == "bf16" else 157.3,
                          "unit": "TFLOP/s",
                          "frac": achieved / ((PEAK_BF16 / 1e12) if args.precision == "bf16"

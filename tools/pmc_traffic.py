@@ -1,0 +1,78 @@
+"""HBM traffic per launch from two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+Follows MI355X_MICROARCH.md "HBM [CDNA4]": FETCH_SIZE and WRITE_SIZE need
+separate passes; on gfx950 FETCH_SIZE reports half the bytes of wide
+coalesced reads, so it is doubled; WRITE_SIZE is exact for 16-B stores and
+float atomics.  Both counters are in KB.  Usage:
+
+  python tools/pmc_traffic.py <fetch counter_collection.csv> <write counter_collection.csv> \
+      [--json profiles/pmc_traffic.json]
+"""
+import argparse
+import csv
+import json
+import re
+from collections import defaultdict
+
+# libdcnr kernel-name patterns -> the bench's kernel classes
+CLASSES = [
+    ("gemm_fwd", r"gemm_nt_kernel<16, 0>"),
+    ("gemm_nt_resid", r"gemm_nt_kernel<16, 2>"),
+    ("gemm_nt_f32", r"gemm_nt_kernel<16, 1>"),
+    ("gemm_dw", r"gemm_kernel<"),
+    ("gather_cross", r"gather_cross_fwd_kernel"),
+    ("cross_bwd", r"cross_bwd_kernel"),
+    ("adam", r"adam_kernel"),
+]
+
+
+def short(name):
+    name = name.replace("(anonymous namespace)::", "").replace("void ", "")
+    name = re.sub(r"\(.*", "", name)
+    return name[:110]
+
+
+def load(path, counter):
+    per = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] != counter:
+                continue
+            per[row["Kernel_Name"]].append(float(row["Counter_Value"]) * 1024.0)
+    return per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch")
+    ap.add_argument("write")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    fe = load(a.fetch, "FETCH_SIZE")
+    wr = load(a.write, "WRITE_SIZE")
+    rows = []
+    for name in sorted(set(fe) | set(wr)):
+        f = fe.get(name, [])
+        w = wr.get(name, [])
+        fb = 2.0 * sum(f) / len(f) if f else 0.0
+        wb = sum(w) / len(w) if w else 0.0
+        rows.append((name, len(f), fb, wb))
+    rows.sort(key=lambda r: -(r[2] + r[3]) * r[1])
+    print(f"{'launches':>8} {'read_MB':>10} {'write_MB':>10}  kernel (per-launch HBM bytes; "
+          f"FETCH_SIZE x2, WRITE_SIZE x1)")
+    for name, n, fb, wb in rows:
+        print(f"{n:8d} {fb / 1e6:10.2f} {wb / 1e6:10.2f}  {short(name)}")
+    out = {}
+    for cls, pat in CLASSES:
+        sel = [r for r in rows if re.search(re.escape(pat) if "<" in pat else pat, r[0])]
+        if sel:
+            n = sum(r[1] for r in sel)
+            out[cls] = sum((r[2] + r[3]) * r[1] for r in sel) / max(n, 1)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
