@@ -23,16 +23,25 @@
 //    (out-of-range loads read 0, stores are dropped): branch-free edges.
 #include "dcnr_internal.h"
 
+// tools/gemm_lab.hip rebuilds this file with NT_LAB_MODE bits set to time
+// parts of the kernel in isolation (1: no C stores, 2: no X loads in the
+// k-loop, 4: no MFMAs).  The library always builds mode 0.
+#ifndef NT_LAB_MODE
+#define NT_LAB_MODE 0
+#endif
+
 namespace dcnr {
 namespace {
 
-constexpr int NT = 256, TM = 128, TN = 128, BK = 32, WROWS = TM / 4;
+// 8 waves (2 per SIMD: one wave's epilogue overlaps the other's MFMAs), 32 rows each
+constexpr int NT = 512, TM = 256, TN = 128, BK = 32, WROWS = TM / 8;
 
 template <int KTP> struct NtCfg {
   static constexpr int WCH = KTP * (BK / 8);                 // 16-B chunks per W row
-  static constexpr int DEPTH = KTP;                          // prefetch ring depth (k-steps)
+  static constexpr int DEPTH = KTP < 8 ? KTP : 8;            // prefetch ring depth (k-steps)
   static constexpr int W_LDS = TN * WCH;                     // uint4 units
-  static constexpr size_t LDS_BYTES = (size_t)W_LDS * 16;
+  static constexpr int BIAS_LDS = TN / 4;                    // uint4 units (128 fp32)
+  static constexpr size_t LDS_BYTES = (size_t)(W_LDS + BIAS_LDS) * 16;
 };
 
 template <int WCH>
@@ -78,8 +87,6 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
       __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, (int)(a.M * a.ldc * es), 0x00020000);
   const __amdgpu_buffer_rsrc_t rr_ = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.R, (short)0, EPI == NT_EPI_RESID ? (int)(a.M * a.ldr * 2) : 0, 0x00020000);
-  const __amdgpu_buffer_rsrc_t br = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.bias, (short)0, a.bias ? a.N * 4 : 0, 0x00020000);
 
   // start the X stream before the W slice load so both are in flight
   u32x4 ring[DEPTH][2];
@@ -98,17 +105,20 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
     Ws[w_slot<C::WCH>(row, ch)] = v;
   }
 
-  // per-column bias for this lane's output columns (loaded once)
-  float bias[8][4];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int n = n0 + j * 16 + (lane >> 4) * 4;
-    // null bias -> descriptor of 0 records -> the load returns zeros (any epilogue)
-    u32x4 b4 = __builtin_amdgcn_raw_buffer_load_b128(br, n < a.N ? n * 4 : OOR, 0, 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bias[j][r] = __uint_as_float(b4[r]);
+  // bias slice in LDS (read per tile in the epilogue; registers go to the ring)
+  float* bias_s = reinterpret_cast<float*>(lds + C::W_LDS);
+  for (int c = tid; c < TN; c += NT) {
+    const int n = n0 + c;
+    bias_s[c] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
   }
   __syncthreads();
+
+  // W fragments of the current k-step (one buffer: each fragment is re-read
+  // for the next k-step right after its two MFMAs have issued)
+  bf16x8 wf[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    wf[j] = __builtin_bit_cast(bf16x8, Ws[w_slot<C::WCH>(j * 16 + (lane & 15), lane >> 4)]);
 
   for (int64_t mt = group; mt < a.mtiles; mt += groups) {
     const int64_t r0 = mt * TM + wave * WROWS;
@@ -133,66 +143,92 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    // W fragments double-buffered in registers: the ds_reads of k-step kt+1
-    // are issued ahead of k-step kt's MFMAs; sched_barrier pins one k-step per
-    // region so the compiler does not hoist the whole tile's reads (spills)
-    bf16x8 wf[2][8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-      wf[0][j] = __builtin_bit_cast(bf16x8, Ws[w_slot<C::WCH>(j * 16 + (lane & 15), lane >> 4)]);
 #pragma unroll
     for (int kt = 0; kt < KTP; ++kt) {
       const int slot = kt % DEPTH;
-      const int cb = kt & 1;
-      if (kt + 1 < KTP) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-          wf[cb ^ 1][j] = __builtin_bit_cast(
-              bf16x8, Ws[w_slot<C::WCH>(j * 16 + (lane & 15), (kt + 1) * 4 + (lane >> 4))]);
-      }
+      const int kn = (kt + 1) % KTP;   // next k-step (wraps to the next M-tile: W is tile-independent)
       bf16x8 xf[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) xf[i] = __builtin_bit_cast(bf16x8, ring[slot][i]);
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 8; ++j) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][j], xf[i], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 2; ++i)
+          if constexpr (!(NT_LAB_MODE & 4))
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+          else
+            acc[i][j][0] += (float)xf[i][j] + (float)wf[j][0];
+        wf[j] = __builtin_bit_cast(bf16x8, Ws[w_slot<C::WCH>(j * 16 + (lane & 15), kn * 4 + (lane >> 4))]);
+      }
       // refill the slot with the k-step DEPTH ahead (same or next M-tile)
-      {
-        const int kn = kt + DEPTH;
-        const int64_t mtn = mt + (kn >= KTP ? groups : 0);
-        load_x(ring[slot], xr, a.ldx, a.M, a.K, mtn * TM + wave * WROWS, kn % KTP, lane,
+      if constexpr (!(NT_LAB_MODE & 2)) {
+        const int kd = kt + DEPTH;
+        const int64_t mtn = mt + (kd >= KTP ? groups : 0);
+        load_x(ring[slot], xr, a.ldx, a.M, a.K, mtn * TM + wave * WROWS, kd % KTP, lane,
                mtn < a.mtiles);
       }
+      // pin the order: per j, 2 MFMAs then the fragment's re-read
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);     // VMEM read (ring refill)
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // epilogue: lane holds C[m][n..n+3] for each (i, j)
+    // epilogue: lane holds C[m][n..n+3] of each (i, j), n = 16j + 4*(lane>>4).
+    // bf16: fragments j and j+1 are exchanged between lane rows with
+    // v_permlane16_swap so every lane stores 8 consecutive columns (16 B) and
+    // each store instruction writes 64 contiguous bytes per output row.
+    const int q = lane >> 4;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const int n = n0 + j * 16 + (lane >> 4) * 4;
-      const bool nok = n < a.N;
+    for (int i = 0; i < 2; ++i) {
+      const int64_t m = r0 + i * 16 + (lane & 15);
+      const bool mok = m < a.M;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int64_t m = r0 + i * 16 + (lane & 15);
-        const bool ok = nok && m < a.M;
-        float v[4];
+      for (int jp = 0; jp < 4; ++jp) {
+        u32x2 o[2];
+        u32x4 of[2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[j][r];
-        if constexpr (EPI == NT_EPI_F32) {
-          u32x4 o = {__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                     __float_as_uint(v[3])};
-          __builtin_amdgcn_raw_buffer_store_b128(o, cr, ok ? (int)((m * a.ldc + n) * 4) : OOR, 0, 0);
-        } else {
+        for (int h = 0; h < 2; ++h) {
+          const int j = 2 * jp + h;
+          const float4 bj = *reinterpret_cast<const float4*>(bias_s + j * 16 + q * 4);
+          float v[4] = {acc[i][j][0] + bj.x, acc[i][j][1] + bj.y, acc[i][j][2] + bj.z,
+                        acc[i][j][3] + bj.w};
           if constexpr (EPI == NT_EPI_RESID) {
             const u32x2 rv = resid[i][j];
             const bf16* rb = reinterpret_cast<const bf16*>(&rv);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += (float)rb[r];
           }
-          u32x2 o = {pack2(v[0], v[1]), pack2(v[2], v[3])};
-          __builtin_amdgcn_raw_buffer_store_b64(o, cr, ok ? (int)((m * a.ldc + n) * 2) : OOR, 0, 0);
+          o[h] = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
+          of[h] = u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
+                        __float_as_uint(v[3])};
+        }
+        if constexpr (EPI == NT_EPI_F32) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int n = n0 + (2 * jp + h) * 16 + q * 4;
+            __builtin_amdgcn_raw_buffer_store_b128(
+                of[h], cr, (mok && n < a.N) ? (int)((m * a.ldc + n) * 4) : OOR, 0, 0);
+          }
+        } else {
+          // rows (q) 0..3 of o[0]/o[1]: after the swap lane row q holds
+          // fragment j = 2jp + (q&1), columns 8*(q>>1) .. +7
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            auto sw = __builtin_amdgcn_permlane16_swap(o[0][d], o[1][d], false, false);
+            o[0][d] = sw[0];
+            o[1][d] = sw[1];
+          }
+          const u32x4 st = {o[0][0], o[0][1], o[1][0], o[1][1]};
+          const int n = n0 + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8;
+          const int off = (mok && n < a.N) ? (int)((m * a.ldc + n) * 2) : OOR;
+          if constexpr (!(NT_LAB_MODE & 1))
+            __builtin_amdgcn_raw_buffer_store_b128(st, cr, off, 0, 0);
+          else if (acc[i][0][0] == 12345.f)
+            __builtin_amdgcn_raw_buffer_store_b128(st, cr, off, 0, 0);
         }
       }
     }
