@@ -175,6 +175,7 @@ struct Layout {
   // backward
   void* G; void* dt2; void* du; void* da;
   float* dx0; float* slab; int64_t slab_elems; float* cpart; size_t cpart_elems;
+  float* cred2; size_t cred2_elems;             // cross partial second stage
   double* bce_part;
   size_t total;
 };
@@ -222,7 +223,7 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws) {
   L.sums = (double*)b.take((size_t)(3 * d.Hp + 1) * 8);
   L.coef = (float*)b.take((size_t)3 * d.Hp * 4);
   L.red2 = (double*)b.take((size_t)RED_G * 3 * d.Hp * 8);
-  L.red_cnt = (int*)b.take(RED_MAX_CGRP * 4);
+  L.red_cnt = (int*)b.take(CNT_SLOTS * 4);
   if (train) {
     L.G = b.take(act);
     L.dt2 = b.take(act);
@@ -233,6 +234,9 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws) {
     L.slab = (float*)b.take((size_t)L.slab_elems * 4);
     L.cpart_elems = cross_bwd_part_elems(d.D, d.L);
     L.cpart = (float*)b.take(L.cpart_elems * 4);
+    L.cred2_elems = cross_red2_elems(d.D, d.L);
+    L.cred2 = (float*)b.take(L.cred2_elems * 4);
+
   }
   L.bce_part = (double*)b.take(bce_ws_bytes());
   L.total = b.off + 256;
@@ -301,10 +305,13 @@ GatherDesc make_gather(const Dims& d, const Params& P, int n_num) {
   GatherDesc g;
   memset(&g, 0, sizeof(g));
   g.n_tab = 2 + d.K;
+  int off = 0;
   for (int t = 0; t < g.n_tab; ++t) {
     g.tab[t] = P.tab[t];
     g.rows[t] = d.rows[t];
     g.width[t] = d.widths[t];
+    g.off[t] = off;
+    off += d.widths[t];
   }
   g.n_num = n_num;
   g.D = d.D;
@@ -340,7 +347,7 @@ dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train
   };
   addb(P.b0, L.b0p);
   // reduce_fused's column-group counters start at zero (a 1-row pack of 0 columns)
-  vb.push_back(PackDesc{P.b0, L.red_cnt, nullptr, 0, 0, RED_MAX_CGRP, 0, 1, 0});
+  vb.push_back(PackDesc{P.b0, L.red_cnt, nullptr, 0, 0, CNT_SLOTS, 0, 1, 0});
   for (int j = 0; j < d.R; ++j) { addb(P.blk[j].b1, L.b1p[j]); addb(P.blk[j].b2, L.b2p[j]); }
   for (size_t o = 0; o < v.size(); o += MAX_PACK) {
     PackBatch pb;
@@ -549,11 +556,19 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
     TRY(bn_layer_fwd(desc, d, L, L.t2[j], B, train, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
                      L.bn[2 * j + 1], s));
-    TRYP(DCNR_K_ROWWISE, bn_add_relu2(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp, L.bn[2 * j + 1].scale,
-                     L.bn[2 * j + 1].shift, s));
+    const bool head = j == d.R - 1 && bn_add_relu_head_supported(d.prec, d.Hp);
+    if (head)   // last block: residual + ReLU + deep head dot + logits in one pass
+      TRYP(DCNR_K_ROWWISE, bn_add_relu_head(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
+                                            L.bn[2 * j + 1].scale, L.bn[2 * j + 1].shift, P.wf,
+                                            d.H, L.zc, P.bf, logits, s));
+    else
+      TRYP(DCNR_K_ROWWISE, bn_add_relu2(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
+                                        L.bn[2 * j + 1].scale, L.bn[2 * j + 1].shift, s));
   }
-  TRYP(DCNR_K_HEAD, row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
-  TRYP(DCNR_K_HEAD, head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
+  if (!bn_add_relu_head_supported(d.prec, d.Hp)) {
+    TRYP(DCNR_K_HEAD, row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
+    TRYP(DCNR_K_HEAD, head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
+  }
   return DCNR_OK;
 }
 
@@ -579,6 +594,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   const float* dz = dlogits;
   const int Hp = d.Hp, H = d.H;
   const float p = d.dropout;
+  // dense embedding grads: zeroed, then scatter-added by the cross backward
   if (!accumulate)
     for (int t = 0; t < 2 + d.K; ++t)
       TRYP(DCNR_K_PACK, fill_zero(Gr.tab[t], (size_t)d.rows[t] * d.widths[t] * 4, s));
@@ -650,8 +666,9 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   cb.dwf_cross = Gr.wf + H;
   cb.dbf = Gr.bf;
   for (int t = 0; t < 2 + d.K; ++t) cb.emb_grad[t] = Gr.tab[t];
+  CrossBwdScratch cws{L.cpart, L.cpart_elems, L.cred2, L.cred2_elems, L.red_cnt, CNT_SLOTS};
   TRYP(DCNR_K_CROSS_BWD, cross_bwd_scatter(g, cb, user_ids, item_ids, cat_features, num_features, dz, B, L.dx0, d.Dp,
-                        L.cpart, L.cpart_elems, accumulate, s));
+                        cws, accumulate, s));
   return DCNR_OK;
 }
 

@@ -92,16 +92,61 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// Counter-based dropout keep-test: deterministic in (seed, layer, row, col),
-// so backward regenerates the forward mask without storing it.
-__device__ __forceinline__ bool dropout_keep(uint64_t seed, int layer, int64_t row, int col,
-                                             uint32_t thresh) {
-  uint64_t x = seed ^ (0x9E3779B97F4A7C15ull * (uint64_t)(layer + 1));
-  x += (uint64_t)row * 0x100000001B3ull + (uint64_t)col * 0xC2B2AE3D27D4EB4Full;
-  x ^= x >> 30; x *= 0xBF58476D1CE4E5B9ull;
-  x ^= x >> 27; x *= 0x94D049BB133111EBull;
-  x ^= x >> 31;
-  return (uint32_t)(x >> 32) >= thresh;
+// ---- register-only wave reductions (no LDS crossbar round trips)
+// gfx950 v_permlane32_swap / v_permlane16_swap exchange half-waves / rows;
+// the last 16 lanes reduce with DPP (quad_perm, row_half_mirror, row_mirror).
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float row16_sum(float t) {   // sum over each 16-lane row, in every lane
+  t += dpp<0xB1>(t);    // quad_perm [1,0,3,2]
+  t += dpp<0x4E>(t);    // quad_perm [2,3,0,1]
+  t += dpp<0x141>(t);   // row_half_mirror
+  t += dpp<0x140>(t);   // row_mirror
+  return t;
+}
+// full 64-lane sum of v, in every lane
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  const unsigned u = __float_as_uint(v);
+  auto h = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+  float t = __uint_as_float(h[0]) + __uint_as_float(h[1]);
+  const unsigned ut = __float_as_uint(t);
+  auto r = __builtin_amdgcn_permlane16_swap(ut, ut, false, false);
+  t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  return row16_sum(t);
+}
+// four independent 64-lane sums at once (wave-uniform results)
+__device__ __forceinline__ void wave_sum4(float a, float b, float c, float d, float& sa, float& sb,
+                                          float& sc, float& sd) {
+  auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(c), __float_as_uint(d), false, false);
+  const float ab = __uint_as_float(p[0]) + __uint_as_float(p[1]);   // lanes 0-31: a, 32-63: b
+  const float cd = __uint_as_float(q[0]) + __uint_as_float(q[1]);   // lanes 0-31: c, 32-63: d
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(ab), __float_as_uint(cd), false, false);
+  const float t = row16_sum(__uint_as_float(r[0]) + __uint_as_float(r[1]));  // rows: a, c, b, d
+  sa = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 0));
+  sc = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 16));
+  sb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 32));
+  sd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t), 48));
+}
+
+// Counter-based dropout mask: 32 random bits per (seed, layer, row, column
+// pair), deterministic, so backward regenerates the forward mask without
+// storing it.  Column 2k uses the low 16 bits, 2k+1 the high 16 bits; an
+// element is kept iff its 16 bits >= thresh16 = round(p * 65536), i.e. with
+// probability 1 - p (to 2^-16).  Two murmur3 fmix32 rounds (32-bit integer
+// ops only: ~8 VALU per element).
+__device__ __forceinline__ uint32_t fmix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x85EBCA6Bu;
+  x ^= x >> 13; x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ uint32_t dropout_bits(uint64_t seed, int layer, int64_t row,
+                                                 int colpair) {
+  uint32_t x = fmix32((uint32_t)row * 0x9E3779B1u ^ (uint32_t)seed ^ ((uint32_t)layer * 0x7FEB352Du));
+  return fmix32((x + (uint32_t)colpair * 0x846CA68Bu) ^ (uint32_t)(seed >> 32));
 }
 
 // ------------------------------------------------------------------ GEMM
@@ -158,11 +203,13 @@ constexpr int MAX_PACK = 20;
 struct PackBatch { PackDesc d[MAX_PACK]; int n; };
 dcnr_status pack_weights(int precision, const PackBatch& pb, hipStream_t s);
 
+constexpr int MAX_TABLES = 66;           // user, item + up to 64 categorical tables
 struct GatherDesc {
-  const float* tab[66];  // user, item, cat...
-  int64_t rows[66];
-  int width[66];
-  int n_tab;             // 2 + n_cat
+  const float* tab[MAX_TABLES];  // user, item, cat...
+  int64_t rows[MAX_TABLES];
+  int width[MAX_TABLES];
+  int off[MAX_TABLES];           // first x0 column of the table
+  int n_tab;                     // 2 + n_cat
   int n_num;
   int D;
 };
@@ -180,17 +227,25 @@ dcnr_status gather_cross_fwd(int precision, const GatherDesc& g, const CrossPara
 
 struct CrossBwdParams {
   CrossParams cp;
-  float* dw[8]; float* db[8];  // grads (final)
-  float* dwf_cross;            // grad final_linear.weight + H
-  float* dbf;                  // grad final_linear.bias
-  float* emb_grad[66];         // dense embedding grads (scatter-add)
+  float* dw[8]; float* db[8];      // grads (final)
+  float* dwf_cross;                // grad final_linear.weight + H
+  float* dbf;                      // grad final_linear.bias
+  float* emb_grad[MAX_TABLES];     // dense embedding grads (atomic scatter-add)
 };
+struct CrossBwdScratch {
+  float* part; size_t part_elems;  // per-block partials
+  float* red2; size_t red2_elems;  // [RED_G][stride] second-stage sums
+  int* counters; int n_counters;   // hand-off counters, zero at rest
+};
+constexpr int64_t BWD_BLOCKS = 2048;
 dcnr_status cross_bwd_scatter(const GatherDesc& g, const CrossBwdParams& p,
                               const int64_t* user, const int64_t* item, const int64_t* cat,
                               const float* num, const float* dz, int64_t B,
-                              const float* dx0_deep, int ld_dx, float* part, size_t part_elems,
+                              const float* dx0_deep, int ld_dx, const CrossBwdScratch& ws,
                               int accumulate, hipStream_t s);
 size_t cross_bwd_part_elems(int D, int L);
+size_t cross_red2_elems(int D, int L);
+int cross_red_groups(int D, int L);
 
 // Column reductions: partial sums per row-chunk, part[nchunks][NK][N] (f32),
 // reduced in fixed order into sums[3][N] (f64; components >= NK zeroed) with
@@ -213,6 +268,7 @@ dcnr_status bn_finalize2(const double* sums, int N, int Nr, int train, const BnF
 enum RedMode : int { RED_BN_FWD = 0, RED_BN_BWD = 1, RED_BIAS = 2, RED_SUMS = 3 };
 constexpr int RED_G = 32;          // chunk groups per column group
 constexpr int RED_MAX_CGRP = 64;   // column groups of 64 -> N <= 4096
+constexpr int CNT_SLOTS = 512;     // hand-off counters in the workspace (zeroed by pack_all)
 struct RedFinal {
   int mode; int accumulate; double count;
   double* red2;                                // workspace [RED_G][3][N] fp64
@@ -265,6 +321,12 @@ dcnr_status splitk_reduce(const float* slab, int splits, int64_t slab_stride, in
                           int N, int K, float* out, int accumulate, hipStream_t s);
 
 // head
+// last block + head fused: out = relu(BN2(t) + x); logits = out . wf[:Nr] + zc + bf
+bool bn_add_relu_head_supported(int precision, int N);
+dcnr_status bn_add_relu_head(int precision, const void* t, const void* x, void* out, int64_t B,
+                             int N, int ld, const float* scale, const float* shift,
+                             const float* wf, int Nr, const float* zc, const float* bf,
+                             float* logits, hipStream_t s);
 dcnr_status row_dot(int precision, const void* X, int ld, int N, const float* w, int64_t B,
                     float* out, hipStream_t s);
 dcnr_status head_logits(const float* zdeep, const float* zc, const float* bf, int64_t B,

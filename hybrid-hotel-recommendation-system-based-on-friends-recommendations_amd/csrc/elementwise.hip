@@ -131,6 +131,18 @@ dcnr_status run_rowcol(const Op& op, int64_t B, int N, float* part, int* nchunks
 
 struct NoCst {};
 
+// y[v] *= keep(r, c+v) ? inv_keep : 0 for V consecutive columns (c even)
+template <int V>
+__device__ __forceinline__ void apply_dropout(uint64_t seed, int layer, int64_t r, int c,
+                                              uint32_t thresh16, float inv_keep, float (&y)[V]) {
+#pragma unroll
+  for (int v = 0; v < V; v += 2) {
+    const uint32_t bits = dropout_bits(seed, layer, r, (c + v) >> 1);
+    y[v] = (bits & 0xFFFFu) >= thresh16 ? y[v] * inv_keep : 0.f;
+    y[v + 1] = (bits >> 16) >= thresh16 ? y[v + 1] * inv_keep : 0.f;
+  }
+}
+
 // ---------------------------------------------------------------- ops
 // sums of (t-K) and (t-K)^2 with K = t[0] (the batch's first row)
 template <typename T> struct StatsOp {
@@ -170,11 +182,8 @@ template <typename T> struct BnReluDropOp {  // a = dropout(relu(t*sc+sh))
   __device__ void load(int64_t r, int c, Reg& q) const { ldv<T>(t + r * ld + c, q.x); }
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&)[1][VE<T>]) const {
 #pragma unroll
-    for (int v = 0; v < VE<T>; ++v) {
-      float y = fmaxf(q.x[v] * k.sc[v] + k.sh[v], 0.f);
-      if (drop) y = dropout_keep(seed, layer, r, c + v, thresh) ? y * inv_keep : 0.f;
-      q.x[v] = y;
-    }
+    for (int v = 0; v < VE<T>; ++v) q.x[v] = fmaxf(q.x[v] * k.sc[v] + k.sh[v], 0.f);
+    if (drop) apply_dropout<VE<T>>(seed, layer, r, c, thresh, inv_keep, q.x);
     stv<T>(a + r * ld + c, q.x);
   }
 };
@@ -192,6 +201,36 @@ template <typename T> struct BnAddReluOp {   // out = relu(t*sc+sh + x)
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) q.a[v] = fmaxf(q.a[v] * k.sc[v] + k.sh[v] + q.b[v], 0.f);
     stv<T>(out + r * ld + c, q.a);
+  }
+};
+
+// last residual block + head: out = relu(t*sc+sh + x) and, with a wave per
+// row (N / V == 64 threads), logits[r] = out[r] . wf[:Nr] + zc[r] + bf
+template <typename T> struct BnAddReluHeadOp {
+  const T* t; const T* x; T* out; int ld; const float* sc; const float* sh;
+  const float* wf; int Nr; const float* zc; const float* bf; float* logits;
+  struct Cst { float sc[VE<T>], sh[VE<T>], wf[VE<T>]; float bf; };
+  struct Reg { float a[VE<T>], b[VE<T>]; };
+  __device__ void prep(int c, Cst& q) const {
+    ldc(sc + c, q.sc); ldc(sh + c, q.sh);
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) q.wf[v] = c + v < Nr ? wf[c + v] : 0.f;
+    q.bf = bf[0];
+  }
+  __device__ void load(int64_t r, int c, Reg& q) const {
+    ldv<T>(t + r * ld + c, q.a);
+    ldv<T>(x + r * ld + c, q.b);
+  }
+  __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&)[1][VE<T>]) const {
+    float d = 0.f;
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) {
+      q.a[v] = fmaxf(q.a[v] * k.sc[v] + k.sh[v] + q.b[v], 0.f);
+      d += (float)(T)q.a[v] * k.wf[v];   // the stored (rounded) activation, as row_dot reads it
+    }
+    stv<T>(out + r * ld + c, q.a);
+    d = wave_sum_dpp(d);
+    if ((threadIdx.x & 63) == 0) logits[r] = (d + zc[r]) + k.bf;
   }
 };
 
@@ -276,12 +315,14 @@ template <typename T> struct Bwd1StatsOp {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
       float pre = q.t[v] * k.sc[v] + k.sh[v];
-      float dr = pre > 0.f ? q.a[v] : 0.f;
-      if (drop) dr = dropout_keep(seed, layer, r, c + v, thresh) ? dr * inv_keep : 0.f;
+      q.a[v] = pre > 0.f ? q.a[v] : 0.f;
+    }
+    if (drop) apply_dropout<VE<T>>(seed, layer, r, c, thresh, inv_keep, q.a);
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) {
       float xh = (q.t[v] - k.mu[v]) * k.is[v];
-      q.a[v] = dr;
-      acc[0][v] += dr;
-      acc[1][v] += dr * xh;
+      acc[0][v] += q.a[v];
+      acc[1][v] += q.a[v] * xh;
     }
     stv<T>(da + r * ld + c, q.a);
   }
@@ -593,8 +634,8 @@ dcnr_status bn_bwd_coef(const double* sums, int N, int Nr, const float* gamma, c
   return DCNR_OK;
 }
 
-static uint32_t drop_thresh(float p) {
-  return (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0);
+static uint32_t drop_thresh(float p) {   // 16-bit threshold (see dropout_bits)
+  return (uint32_t)std::min(65536.0, std::floor((double)p * 65536.0 + 0.5));
 }
 
 template <typename T>
@@ -624,6 +665,30 @@ dcnr_status bn_add_relu2(int precision, const void* t, const void* x, void* out,
   return precision == DCNR_PREC_BF16
              ? bn_add_relu_impl<bf16>(t, x, out, B, N, ld, scale, shift, s)
              : bn_add_relu_impl<float>(t, x, out, B, N, ld, scale, shift, s);
+}
+
+template <typename T>
+static dcnr_status bn_add_relu_head_impl(const void* t, const void* x, void* out, int64_t B, int N,
+                                         int ld, const float* sc, const float* sh, const float* wf,
+                                         int Nr, const float* zc, const float* bf, float* logits,
+                                         hipStream_t s) {
+  BnAddReluHeadOp<T> op{(const T*)t, (const T*)x, (T*)out, ld, sc, sh, wf, Nr, zc, bf, logits};
+  return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
+}
+bool bn_add_relu_head_supported(int precision, int N) {
+  return N / (precision == DCNR_PREC_BF16 ? 8 : 4) == 64;
+}
+dcnr_status bn_add_relu_head(int precision, const void* t, const void* x, void* out, int64_t B,
+                             int N, int ld, const float* scale, const float* shift,
+                             const float* wf, int Nr, const float* zc, const float* bf,
+                             float* logits, hipStream_t s) {
+  if (!bn_add_relu_head_supported(precision, N)) {
+    set_error("bn_add_relu_head: needs a wave per row (N=%d)", N);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  return precision == DCNR_PREC_BF16
+             ? bn_add_relu_head_impl<bf16>(t, x, out, B, N, ld, scale, shift, wf, Nr, zc, bf, logits, s)
+             : bn_add_relu_head_impl<float>(t, x, out, B, N, ld, scale, shift, wf, Nr, zc, bf, logits, s);
 }
 
 template <typename T>

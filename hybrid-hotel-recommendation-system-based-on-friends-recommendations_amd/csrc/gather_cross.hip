@@ -1,5 +1,5 @@
-// Embedding gathers + x0 assembly + the cross stack, forward and backward, one
-// 64-lane wave per sample row (gfx950).
+// Embedding gathers + x0 assembly + the cross stack, forward and backward, and
+// the dense embedding gradient (gfx950, 64-lane waves, one wave per sample row).
 //
 // Forward  (DCN_RecSys.forward, train.py:156-159 and 167-168):
 //   x0[b] = [U[u_b] | I[i_b] | C_0[c_b0] ... C_{K-1}[c_b,K-1] | num_b]   (bit-exact fp32 gather)
@@ -12,10 +12,28 @@
 // Backward re-gathers x0 in fp32 and recomputes the (cheap) cross forward in
 // registers instead of saving per-layer activations:
 //   g_L = dz * w_f[H:];  dx_l = g(1+s_l) + (g.x_l) w_l;  dw_l += (g.x_l) x_l;  db_l += g
-//   dx0 = dx0_cross + dx0_deep  ->  dense embedding grads by row scatter-add
-//   (embedding_dense_backward semantics; fp32 atomics, 128-B row segments).
-// The x_l . w_l and g . x_l dots are wave reductions (xor shuffles).
+//   dx0 = dx0_cross + dx0_deep  ->  dense embedding grads (embedding_dense_backward)
+//
+// Latency structure (the gathers are dependent loads: id -> row): a block
+// stages the ids of a tile of samples in LDS with coalesced loads, then each
+// wave issues the row loads of several samples back to back (unconditional
+// loads at clamped addresses, so no per-element branch serialises them)
+// before computing any of them.
+//
+// Embedding gradients: every table row segment is added with no-return fp32
+// atomics (128-B row segments, executed memory-side and overlapped with the
+// kernel's own work).  Measured alternative (kept out): privatising the small
+// categorical tables in LDS (per-sample dcat stores + an LDS-atomic per-table
+// pass) cost 285 us against +30 us for the inline atomics at cfg3.
 #include "dcnr_internal.h"
+
+// tools/gather_lab.hip rebuilds this file with GC_LAB_MODE bits set to time
+// parts of the kernels in isolation (forward 1: no x0 stores, 2: no cross
+// compute, 4: no row loads; backward 8: no gradient scatter, 16: no cross
+// compute).  The library always builds mode 0.
+#ifndef GC_LAB_MODE
+#define GC_LAB_MODE 0
+#endif
 
 namespace dcnr {
 namespace {
@@ -25,68 +43,95 @@ constexpr int WPB = NT / WAVE;
 constexpr int NUM_TAB = -1, NO_ELEM = -2;
 
 struct TabLds {
-  const float* tab[66];
-  float* grad[66];
-  int rows[66];
-  int width[66];
+  const float* tab[MAX_TABLES];
+  float* grad[MAX_TABLES];
+  int rows[MAX_TABLES];
+  int width[MAX_TABLES];
+  int off[MAX_TABLES];
+};
+
+// Per-lane element map of a sample row: element e = lane + 64 r.
+template <int RM>
+struct LaneMap {
+  const float* base[RM];  // row-0 address of this element's source (or a valid dummy)
+  int stride[RM];         // source row stride (floats)
+  int tab[RM];            // table index, NUM_TAB or NO_ELEM
+  int col[RM];            // column inside the table row
 };
 
 template <int RM>
-__device__ __forceinline__ void lane_map(const GatherDesc& g, int lane, int (&tab)[RM],
-                                         int (&col)[RM]) {
+__device__ __forceinline__ void make_lanes(const GatherDesc& g, const TabLds& tl, const float* num,
+                                           int lane, LaneMap<RM>& m) {
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
-    int e = lane + WAVE * r;
-    tab[r] = NO_ELEM;
-    col[r] = 0;
+    const int e = lane + WAVE * r;
+    int t = NO_ELEM, col = 0;
     if (e < g.D) {
-      int off = 0, t = 0;
-      for (; t < g.n_tab; ++t) {
-        if (e < off + g.width[t]) break;
-        off += g.width[t];
+      t = NUM_TAB;
+      col = e - (g.D - g.n_num);
+      for (int q = 0; q < g.n_tab; ++q)
+        if (e >= tl.off[q] && e < tl.off[q] + tl.width[q]) { t = q; col = e - tl.off[q]; }
+    }
+    m.tab[r] = t;
+    m.col[r] = col;
+    m.base[r] = t >= 0 ? tl.tab[t] + col : (t == NUM_TAB ? num + col : tl.tab[0]);
+    m.stride[r] = t >= 0 ? tl.width[t] : (t == NUM_TAB ? g.n_num : 0);
+  }
+}
+
+// Stage the clamped row ids of samples [b0, b0 + S) into LDS ids[S][n_tab]
+// (tail samples get id 0, a valid row).  Coalesced: consecutive threads read
+// consecutive index entries.
+__device__ __forceinline__ void stage_ids(const GatherDesc& g, const TabLds& tl,
+                                          const int64_t* user, const int64_t* item,
+                                          const int64_t* cat, int64_t b0, int S, int64_t B,
+                                          int* ids, int* err, int check) {
+  const int nt = g.n_tab;
+  for (int e = threadIdx.x; e < S * nt; e += NT) {
+    const int s = e / nt, t = e - s * nt;
+    const int64_t b = b0 + s;
+    int id = 0;
+    if (b < B) {
+      int64_t raw = t == 0 ? user[b] : t == 1 ? item[b] : cat[b * (nt - 2) + (t - 2)];
+      const int64_t n = tl.rows[t];
+      if (raw < 0 || raw >= n) {
+        if (check && err) atomicOr(err, 1);
+        raw = raw < 0 ? 0 : n - 1;
       }
-      tab[r] = t < g.n_tab ? t : NUM_TAB;
-      col[r] = e - off;
+      id = (int)raw;
     }
+    ids[e] = id;
   }
 }
 
-// lanes < n_tab hold the (clamped) row index of table `lane` for sample b
-__device__ __forceinline__ int load_ids(const GatherDesc& g, const int64_t* user,
-                                        const int64_t* item, const int64_t* cat, int64_t b,
-                                        int lane, int* err, int check) {
-  int id = 0;
-  if (lane < g.n_tab) {
-    int64_t raw = lane == 0 ? user[b] : lane == 1 ? item[b]
-                                                  : cat[b * (g.n_tab - 2) + (lane - 2)];
-    int64_t n = g.rows[lane];
-    if (raw < 0 || raw >= n) {
-      if (check && err) atomicOr(err, 1);
-      raw = raw < 0 ? 0 : n - 1;
-    }
-    id = (int)raw;
-  }
-  return id;
-}
-
+// x0 row of tile-sample s (global row b, clamped for the tail): RM loads, all
+// unconditional
 template <int RM>
-__device__ __forceinline__ void gather_row(const GatherDesc& g, const TabLds& tl,
-                                           const float* num, int64_t b, int myid,
-                                           const int (&tab)[RM], const int (&col)[RM],
-                                           int (&ids)[RM], float (&x)[RM]) {
+__device__ __forceinline__ void load_row(const LaneMap<RM>& m, const int* ids_s, int64_t bc,
+                                         float (&x)[RM]) {
 #pragma unroll
   for (int r = 0; r < RM; ++r) {
-    int t = tab[r];
-    int id = __shfl(myid, t >= 0 ? t : 0, WAVE);
-    ids[r] = id;
-    float v = 0.f;
-    if (t >= 0) v = tl.tab[t][(int64_t)id * tl.width[t] + col[r]];
-    else if (t == NUM_TAB) v = num[b * g.n_num + col[r]];
-    x[r] = v;
+    const int t = m.tab[r];
+    const int64_t row = t >= 0 ? (int64_t)ids_s[t] : (t == NUM_TAB ? bc : 0);
+    x[r] = m.base[r][row * m.stride[r]];
+  }
+#pragma unroll
+  for (int r = 0; r < RM; ++r) x[r] = m.tab[r] == NO_ELEM ? 0.f : x[r];
+}
+
+__device__ __forceinline__ void fill_tab_lds(const GatherDesc& g, TabLds& tl, float* const* grad) {
+  for (int i = threadIdx.x; i < g.n_tab; i += NT) {
+    tl.tab[i] = g.tab[i];
+    tl.rows[i] = (int)g.rows[i];
+    tl.width[i] = g.width[i];
+    tl.off[i] = g.off[i];
+    tl.grad[i] = grad ? grad[i] : nullptr;
   }
 }
 
-template <typename T, int RM>
+// ---------------------------------------------------------------- forward
+// SPW samples per wave per tile, all row loads of a tile issued before use.
+template <typename T, int RM, int SPW>
 __global__ __launch_bounds__(NT) void gather_cross_fwd_kernel(GatherDesc g, CrossParams cp,
                                                                const int64_t* user,
                                                                const int64_t* item,
@@ -94,92 +139,149 @@ __global__ __launch_bounds__(NT) void gather_cross_fwd_kernel(GatherDesc g, Cros
                                                                const float* num, int64_t B, T* x0,
                                                                int ldx, float* zc, int* err,
                                                                int check) {
+  constexpr int S = SPW * WPB;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ TabLds tl;
   const int D = g.D, L = cp.L;
   float* sw = smem;              // [L][D]
   float* sb = sw + L * D;        // [L][D]
   float* swf = sb + L * D;       // [D]
+  int* ids = reinterpret_cast<int*>(swf + D);  // [S][n_tab]
+  // per-wave bf16 staging row for the x0 store (16-B aligned)
+  bf16* stage = reinterpret_cast<bf16*>(smem + ((L * D * 2 + D + S * g.n_tab + 3) & ~3)) +
+                (threadIdx.x >> 6) * RM * WAVE;
+  static_assert(SPW == 4, "the forward reduces 4 samples per wave together");
   for (int i = threadIdx.x; i < L * D; i += NT) {
     sw[i] = cp.w[i / D][i % D];
     sb[i] = cp.b[i / D][i % D];
   }
   for (int i = threadIdx.x; i < D; i += NT) swf[i] = cp.wf_cross[i];
-  for (int i = threadIdx.x; i < g.n_tab; i += NT) {
-    tl.tab[i] = g.tab[i];
-    tl.width[i] = g.width[i];
-  }
+  fill_tab_lds(g, tl, nullptr);
   __syncthreads();
 
-  const int lane = threadIdx.x & 63;
-  int tab[RM], col[RM], ids[RM];
-  lane_map<RM>(g, lane, tab, col);
-  float x[RM];
-  const int64_t nw = (int64_t)gridDim.x * WPB;
-  for (int64_t b = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6); b < B; b += nw) {
-    int myid = load_ids(g, user, item, cat, b, lane, err, check);
-    gather_row<RM>(g, tl, num, b, myid, tab, col, ids, x);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  LaneMap<RM> m;
+  make_lanes<RM>(g, tl, num, lane, m);
+  const int64_t ntiles = (B + S - 1) / S;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t b0 = tile * S;
+    __syncthreads();  // the previous tile's ids are consumed
+    stage_ids(g, tl, user, item, cat, b0, S, B, ids, err, check);
+    __syncthreads();
+    float x[SPW][RM];
 #pragma unroll
-    for (int r = 0; r < RM; ++r) {
-      int e = lane + WAVE * r;
-      if (e < ldx) St<T>::st(x0 + b * ldx + e, x[r]);  // pad columns get 0
+    for (int u = 0; u < SPW; ++u) {
+      const int s = w * SPW + u;
+      const int64_t b = b0 + s;
+      if constexpr (!(GC_LAB_MODE & 4))
+        load_row<RM>(m, ids + s * g.n_tab, b < B ? b : B - 1, x[u]);
+      else
+        for (int r = 0; r < RM; ++r) x[u][r] = (float)ids[s * g.n_tab + (r & 1)];
     }
-    for (int l = 0; l < L; ++l) {
-      float d = 0.f;
+    // x0 in the deep tower's storage type.  bf16: staged through this wave's
+    // LDS row so every lane stores 16 contiguous bytes (8 columns)
+#pragma unroll
+    for (int u = 0; u < SPW; ++u) {
+      const int64_t b = b0 + w * SPW + u;
+      if constexpr (!(GC_LAB_MODE & 1)) {
+        if constexpr (sizeof(T) == 2) {
+#pragma unroll
+          for (int r = 0; r < RM; ++r) {
+            const int e = lane + WAVE * r;
+            if (e < ldx) stage[e] = (bf16)x[u][r];   // pad columns get 0
+          }
+          if (b < B && lane * 8 < ldx)
+            *reinterpret_cast<uint4*>(x0 + b * ldx + lane * 8) =
+                *reinterpret_cast<const uint4*>(stage + lane * 8);
+          if constexpr (RM > 8)
+            if (b < B && (lane + 64) * 8 < ldx)
+              *reinterpret_cast<uint4*>(x0 + b * ldx + (lane + 64) * 8) =
+                  *reinterpret_cast<const uint4*>(stage + (lane + 64) * 8);
+        } else {
+#pragma unroll
+          for (int r = 0; r < RM; ++r) {
+            const int e = lane + WAVE * r;
+            if (b < B && e < ldx) St<T>::st(x0 + b * ldx + e, x[u][r]);
+          }
+        }
+      }
+    }
+    // cross stack: the SPW (=4) samples' dot products are reduced together
+    if constexpr (!(GC_LAB_MODE & 2)) {
+      for (int l = 0; l < L; ++l) {
+        float d[SPW];
+#pragma unroll
+        for (int u = 0; u < SPW; ++u) {
+          d[u] = 0.f;
+#pragma unroll
+          for (int r = 0; r < RM; ++r) {
+            const int e = lane + WAVE * r;
+            if (e < D) d[u] += x[u][r] * sw[l * D + e];
+          }
+        }
+        float sl[SPW];
+        wave_sum4(d[0], d[1], d[2], d[3], sl[0], sl[1], sl[2], sl[3]);
+#pragma unroll
+        for (int u = 0; u < SPW; ++u)
+#pragma unroll
+          for (int r = 0; r < RM; ++r) {
+            const int e = lane + WAVE * r;
+            if (e < D) x[u][r] = (x[u][r] + x[u][r] * sl[u]) + sb[l * D + e];
+          }
+      }
+    }
+    float z[SPW];
+#pragma unroll
+    for (int u = 0; u < SPW; ++u) {
+      z[u] = 0.f;
 #pragma unroll
       for (int r = 0; r < RM; ++r) {
-        int e = lane + WAVE * r;
-        if (e < D) d += x[r] * sw[l * D + e];
-      }
-      float s = wave_sum(d);
-#pragma unroll
-      for (int r = 0; r < RM; ++r) {
-        int e = lane + WAVE * r;
-        if (e < D) x[r] = (x[r] + x[r] * s) + sb[l * D + e];
+        const int e = lane + WAVE * r;
+        if (e < D) z[u] += x[u][r] * swf[e];
       }
     }
-    float z = 0.f;
-#pragma unroll
-    for (int r = 0; r < RM; ++r) {
-      int e = lane + WAVE * r;
-      if (e < D) z += x[r] * swf[e];
+    float zs[SPW];
+    wave_sum4(z[0], z[1], z[2], z[3], zs[0], zs[1], zs[2], zs[3]);
+    if (lane < SPW) {
+      const int64_t b = b0 + w * SPW + lane;
+      const float zv = lane == 0 ? zs[0] : lane == 1 ? zs[1] : lane == 2 ? zs[2] : zs[3];
+      if (b < B) zc[b] = zv;
     }
-    z = wave_sum(z);
-    if (lane == 0) zc[b] = z;
   }
 }
 
-// part layout per wave: [L][D] dw | [L][D] db | [D] dwf | [1] dbf
-template <int RM, int L>
-__global__ __launch_bounds__(NT) void cross_bwd_kernel(GatherDesc g, CrossBwdParams p,
+// --------------------------------------------------------------- backward
+// part layout per block: [L][D] dw | [L][D] db | [D] dwf | [1] dbf
+template <int RM, int L, int SPW>
+__global__ __launch_bounds__(NT, 2) void cross_bwd_kernel(GatherDesc g, CrossBwdParams p,
                                                         const int64_t* user, const int64_t* item,
                                                         const int64_t* cat, const float* num,
                                                         const float* dz, int64_t B,
                                                         const float* dx0_deep, int ld_dx,
                                                         float* part) {
+  constexpr int S = SPW * WPB;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ TabLds tl;
   const int D = g.D;
   float* sw = smem;
   float* sb = sw + L * D;
   float* swf = sb + L * D;
+  float* red = swf + D;                                   // [(2L+1)D+1] block partial
+  int* ids = reinterpret_cast<int*>(red + (2 * L + 1) * D + 1);  // [S][n_tab]
+  // per-wave cross activations x_0..x_L of the sample in flight (LDS instead
+  // of 32+ registers: keeps the kernel at 2 waves/SIMD without spills)
+  float* xsl = reinterpret_cast<float*>(ids + S * g.n_tab) + (threadIdx.x >> 6) * (L + 1) * RM * WAVE;
   for (int i = threadIdx.x; i < L * D; i += NT) {
     sw[i] = p.cp.w[i / D][i % D];
     sb[i] = p.cp.b[i / D][i % D];
   }
   for (int i = threadIdx.x; i < D; i += NT) swf[i] = p.cp.wf_cross[i];
-  for (int i = threadIdx.x; i < g.n_tab; i += NT) {
-    tl.tab[i] = g.tab[i];
-    tl.grad[i] = p.emb_grad[i];
-    tl.width[i] = g.width[i];
-  }
+  fill_tab_lds(g, tl, p.emb_grad);
   __syncthreads();
 
-  const int lane = threadIdx.x & 63;
-  int tab[RM], col[RM], ids[RM];
-  lane_map<RM>(g, lane, tab, col);
-  float xs[L + 1][RM];
-  float s[L > 0 ? L : 1];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  LaneMap<RM> m;
+  make_lanes<RM>(g, tl, num, lane, m);
   float dwa[L > 0 ? L : 1][RM], dba[L > 0 ? L : 1][RM], dwfa[RM];
   float dbf = 0.f;
 #pragma unroll
@@ -188,70 +290,96 @@ __global__ __launch_bounds__(NT) void cross_bwd_kernel(GatherDesc g, CrossBwdPar
 #pragma unroll
     for (int l = 0; l < L; ++l) { dwa[l][r] = 0.f; dba[l][r] = 0.f; }
   }
-  const int64_t wid = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
-  const int64_t nw = (int64_t)gridDim.x * WPB;
-  for (int64_t b = wid; b < B; b += nw) {
-    int myid = load_ids(g, user, item, cat, b, lane, nullptr, 0);
-    gather_row<RM>(g, tl, num, b, myid, tab, col, ids, xs[0]);
+  const int64_t ntiles = (B + S - 1) / S;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t b0 = tile * S;
+    __syncthreads();
+    stage_ids(g, tl, user, item, cat, b0, S, B, ids, nullptr, 0);
+    __syncthreads();
+    float x[SPW][RM], dd[SPW][RM], dzv[SPW];
 #pragma unroll
-    for (int l = 0; l < L; ++l) {
-      float d = 0.f;
-#pragma unroll
-      for (int r = 0; r < RM; ++r) {
-        int e = lane + WAVE * r;
-        if (e < D) d += xs[l][r] * sw[l * D + e];
-      }
-      s[l] = wave_sum(d);
-#pragma unroll
-      for (int r = 0; r < RM; ++r) {
-        int e = lane + WAVE * r;
-        xs[l + 1][r] = e < D ? (xs[l][r] + xs[l][r] * s[l]) + sb[l * D + e] : 0.f;
-      }
-    }
-    const float dd = dz[b];
-    dbf += dd;
-    float gr[RM];
-#pragma unroll
-    for (int r = 0; r < RM; ++r) {
-      int e = lane + WAVE * r;
-      gr[r] = e < D ? dd * swf[e] : 0.f;
-      dwfa[r] += dd * xs[L][r];
-    }
-#pragma unroll
-    for (int l = L - 1; l >= 0; --l) {
-      float d = 0.f;
-#pragma unroll
-      for (int r = 0; r < RM; ++r) d += gr[r] * xs[l][r];
-      float gx = wave_sum(d);
+    for (int u = 0; u < SPW; ++u) {
+      const int s = w * SPW + u;
+      const int64_t b = b0 + s;
+      const int64_t bc = b < B ? b : B - 1;
+      load_row<RM>(m, ids + s * g.n_tab, bc, x[u]);
 #pragma unroll
       for (int r = 0; r < RM; ++r) {
-        int e = lane + WAVE * r;
-        dba[l][r] += gr[r];
-        dwa[l][r] += gx * xs[l][r];
-        gr[r] = e < D ? gr[r] * (1.f + s[l]) + gx * sw[l * D + e] : 0.f;
+        const int e = lane + WAVE * r;
+        dd[u][r] = dx0_deep[bc * ld_dx + (e < ld_dx ? e : 0)];
       }
+      dzv[u] = dz[bc];
     }
-    // dx0 = cross part + deep part; scatter into the dense embedding grads
 #pragma unroll
-    for (int r = 0; r < RM; ++r) {
-      int t = tab[r];
-      if (t >= 0) {
-        int e = lane + WAVE * r;
-        float v = gr[r] + dx0_deep[b * ld_dx + e];
-        atomicAdd(tl.grad[t] + (int64_t)ids[r] * tl.width[t] + col[r], v);
+    for (int u = 0; u < SPW; ++u) {
+      const int s = w * SPW + u;
+      const int64_t b = b0 + s;
+      if (b >= B) break;
+      float sl[L > 0 ? L : 1];
+      float xc[RM];
+#pragma unroll
+      for (int r = 0; r < RM; ++r) xc[r] = x[u][r];
+#pragma unroll
+      for (int l = 0; l < ((GC_LAB_MODE & 16) ? 0 : L); ++l) {
+        float d = 0.f;
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          const int e = lane + WAVE * r;
+          xsl[(l * RM + r) * WAVE + lane] = xc[r];
+          if (e < D) d += xc[r] * sw[l * D + e];
+        }
+        sl[l] = wave_sum_dpp(d);
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          const int e = lane + WAVE * r;
+          xc[r] = e < D ? (xc[r] + xc[r] * sl[l]) + sb[l * D + e] : 0.f;
+        }
+      }
+      const float dzb = dzv[u];
+      dbf += dzb;
+      float gr[RM];
+#pragma unroll
+      for (int r = 0; r < RM; ++r) {
+        const int e = lane + WAVE * r;
+        gr[r] = e < D ? dzb * swf[e] : 0.f;
+        dwfa[r] += dzb * xc[r];
+      }
+#pragma unroll
+      for (int l = ((GC_LAB_MODE & 16) ? -1 : L - 1); l >= 0; --l) {
+        float xl[RM];
+#pragma unroll
+        for (int r = 0; r < RM; ++r) xl[r] = xsl[(l * RM + r) * WAVE + lane];
+        float d = 0.f;
+#pragma unroll
+        for (int r = 0; r < RM; ++r) d += gr[r] * xl[r];
+        const float gx = wave_sum_dpp(d);
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          const int e = lane + WAVE * r;
+          dba[l][r] += gr[r];
+          dwa[l][r] += gx * xl[r];
+          gr[r] = e < D ? gr[r] * (1.f + sl[l]) + gx * sw[l * D + e] : 0.f;
+        }
+      }
+      // dx0 = cross part + deep part -> embedding grads
+      const int* ids_s = ids + s * g.n_tab;
+#pragma unroll
+      for (int r = 0; r < RM; ++r) {
+        const int t = m.tab[r];
+        const float v = gr[r] + dd[u][r];
+        if constexpr (!(GC_LAB_MODE & 8))
+          if (t >= 0) atomicAdd(tl.grad[t] + (int64_t)ids_s[t] * tl.width[t] + m.col[r], v);
       }
     }
   }
   // block-level partial: the 4 waves add into LDS in fixed wave order
   // (deterministic), then one coalesced store per block
   const int stride = (2 * L + 1) * D + 1;
-  float* red = swf + D;   // [stride] after the weight region
-  const int w = threadIdx.x >> 6;
   for (int ww = 0; ww < WPB; ++ww) {
     if (w == ww) {
 #pragma unroll
       for (int r = 0; r < RM; ++r) {
-        int e = lane + WAVE * r;
+        const int e = lane + WAVE * r;
         if (e >= D) continue;
 #pragma unroll
         for (int l = 0; l < L; ++l) {
@@ -268,40 +396,72 @@ __global__ __launch_bounds__(NT) void cross_bwd_kernel(GatherDesc g, CrossBwdPar
   for (int i = threadIdx.x; i < stride; i += NT) mp[i] = red[i];
 }
 
-// reduce per-block partials -> grads (8 elements x 32 lanes per block, fixed order)
-__global__ __launch_bounds__(NT) void cross_reduce_kernel(const float* part, int64_t nb, int D,
-                                                          int L, CrossBwdParams p, int accumulate) {
-  __shared__ float red[32][8];
-  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
-  const int64_t stride = (int64_t)(2 * L + 1) * D + 1;
-  const int64_t i = (int64_t)blockIdx.x * 8 + tx;
+// Reduce per-block partials -> grads.  Block = 64 columns x 4 partial lanes
+// over a range of partial rows (RED_G ranges in blockIdx.y), fp32 block sums
+// to cred2 [RED_G][stride], and the last arriver of each column group adds the
+// RED_G sums in fixed order and writes the gradients.
+__global__ __launch_bounds__(NT) void cross_reduce_kernel(const float* part, int nb, int D, int L,
+                                                          CrossBwdParams p, float* red2,
+                                                          int* counters, int accumulate) {
+  __shared__ float red[4 * 64 + 1];
+  int* flag = reinterpret_cast<int*>(&red[4 * 64]);
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int stride = (2 * L + 1) * D + 1;
+  const int i = blockIdx.x * 64 + tx;
+  const int g = blockIdx.y;
+  const int per = (nb + RED_G - 1) / RED_G;
+  const int w0 = g * per, w1 = min(nb, w0 + per);
+  const __amdgpu_buffer_rsrc_t pr = buf_rsrc(part, (int64_t)nb * stride * 4);
+  constexpr int U = 8;
   float s = 0.f;
-  if (i < stride)
-    for (int64_t w = ty; w < nb; w += 32) s += part[w * stride + i];
-  red[ty][tx] = s;
-  __syncthreads();
-  for (int o = 16; o > 0; o >>= 1) {
-    if (ty < o) red[ty][tx] += red[ty + o][tx];
-    __syncthreads();
+  for (int wr = w0 + ty; wr < w1; wr += 4 * U) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ww = wr + 4 * u;
+      const bool ok = i < stride && ww < w1;
+      v[u] = __uint_as_float(
+          __builtin_amdgcn_raw_buffer_load_b32(pr, ok ? (ww * stride + i) * 4 : OOR, 0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s += v[u];
   }
+  red[ty * 64 + tx] = s;
+  __syncthreads();
+  if (ty == 0 && i < stride)
+    red2[(int64_t)g * stride + i] = ((red[tx] + red[64 + tx]) + red[128 + tx]) + red[192 + tx];
+  if (!last_arriver(&counters[blockIdx.x], RED_G, flag)) return;
   if (ty != 0 || i >= stride) return;
-  s = red[0][tx];
+  const __amdgpu_buffer_rsrc_t rr = buf_rsrc(red2, (int64_t)RED_G * stride * 4);
+  float v[RED_G];
+#pragma unroll
+  for (int q = 0; q < RED_G; ++q)
+    v[q] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rr, (q * stride + i) * 4, 0, 0));
+  float t = 0.f;
+#pragma unroll
+  for (int q = 0; q < RED_G; ++q) t += v[q];
   float* dst;
-  if (i < (int64_t)L * D) dst = p.dw[i / D] + i % D;
-  else if (i < (int64_t)2 * L * D) dst = p.db[(i - L * D) / D] + (i - L * D) % D;
+  if (i < L * D) dst = p.dw[i / D] + i % D;
+  else if (i < 2 * L * D) dst = p.db[(i - L * D) / D] + (i - L * D) % D;
   else if (i < stride - 1) dst = p.dwf_cross + (i - 2 * L * D);
   else dst = p.dbf;
-  *dst = accumulate ? *dst + s : s;
+  *dst = accumulate ? *dst + t : t;
 }
+
+// -------------------------------------------------------------- launchers
+constexpr int FWD_SPW = 4;   // samples per wave per tile (forward)
+constexpr int BWD_SPW = 1;   // (backward: 2 waves/SIMD need the registers)
 
 template <typename T, int RM>
 dcnr_status launch_fwd(const GatherDesc& g, const CrossParams& cp, const int64_t* user,
                        const int64_t* item, const int64_t* cat, const float* num, int64_t B,
                        void* x0, int ldx, float* zc, int* err, int check, hipStream_t s) {
-  size_t lds = (size_t)(2 * cp.L + 1) * g.D * sizeof(float);
-  int64_t blocks = std::min<int64_t>(cdiv(B, WPB), 256 * 8);
-  hipLaunchKernelGGL((gather_cross_fwd_kernel<T, RM>), dim3((unsigned)blocks), dim3(NT), lds, s, g,
-                     cp, user, item, cat, num, B, (T*)x0, ldx, zc, err, check);
+  constexpr int S = FWD_SPW * WPB;
+  size_t lds = (size_t)(((2 * cp.L + 1) * g.D + S * g.n_tab + 3) & ~3) * sizeof(float) +
+               (size_t)WPB * RM * WAVE * sizeof(bf16);
+  int64_t blocks = std::min<int64_t>(cdiv(B, S), 256 * 8);
+  hipLaunchKernelGGL((gather_cross_fwd_kernel<T, RM, FWD_SPW>), dim3((unsigned)blocks), dim3(NT),
+                     lds, s, g, cp, user, item, cat, num, B, (T*)x0, ldx, zc, err, check);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
@@ -309,11 +469,19 @@ dcnr_status launch_fwd(const GatherDesc& g, const CrossParams& cp, const int64_t
 template <int RM, int L>
 dcnr_status launch_bwd(const GatherDesc& g, const CrossBwdParams& p, const int64_t* user,
                        const int64_t* item, const int64_t* cat, const float* num, const float* dz,
-                       int64_t B, const float* dx0, int ld_dx, float* part, int64_t nw,
+                       int64_t B, const float* dx0, int ld_dx, float* part, int64_t nb,
                        hipStream_t s) {
-  size_t lds = (size_t)(2 * (2 * L + 1) * g.D + 1) * sizeof(float);
-  hipLaunchKernelGGL((cross_bwd_kernel<RM, L>), dim3((unsigned)nw), dim3(NT), lds, s, g, p,
-                     user, item, cat, num, dz, B, dx0, ld_dx, part);
+  constexpr int S = BWD_SPW * WPB;
+  size_t lds = (size_t)(2 * (2 * L + 1) * g.D + 1) * sizeof(float) +
+               (size_t)S * g.n_tab * sizeof(int) + (size_t)WPB * (L + 1) * RM * WAVE * sizeof(float);
+  static size_t attr_lds = 0;   // raise the dynamic-LDS limit once per size class
+  if (lds > 64 * 1024 && lds > attr_lds) {
+    DCNR_HIP(hipFuncSetAttribute((const void*)cross_bwd_kernel<RM, L, BWD_SPW>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr_lds = lds;
+  }
+  hipLaunchKernelGGL((cross_bwd_kernel<RM, L, BWD_SPW>), dim3((unsigned)nb), dim3(NT), lds, s, g,
+                     p, user, item, cat, num, dz, B, dx0, ld_dx, part);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
@@ -322,10 +490,10 @@ template <int RM>
 dcnr_status dispatch_bwd_L(int L, const GatherDesc& g, const CrossBwdParams& p,
                            const int64_t* user, const int64_t* item, const int64_t* cat,
                            const float* num, const float* dz, int64_t B, const float* dx0,
-                           int ld_dx, float* part, int64_t nw, hipStream_t s) {
+                           int ld_dx, float* part, int64_t nb, hipStream_t s) {
   switch (L) {
 #define CASE(n) \
-  case n: return launch_bwd<RM, n>(g, p, user, item, cat, num, dz, B, dx0, ld_dx, part, nw, s);
+  case n: return launch_bwd<RM, n>(g, p, user, item, cat, num, dz, B, dx0, ld_dx, part, nb, s);
     CASE(0) CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7)
 #undef CASE
   }
@@ -333,18 +501,20 @@ dcnr_status dispatch_bwd_L(int L, const GatherDesc& g, const CrossBwdParams& p,
   return DCNR_UNSUPPORTED_SHAPE;
 }
 
-constexpr int64_t BWD_BLOCKS = 2048;  // x4 waves: 32 waves/CU of latency hiding
+int64_t bwd_blocks(int64_t B) { return std::max<int64_t>(1, std::min<int64_t>(cdiv(B, BWD_SPW * WPB), BWD_BLOCKS)); }
 
 }  // namespace
 
 size_t cross_bwd_part_elems(int D, int L) { return (size_t)BWD_BLOCKS * ((2 * L + 1) * D + 1); }
+size_t cross_red2_elems(int D, int L) { return (size_t)RED_G * ((2 * L + 1) * D + 1); }
+int cross_red_groups(int D, int L) { return (int)cdiv((2 * L + 1) * D + 1, 64); }
 
 dcnr_status gather_cross_fwd(int precision, const GatherDesc& g, const CrossParams& cp,
                              const int64_t* user, const int64_t* item, const int64_t* cat,
                              const float* num, int64_t B, void* x0, int ldx, float* zc, int* err,
                              int check, hipStream_t s) {
   if (B <= 0) return DCNR_OK;
-  if (g.D > 16 * WAVE || cp.L > 8 || g.n_tab > 66) {
+  if (g.D > 16 * WAVE || cp.L > 8 || g.n_tab > MAX_TABLES) {
     set_error("gather: unsupported D=%d / n_cross=%d / tables=%d", g.D, cp.L, g.n_tab);
     return DCNR_UNSUPPORTED_SHAPE;
   }
@@ -359,25 +529,26 @@ dcnr_status gather_cross_fwd(int precision, const GatherDesc& g, const CrossPara
 dcnr_status cross_bwd_scatter(const GatherDesc& g, const CrossBwdParams& p, const int64_t* user,
                               const int64_t* item, const int64_t* cat, const float* num,
                               const float* dz, int64_t B, const float* dx0_deep, int ld_dx,
-                              float* part, size_t part_elems, int accumulate, hipStream_t s) {
+                              const CrossBwdScratch& ws, int accumulate, hipStream_t s) {
   const int L = p.cp.L, D = g.D;
-  if (part_elems < cross_bwd_part_elems(D, L)) {
-    set_error("cross_bwd: partial buffer too small");
+  if (ws.part_elems < cross_bwd_part_elems(D, L) || ws.red2_elems < cross_red2_elems(D, L) ||
+      ws.n_counters < cross_red_groups(D, L)) {
+    set_error("cross_bwd: scratch too small");
     return DCNR_WORKSPACE_TOO_SMALL;
   }
   if (D > 16 * WAVE) {
     set_error("cross_bwd: D=%d unsupported", D);
     return DCNR_UNSUPPORTED_SHAPE;
   }
+  const int64_t nb = bwd_blocks(B);
   dcnr_status st = D <= 8 * WAVE
                        ? dispatch_bwd_L<8>(L, g, p, user, item, cat, num, dz, B, dx0_deep, ld_dx,
-                                           part, BWD_BLOCKS, s)
+                                           ws.part, nb, s)
                        : dispatch_bwd_L<16>(L, g, p, user, item, cat, num, dz, B, dx0_deep, ld_dx,
-                                            part, BWD_BLOCKS, s);
+                                            ws.part, nb, s);
   if (st != DCNR_OK) return st;
-  int64_t stride = (int64_t)(2 * L + 1) * D + 1;
-  hipLaunchKernelGGL(cross_reduce_kernel, dim3((unsigned)cdiv(stride, 8)), dim3(NT), 0, s, part,
-                     BWD_BLOCKS, D, L, p, accumulate);
+  hipLaunchKernelGGL(cross_reduce_kernel, dim3((unsigned)cross_red_groups(D, L), RED_G), dim3(NT),
+                     0, s, ws.part, (int)nb, D, L, p, ws.red2, ws.counters, accumulate);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }

@@ -65,17 +65,25 @@ def assert_grads_close(grads: dict, ref: dict, rtol=5e-3, atol=1e-7, names=None)
     assert not bad, f"grad mismatches: {bad}"
 
 
+def _fmix32(x):
+    U = np.uint32
+    x = x ^ (x >> U(16)); x = x * U(0x85EBCA6B)
+    x = x ^ (x >> U(13)); x = x * U(0xC2B2AE35)
+    return x ^ (x >> U(16))
+
+
 def dropout_mask_np(seed: int, layer: int, B: int, H: int, p: float) -> np.ndarray:
-    """Host replica of libdcnr's counter-based dropout keep-test
-    (csrc/dcnr_internal.h dropout_keep): keep(seed, layer, row, col)."""
-    M = np.uint64
+    """Host replica of libdcnr's counter-based dropout mask
+    (csrc/dcnr_internal.h dropout_bits): 32 bits per (row, column pair), low
+    16 bits for the even column, high 16 for the odd one; keep iff the 16
+    bits >= round(p * 65536)."""
+    U = np.uint32
     with np.errstate(over="ignore"):
-        x = M(seed) ^ (M(0x9E3779B97F4A7C15) * M(layer + 1))
-        rows = np.arange(B, dtype=np.uint64)[:, None]
-        cols = np.arange(H, dtype=np.uint64)[None, :]
-        x = x + rows * M(0x100000001B3) + cols * M(0xC2B2AE3D27D4EB4F)
-        x = x ^ (x >> M(30)); x = x * M(0xBF58476D1CE4E5B9)
-        x = x ^ (x >> M(27)); x = x * M(0x94D049BB133111EB)
-        x = x ^ (x >> M(31))
-    thresh = np.uint64(min(4294967295.0, float(np.float32(p)) * 4294967296.0))
-    return ((x >> M(32)) >= thresh).astype(np.float64)
+        rows = np.arange(B, dtype=np.uint64).astype(U)[:, None]
+        pairs = (np.arange(H, dtype=np.uint32) >> U(1))[None, :]
+        x = _fmix32(rows * U(0x9E3779B1) ^ U(seed & 0xFFFFFFFF) ^ U((layer * 0x7FEB352D) & 0xFFFFFFFF))
+        x = _fmix32((x + pairs * U(0x846CA68B)) ^ U(seed >> 32))
+    odd = (np.arange(H) & 1).astype(bool)[None, :]
+    bits16 = np.where(odd, x >> U(16), x & U(0xFFFF))
+    thresh = min(65536, int(np.floor(float(np.float32(p)) * 65536.0 + 0.5)))
+    return (bits16.astype(np.int64) >= thresh).astype(np.float64)
