@@ -167,7 +167,8 @@ struct Layout {
   void* x0;
   void* h[MAX_RES + 1];
   void* t1[MAX_RES]; void* t2[MAX_RES];
-  void* a1;
+  void* a1;                 // eval: BN1/ReLU output scratch; train: backward scratch (dt1)
+  void* a1s[MAX_RES];       // train: each block's dropout(relu(BN1(t1))), saved for dW2
   float* zc; float* zdeep;
   BnBufs bn[2 * MAX_RES];
   float* part; double* sums; float* coef;
@@ -211,6 +212,8 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws) {
     for (int j = 0; j < d.R; ++j) L.t1[j] = L.t2[j] = t;
   }
   L.a1 = b.take(act);
+  if (train)
+    for (int j = 0; j < d.R; ++j) L.a1s[j] = b.take(act);
   L.zc = (float*)b.take(B * 4);
   L.zdeep = (float*)b.take(B * 4);
   for (int i = 0; i < 2 * d.R; ++i) {
@@ -551,9 +554,10 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
     TRY(bn_layer_fwd(desc, d, L, L.t1[j], B, train, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
                      L.bn[2 * j], s));
-    TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], L.a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
+    void* a1 = train ? L.a1s[j] : L.a1;
+    TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
                      dropout_seed, j, s));
-    TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
+    TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
     TRY(bn_layer_fwd(desc, d, L, L.t2[j], B, train, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
                      L.bn[2 * j + 1], s));
     const bool head = j == d.R - 1 && bn_add_relu_head_supported(d.prec, d.Hp);
@@ -595,9 +599,12 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   const int Hp = d.Hp, H = d.H;
   const float p = d.dropout;
   // dense embedding grads: zeroed, then scatter-added by the cross backward
-  if (!accumulate)
-    for (int t = 0; t < 2 + d.K; ++t)
-      TRYP(DCNR_K_PACK, fill_zero(Gr.tab[t], (size_t)d.rows[t] * d.widths[t] * 4, s));
+  if (!accumulate) {
+    void* zp[2 + MAX_CAT];
+    int64_t zn[2 + MAX_CAT];
+    for (int t = 0; t < 2 + d.K; ++t) { zp[t] = Gr.tab[t]; zn[t] = d.rows[t] * d.widths[t] * 4; }
+    TRYP(DCNR_K_PACK, fill_zero_multi(2 + d.K, zp, zn, s));
+  }
 
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   for (int j = d.R - 1; j >= 0; --j) {
@@ -608,16 +615,15 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     int nc = 0;
     // ---- out = relu(BN2(t2) + h_j):  du, BN2 backward
     TRYP(DCNR_K_ROWWISE, bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, B, Hp,
-                       Hp, L.part, &nc, s));
+                       Hp, L.du, L.part, &nc, s));
     // dbeta2, dgamma2 and (last block only) dW_f[:H]
     TRY(bn_bwd_reduce(desc, d, L, nc, 3, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, Gin ? nullptr : Gr.wf,
                       accumulate, s));
-    TRYP(DCNR_K_ROWWISE, bwd_bn2_apply2(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, L.coef,
-                       B, Hp, Hp, L.dt2, L.du, L.part, &nc, s));
+    TRYP(DCNR_K_ROWWISE, bwd_bn2_apply2(d.prec, L.du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
+                       L.dt2, L.part, &nc, s));
     TRY(bias_reduce(d, L, nc, Gk.b2, accumulate, s));  // dbias2
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
-    TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], L.a1, B, Hp, Hp, bn1.scale, bn1.shift, p, dropout_seed, j, s));
-    TRY(linear_dw(d, L, L.dt2, Hp, Hp, L.a1, Hp, Hp, B, Gk.w2, H, H, accumulate, s));
+    TRY(linear_dw(d, L, L.dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s));
     {
       GemmArgs g;
       memset(&g, 0, sizeof(g));

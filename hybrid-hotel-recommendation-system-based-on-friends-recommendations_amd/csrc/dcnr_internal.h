@@ -297,14 +297,15 @@ dcnr_status bn_add_relu2(int precision, const void* t, const void* x, void* out,
 // backward helpers -----------------------------------------------------
 // du = g*[out>0], g = G[b,n] (G != null) or dz[b]*wf[n]; NK=3 partials:
 // [du, du*xhat, dz*out] (xhat = (t-mean)*invstd; the 3rd only when G == null)
+// (also writes du = g*[out>0] in the storage type)
 dcnr_status bwd_bn2_stats3(int precision, const void* G, const float* dz, const float* wf,
                            const void* out, const void* t, const float* mean, const float* invstd,
-                           int64_t B, int N, int ld, float* part, int* nchunks, hipStream_t s);
-// dt = coef0*du - coef1*xhat - coef2 ; writes dt and du ; NK=1 partials of dt
-dcnr_status bwd_bn2_apply2(int precision, const void* G, const float* dz, const float* wf,
-                           const void* out, const void* t, const float* mean, const float* invstd,
-                           const float* coef, int64_t B, int N, int ld, void* dt, void* du,
-                           float* part, int* nchunks, hipStream_t s);
+                           int64_t B, int N, int ld, void* du, float* part, int* nchunks,
+                           hipStream_t s);
+// dt = coef0*du - coef1*xhat - coef2 ; NK=1 partials of dt
+dcnr_status bwd_bn2_apply2(int precision, const void* du, const void* t, const float* mean,
+                           const float* invstd, const float* coef, int64_t B, int N, int ld,
+                           void* dt, float* part, int* nchunks, hipStream_t s);
 // dr = da * keep/(1-p) * [t*scale+shift > 0] (in place); NK=2 partials [dr, dr*xhat]
 dcnr_status bwd_bn1_stats(int precision, void* da_dr, const void* t, const float* scale,
                           const float* shift, const float* mean, const float* invstd, int64_t B,
@@ -348,5 +349,6 @@ dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, cons
                         hipStream_t s);
 
 dcnr_status fill_zero(void* p, size_t bytes, hipStream_t s);
+dcnr_status fill_zero_multi(int n, void* const* ptrs, const int64_t* bytes, hipStream_t s);
 
 }  // namespace dcnr

@@ -237,7 +237,7 @@ template <typename T> struct BnAddReluHeadOp {
 // backward of out = relu(BN2(t2) + x): du = g*[out>0]; g = G or dz (x) wf
 template <typename T, bool HAS_G> struct Bwd2StatsOp {
   const T* G; const float* dz; const float* wf; const T* out; const T* t;
-  const float* mean; const float* invstd; int ld;
+  const float* mean; const float* invstd; int ld; T* du_out;
   struct Cst { float wf[VE<T>], mu[VE<T>], is[VE<T>]; };
   struct Reg { float o[VE<T>], t[VE<T>], g[VE<T>]; float d = 0.f; };
   __device__ void prep(int c, Cst& q) const {
@@ -250,55 +250,47 @@ template <typename T, bool HAS_G> struct Bwd2StatsOp {
     if constexpr (HAS_G) ldv<T>(G + r * ld + c, q.g);
     else q.d = dz[r];
   }
-  __device__ void apply(int64_t, int, const Cst& k, Reg& q, float (&acc)[3][VE<T>]) const {
+  // du = g * [out > 0] is stored (storage type) and the sums use the stored
+  // value, so the apply pass needs only du and t
+  __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[3][VE<T>]) const {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
       float g = HAS_G ? q.g[v] : q.d * k.wf[v];
-      float du = q.o[v] > 0.f ? g : 0.f;
+      float du = (float)(T)(q.o[v] > 0.f ? g : 0.f);
       float xh = (q.t[v] - k.mu[v]) * k.is[v];
       acc[0][v] += du;
       acc[1][v] += du * xh;
       if (!HAS_G) acc[2][v] += q.d * q.o[v];
+      q.g[v] = du;
     }
+    stv<T>(du_out + r * ld + c, q.g);
   }
 };
-
-// dt = c0*du - c1*xh - c2 ; writes dt, du ; partial sum of dt (bias grad)
-template <typename T, bool HAS_G> struct Bwd2ApplyOp {
-  const T* G; const float* dz; const float* wf; const T* out; const T* t;
-  const float* mean; const float* invstd; const float* coef; int ld, N;
-  T* dt; T* du_out;
-  struct Cst { float wf[VE<T>], mu[VE<T>], is[VE<T>], k0[VE<T>], k1[VE<T>], k2[VE<T>]; };
-  struct Reg { float o[VE<T>], t[VE<T>], g[VE<T>]; float d = 0.f; };
+// dt2 = k0*du - k1*xhat - k2 (BN2 backward), column sums of dt2 (= dbias2)
+template <typename T> struct Bwd2ApplyOp {
+  const T* du; const T* t; const float* mean; const float* invstd; const float* coef; int ld, N;
+  T* dt;
+  struct Cst { float mu[VE<T>], is[VE<T>], k0[VE<T>], k1[VE<T>], k2[VE<T>]; };
+  struct Reg { float u[VE<T>], t[VE<T>]; };
   __device__ void prep(int c, Cst& q) const {
-    if (!HAS_G) ldc(wf + c, q.wf);
     ldc(mean + c, q.mu); ldc(invstd + c, q.is);
     ldc(coef + c, q.k0); ldc(coef + N + c, q.k1); ldc(coef + 2 * N + c, q.k2);
   }
   __device__ void load(int64_t r, int c, Reg& q) const {
-    ldv<T>(out + r * ld + c, q.o);
+    ldv<T>(du + r * ld + c, q.u);
     ldv<T>(t + r * ld + c, q.t);
-    if constexpr (HAS_G) ldv<T>(G + r * ld + c, q.g);
-    else q.d = dz[r];
   }
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[1][VE<T>]) const {
-    float d[VE<T>];
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      float g = HAS_G ? q.g[v] : q.d * k.wf[v];
-      float du = q.o[v] > 0.f ? g : 0.f;
       float xh = (q.t[v] - k.mu[v]) * k.is[v];
-      float y = k.k0[v] * du - k.k1[v] * xh - k.k2[v];
-      q.g[v] = du;
-      d[v] = y;
+      float y = k.k0[v] * q.u[v] - k.k1[v] * xh - k.k2[v];
+      q.u[v] = y;
       acc[0][v] += y;
     }
-    stv<T>(dt + r * ld + c, d);
-    stv<T>(du_out + r * ld + c, q.g);
+    stv<T>(dt + r * ld + c, q.u);
   }
 };
-
-// dr = da * keep/(1-p) * [t*sc+sh > 0] (in place) ; partials [dr, dr*xh]
 template <typename T> struct Bwd1StatsOp {
   T* da; const T* t; const float* sc; const float* sh; const float* mean; const float* invstd;
   int ld; float inv_keep; uint32_t thresh; uint64_t seed; int layer; int drop;
@@ -694,46 +686,39 @@ dcnr_status bn_add_relu_head(int precision, const void* t, const void* x, void* 
 template <typename T>
 static dcnr_status bwd2_stats_impl(const void* G, const float* dz, const float* wf, const void* out,
                                    const void* t, const float* mean, const float* invstd,
-                                   int64_t B, int N, int ld, float* part, int* nc, hipStream_t s) {
+                                   int64_t B, int N, int ld, void* du, float* part, int* nc,
+                                   hipStream_t s) {
   if (G) {
-    Bwd2StatsOp<T, true> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, ld};
+    Bwd2StatsOp<T, true> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, ld,
+                            (T*)du};
     return run_rowcol<T, 3>(op, B, N, part, nc, s);
   }
-  Bwd2StatsOp<T, false> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, ld};
+  Bwd2StatsOp<T, false> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, ld,
+                           (T*)du};
   return run_rowcol<T, 3>(op, B, N, part, nc, s);
 }
 dcnr_status bwd_bn2_stats3(int precision, const void* G, const float* dz, const float* wf,
                            const void* out, const void* t, const float* mean, const float* invstd,
-                           int64_t B, int N, int ld, float* part, int* nchunks, hipStream_t s) {
+                           int64_t B, int N, int ld, void* du, float* part, int* nchunks,
+                           hipStream_t s) {
   return precision == DCNR_PREC_BF16
-             ? bwd2_stats_impl<bf16>(G, dz, wf, out, t, mean, invstd, B, N, ld, part, nchunks, s)
-             : bwd2_stats_impl<float>(G, dz, wf, out, t, mean, invstd, B, N, ld, part, nchunks, s);
+             ? bwd2_stats_impl<bf16>(G, dz, wf, out, t, mean, invstd, B, N, ld, du, part, nchunks, s)
+             : bwd2_stats_impl<float>(G, dz, wf, out, t, mean, invstd, B, N, ld, du, part, nchunks, s);
 }
 
 template <typename T>
-static dcnr_status bwd2_apply_impl(const void* G, const float* dz, const float* wf,
-                                   const void* out, const void* t, const float* mean,
+static dcnr_status bwd2_apply_impl(const void* du, const void* t, const float* mean,
                                    const float* invstd, const float* coef, int64_t B, int N,
-                                   int ld, void* dt, void* du, float* part, int* nc,
-                                   hipStream_t s) {
-  if (G) {
-    Bwd2ApplyOp<T, true> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, coef,
-                            ld, N, (T*)dt, (T*)du};
-    return run_rowcol<T, 1>(op, B, N, part, nc, s);
-  }
-  Bwd2ApplyOp<T, false> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, coef,
-                           ld, N, (T*)dt, (T*)du};
+                                   int ld, void* dt, float* part, int* nc, hipStream_t s) {
+  Bwd2ApplyOp<T> op{(const T*)du, (const T*)t, mean, invstd, coef, ld, N, (T*)dt};
   return run_rowcol<T, 1>(op, B, N, part, nc, s);
 }
-dcnr_status bwd_bn2_apply2(int precision, const void* G, const float* dz, const float* wf,
-                           const void* out, const void* t, const float* mean, const float* invstd,
-                           const float* coef, int64_t B, int N, int ld, void* dt, void* du,
-                           float* part, int* nchunks, hipStream_t s) {
+dcnr_status bwd_bn2_apply2(int precision, const void* du, const void* t, const float* mean,
+                           const float* invstd, const float* coef, int64_t B, int N, int ld,
+                           void* dt, float* part, int* nchunks, hipStream_t s) {
   return precision == DCNR_PREC_BF16
-             ? bwd2_apply_impl<bf16>(G, dz, wf, out, t, mean, invstd, coef, B, N, ld, dt, du,
-                                     part, nchunks, s)
-             : bwd2_apply_impl<float>(G, dz, wf, out, t, mean, invstd, coef, B, N, ld, dt, du,
-                                      part, nchunks, s);
+             ? bwd2_apply_impl<bf16>(du, t, mean, invstd, coef, B, N, ld, dt, part, nchunks, s)
+             : bwd2_apply_impl<float>(du, t, mean, invstd, coef, B, N, ld, dt, part, nchunks, s);
 }
 
 template <typename T>
@@ -792,6 +777,53 @@ dcnr_status splitk_reduce(const float* slab, int splits, int64_t slab_stride, in
 dcnr_status fill_zero(void* p, size_t bytes, hipStream_t s) {
   if (!bytes) return DCNR_OK;
   DCNR_HIP(hipMemsetAsync(p, 0, bytes, s));
+  return DCNR_OK;
+}
+
+namespace {
+constexpr int ZB_MAX = 66;
+constexpr int ZB_CHUNK = NT * 16;   // 16-B units per block
+struct ZeroBatch {
+  char* p[ZB_MAX]; int64_t bytes[ZB_MAX]; int64_t blk0[ZB_MAX + 1]; int n;
+};
+// zero n buffers in one launch: 16-B stores for the body, 4-B for a tail
+__global__ __launch_bounds__(NT) void zero_multi_kernel(ZeroBatch zb) {
+  int t = 0;
+  while (t + 1 < zb.n && (int64_t)blockIdx.x >= zb.blk0[t + 1]) ++t;
+  char* p = zb.p[t];
+  const int64_t n16 = zb.bytes[t] / 16;
+  const int64_t u0 = ((int64_t)blockIdx.x - zb.blk0[t]) * ZB_CHUNK;
+  for (int64_t u = u0 + threadIdx.x; u < min(n16, u0 + ZB_CHUNK); u += NT)
+    reinterpret_cast<uint4*>(p)[u] = make_uint4(0, 0, 0, 0);
+  if ((int64_t)blockIdx.x == zb.blk0[t + 1] - 1)
+    for (int64_t i = n16 * 16 + threadIdx.x * 4; i < zb.bytes[t]; i += NT * 4)
+      *reinterpret_cast<float*>(p + i) = 0.f;
+}
+}  // namespace
+
+dcnr_status fill_zero_multi(int n, void* const* ptrs, const int64_t* bytes, hipStream_t s) {
+  for (int o = 0; o < n; o += ZB_MAX) {
+    ZeroBatch zb;
+    zb.n = std::min(ZB_MAX, n - o);
+    zb.blk0[0] = 0;
+    for (int i = 0; i < zb.n; ++i) {
+      zb.p[i] = (char*)ptrs[o + i];
+      zb.bytes[i] = bytes[o + i];
+      zb.blk0[i + 1] = zb.blk0[i] + std::max<int64_t>(1, cdiv(bytes[o + i] / 16, ZB_CHUNK));
+    }
+    bool aligned = true;
+    for (int i = 0; i < zb.n; ++i)
+      aligned = aligned && !((uintptr_t)zb.p[i] & 15) && !(zb.bytes[i] & 3);
+    if (!aligned) {   // unaligned buffers (not from torch's allocator): plain memsets
+      for (int i = 0; i < zb.n; ++i) {
+        dcnr_status st = fill_zero(zb.p[i], (size_t)zb.bytes[i], s);
+        if (st != DCNR_OK) return st;
+      }
+      continue;
+    }
+    hipLaunchKernelGGL(zero_multi_kernel, dim3((unsigned)zb.blk0[zb.n]), dim3(NT), 0, s, zb);
+    DCNR_LAUNCH_CHECK();
+  }
   return DCNR_OK;
 }
 

@@ -50,12 +50,19 @@ __global__ __launch_bounds__(NT) void bce_kernel(const float* z, const float* y,
   if (threadIdx.x == 0) part[blockIdx.x] = red[0];
 }
 
-__global__ void bce_final_kernel(const double* part, int n, int64_t B, float* loss) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    double s = 0.0;
-    for (int i = 0; i < n; ++i) s += part[i];
-    loss[0] = (float)(s / (double)B);
+// fixed-order (deterministic) sum of the per-block partials
+__global__ __launch_bounds__(NT) void bce_final_kernel(const double* part, int n, int64_t B,
+                                                       float* loss) {
+  __shared__ double red[NT];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < n; i += NT) s += part[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = NT / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
   }
+  if (threadIdx.x == 0) loss[0] = (float)(red[0] / (double)B);
 }
 
 constexpr int MAXT = 64;
@@ -128,7 +135,7 @@ dcnr_status bce(const float* z, const float* y, int64_t B, float* loss, float* d
   int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(BCE_BLOCKS, cdiv(B, NT)));
   hipLaunchKernelGGL(bce_kernel, dim3(blocks), dim3(NT), 0, s, z, y, B, dz, scale, part);
   DCNR_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bce_final_kernel, dim3(1), dim3(64), 0, s, part, blocks, B, loss);
+  hipLaunchKernelGGL(bce_final_kernel, dim3(1), dim3(NT), 0, s, part, blocks, B, loss);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
