@@ -463,12 +463,14 @@ dcnr_status bn_layer_fwd(const dcnr_model_desc* desc, const Dims& d, const Layou
 // the statistics across ranks first.
 dcnr_status bn_bwd_reduce(const dcnr_model_desc* desc, const Dims& d, const Layout& L, int nc,
                           int NK, int64_t B, const float* gamma, const float* invstd,
-                          float* dgamma, float* dbeta, float* dwf, int accumulate, hipStream_t s) {
+                          float* dgamma, float* dbeta, float* dwf, float* dbias_pre,
+                          int accumulate, hipStream_t s) {
   const int Hp = d.Hp, H = d.H;
   if (!desc->bn_allreduce) {
     RedFinal rf = red_init(L, RED_BN_BWD, (double)B, accumulate);
     rf.gamma = gamma; rf.invstd = invstd; rf.dgamma = dgamma; rf.dbeta = dbeta; rf.dwf = dwf;
     rf.coef = L.coef;
+    rf.dbias_pre = dbias_pre;
     TRYP(DCNR_K_REDUCE, reduce_fused(DCNR_PREC_FP32, L.part, nc, NK, Hp, H, nullptr, rf, s));
     return DCNR_OK;
   }
@@ -479,6 +481,7 @@ dcnr_status bn_bwd_reduce(const dcnr_model_desc* desc, const Dims& d, const Layo
   TRYP(DCNR_K_REDUCE, sums_to_grad(L.sums, H, dbeta, accumulate, s));
   TRY(hook(desc, d, L, s));
   TRYP(DCNR_K_REDUCE, bn_bwd_coef(L.sums, Hp, H, gamma, invstd, L.coef, 1, s));
+  if (!accumulate) TRYP(DCNR_K_PACK, fill_zero(dbias_pre, (size_t)H * 4, s));   // exactly 0 (see finalize)
   return DCNR_OK;
 }
 
@@ -618,10 +621,9 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
                        Hp, L.du, L.part, &nc, s));
     // dbeta2, dgamma2 and (last block only) dW_f[:H]
     TRY(bn_bwd_reduce(desc, d, L, nc, 3, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, Gin ? nullptr : Gr.wf,
-                      accumulate, s));
+                      Gk.b2, accumulate, s));
     TRYP(DCNR_K_ROWWISE, bwd_bn2_apply2(d.prec, L.du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
                        L.dt2, L.part, &nc, s));
-    TRY(bias_reduce(d, L, nc, Gk.b2, accumulate, s));  // dbias2
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
     TRY(linear_dw(d, L, L.dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s));
     {
@@ -634,11 +636,10 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     // ---- relu/dropout + BN1 backward
     TRYP(DCNR_K_ROWWISE, bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean, bn1.invstd, B, Hp, Hp,
                       p, dropout_seed, j, L.part, &nc, s));
-    TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, accumulate,
-                      s));
+    TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
+                      accumulate, s));
     TRYP(DCNR_K_ROWWISE, bwd_bn1_apply2(d.prec, L.da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, L.a1,
                        L.part, &nc, s));
-    TRY(bias_reduce(d, L, nc, Gk.b1, accumulate, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
     TRY(linear_dw(d, L, L.a1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s));
     {

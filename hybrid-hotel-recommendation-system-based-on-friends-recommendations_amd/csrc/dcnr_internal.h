@@ -278,6 +278,7 @@ struct RedFinal {
   BnFinal f;                                   // RED_BN_FWD (train)
   const float* gamma; const float* invstd;     // RED_BN_BWD
   float* dgamma; float* dbeta; float* dwf; float* coef;
+  float* dbias_pre;                            // Linear bias in front of the BN: grad = 0
   float* grad;                                 // RED_BIAS
 };
 dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, int N, int Nr,
@@ -302,7 +303,7 @@ dcnr_status bwd_bn2_stats3(int precision, const void* G, const float* dz, const 
                            const void* out, const void* t, const float* mean, const float* invstd,
                            int64_t B, int N, int ld, void* du, float* part, int* nchunks,
                            hipStream_t s);
-// dt = coef0*du - coef1*xhat - coef2 ; NK=1 partials of dt
+// dt = coef0*du - coef1*xhat - coef2 (part/nchunks unused)
 dcnr_status bwd_bn2_apply2(int precision, const void* du, const void* t, const float* mean,
                            const float* invstd, const float* coef, int64_t B, int N, int ld,
                            void* dt, float* part, int* nchunks, hipStream_t s);

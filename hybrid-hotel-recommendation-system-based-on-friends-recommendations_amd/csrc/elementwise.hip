@@ -266,7 +266,7 @@ template <typename T, bool HAS_G> struct Bwd2StatsOp {
     stv<T>(du_out + r * ld + c, q.g);
   }
 };
-// dt2 = k0*du - k1*xhat - k2 (BN2 backward), column sums of dt2 (= dbias2)
+// dt2 = k0*du - k1*xhat - k2 (BN2 backward)
 template <typename T> struct Bwd2ApplyOp {
   const T* du; const T* t; const float* mean; const float* invstd; const float* coef; int ld, N;
   T* dt;
@@ -284,9 +284,7 @@ template <typename T> struct Bwd2ApplyOp {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
       float xh = (q.t[v] - k.mu[v]) * k.is[v];
-      float y = k.k0[v] * q.u[v] - k.k1[v] * xh - k.k2[v];
-      q.u[v] = y;
-      acc[0][v] += y;
+      q.u[v] = k.k0[v] * q.u[v] - k.k1[v] * xh - k.k2[v];
     }
     stv<T>(dt + r * ld + c, q.u);
   }
@@ -337,9 +335,7 @@ template <typename T> struct Bwd1ApplyOp {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
       float xh = (q.t[v] - k.mu[v]) * k.is[v];
-      float y = k.k0[v] * q.a[v] - k.k1[v] * xh - k.k2[v];
-      q.a[v] = y;
-      acc[0][v] += y;
+      q.a[v] = k.k0[v] * q.a[v] - k.k1[v] * xh - k.k2[v];
     }
     stv<T>(dt + r * ld + c, q.a);
   }
@@ -551,6 +547,9 @@ __global__ __launch_bounds__(NT) void reduce_fused_kernel(const float* part, int
       rf.dgamma[n] = rf.accumulate ? rf.dgamma[n] + (float)v1 : (float)v1;
       rf.dbeta[n] = rf.accumulate ? rf.dbeta[n] + (float)v0 : (float)v0;
       if (rf.dwf) rf.dwf[n] = rf.accumulate ? rf.dwf[n] + (float)v2 : (float)v2;
+      // the Linear bias in front of a train-mode BatchNorm has an exactly zero
+      // gradient (sum_b dt = gamma*invstd*(sum du - sum du - sum(xhat)*..) = 0)
+      if (rf.dbias_pre && !rf.accumulate) rf.dbias_pre[n] = 0.f;
     }
   } else {  // RED_BIAS
     if (real) rf.grad[n] = rf.accumulate ? rf.grad[n] + (float)v0 : (float)v0;
@@ -711,7 +710,7 @@ static dcnr_status bwd2_apply_impl(const void* du, const void* t, const float* m
                                    const float* invstd, const float* coef, int64_t B, int N,
                                    int ld, void* dt, float* part, int* nc, hipStream_t s) {
   Bwd2ApplyOp<T> op{(const T*)du, (const T*)t, mean, invstd, coef, ld, N, (T*)dt};
-  return run_rowcol<T, 1>(op, B, N, part, nc, s);
+  return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
 }
 dcnr_status bwd_bn2_apply2(int precision, const void* du, const void* t, const float* mean,
                            const float* invstd, const float* coef, int64_t B, int N, int ld,
@@ -746,7 +745,7 @@ static dcnr_status bwd1_apply_impl(const void* dr, const void* t, const float* m
                                    const float* invstd, const float* coef, int64_t B, int N,
                                    int ld, void* dt, float* part, int* nc, hipStream_t s) {
   Bwd1ApplyOp<T> op{(const T*)dr, (const T*)t, mean, invstd, coef, ld, N, (T*)dt};
-  return run_rowcol<T, 1>(op, B, N, part, nc, s);
+  return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
 }
 dcnr_status bwd_bn1_apply2(int precision, const void* dr, const void* t, const float* mean,
                            const float* invstd, const float* coef, int64_t B, int N, int ld,
