@@ -396,9 +396,33 @@ dcnr_status linear_fwd(const Dims& d, const void* A, int lda, const void* W, int
 }
 
 // dW[N][Kc] = sum_b dY[b][n] X[b][k]   (real extents Nr x Kr written to out)
+// bf16: the 256x256 LDS-DMA weight-gradient kernel (gemm_dw.hip), S batch
+// splits, fp32 slabs summed by splitk_reduce
+dcnr_status wgrad_bf16(const void* dY, int64_t ldy, int N, const void* X, int64_t ldx, int Kc,
+                       int64_t B, float* slab, int64_t slab_elems, float* out, int Nr, int Kr,
+                       int accumulate, hipStream_t s) {
+  const int S = gemm_dw_splits(N, Kc, B);
+  if ((int64_t)S * N * Kc > slab_elems) {
+    set_error("wgrad: slab too small");
+    return DCNR_WORKSPACE_TOO_SMALL;
+  }
+  DwArgs a;
+  memset(&a, 0, sizeof(a));
+  a.A = (const bf16*)dY; a.lda = ldy; a.B = (const bf16*)X; a.ldb = ldx;
+  a.C = slab; a.ldc = Kc; a.slab_stride = (int64_t)N * Kc;
+  a.Btot = B; a.k_per_split = rup(cdiv(B, S), 64);
+  a.N = N; a.K = Kc; a.splits = S;
+  TRYP(DCNR_K_GEMM_DW, gemm_dw(a, s));
+  TRYP(DCNR_K_REDUCE, splitk_reduce(slab, S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s));
+  return DCNR_OK;
+}
+
 dcnr_status linear_dw(const Dims& d, const Layout& L, const void* dY, int ldy, int N,
                       const void* X, int ldx, int Kc, int64_t B, float* out, int Nr, int Kr,
                       int accumulate, hipStream_t s) {
+  if (d.prec == DCNR_PREC_BF16 && gemm_dw_supported(N, Kc, ldy, ldx, B) &&
+      getenv("DCNR_DISABLE_GEMM_DW") == nullptr)
+    return wgrad_bf16(dY, ldy, N, X, ldx, Kc, B, L.slab, L.slab_elems, out, Nr, Kr, accumulate, s);
   int64_t tiles = cdiv(N, 128) * cdiv(Kc, 128);
   int64_t S = std::max<int64_t>(1, std::min<int64_t>(512 / tiles, cdiv(B, 256)));
   int64_t kps = rup(cdiv(B, S), 64);
@@ -756,6 +780,25 @@ dcnr_status dcnr_linear_bf16(const void* X, int64_t ldx, int64_t M, int32_t K, c
   g.M = M; g.N = N; g.K = K; g.k_per_split = K; g.out_f32 = out_f32 ? 1 : 0;
   TRYP(DCNR_K_GEMM_FWD, gemm_nn(DCNR_PREC_BF16, EPI_STORE, g, 1, s));
   return DCNR_OK;
+}
+
+size_t dcnr_linear_wgrad_workspace_size(int32_t N, int32_t K, int64_t B) {
+  return (size_t)gemm_dw_splits(N, K, B) * (size_t)N * (size_t)K * sizeof(float);
+}
+
+dcnr_status dcnr_linear_wgrad_bf16(const void* dY, int64_t ldy, const void* X, int64_t ldx,
+                                   int64_t B, int32_t N, int32_t K, float* dW, int accumulate,
+                                   void* ws, size_t ws_bytes, dcnr_stream_t stream) {
+  if (!dY || !X || !dW || !ws || B < 1 || N < 1 || K < 1 || !gemm_dw_supported(N, K, ldy, ldx, B)) {
+    set_error("dcnr_linear_wgrad_bf16: bad or unsupported arguments");
+    return DCNR_BAD_ARG;
+  }
+  if (ws_bytes < dcnr_linear_wgrad_workspace_size(N, K, B)) {
+    set_error("workspace too small");
+    return DCNR_WORKSPACE_TOO_SMALL;
+  }
+  return wgrad_bf16(dY, ldy, N, X, ldx, K, B, (float*)ws, (int64_t)(ws_bytes / 4), dW, N, K,
+                    accumulate, (hipStream_t)stream);
 }
 
 void dcnr_profile_enable(int on) {

@@ -116,6 +116,16 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   t = __uint_as_float(r[0]) + __uint_as_float(r[1]);
   return row16_sum(t);
 }
+// two independent 64-lane sums at once (wave-uniform results)
+__device__ __forceinline__ void wave_sum2(float a, float b, float& sa, float& sb) {
+  auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+  const float t = __uint_as_float(p[0]) + __uint_as_float(p[1]);     // lanes 0-31: a, 32-63: b
+  const unsigned ut = __float_as_uint(t);
+  auto r = __builtin_amdgcn_permlane16_swap(ut, ut, false, false);
+  const float u = row16_sum(__uint_as_float(r[0]) + __uint_as_float(r[1]));  // rows: a, a, b, b
+  sa = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), 0));
+  sb = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(u), 32));
+}
 // four independent 64-lane sums at once (wave-uniform results)
 __device__ __forceinline__ void wave_sum4(float a, float b, float c, float d, float& sa, float& sb,
                                           float& sc, float& sd) {
@@ -192,6 +202,20 @@ struct NtArgs {
 };
 bool gemm_nt_supported(int64_t K, int64_t N);
 dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s);
+
+// bf16 weight-gradient GEMM (gemm_dw.hip): slab[split][n][k] = sum over the
+// split's batch rows of A[b][n] * B[b][k]; A = dY [Btot][lda], B = X [Btot][ldb]
+struct DwArgs {
+  const bf16* A; int64_t lda;
+  const bf16* B; int64_t ldb;
+  float* C; int64_t ldc; int64_t slab_stride;
+  int64_t Btot, k_per_split;
+  int N, K, splits;
+  int tiles_n, tiles_k;            // filled by gemm_dw
+};
+bool gemm_dw_supported(int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t Btot);
+int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot);
+dcnr_status gemm_dw(const DwArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ elementwise
 struct PackDesc {            // W [rows][cols] f32 -> dst T [rows_p][ld] (+ optional transpose)

@@ -1,0 +1,222 @@
+// Weight-gradient GEMM of the bf16 deep tower (gfx950):
+//
+//   dW[n][k] = sum_b dY[b][n] * X[b][k]      (train.py:225, backward of nn.Linear)
+//
+// Both operands are batch-major ([B][ld] row-major, the layout the forward
+// and the dX GEMM produce), so the contraction runs over their slow index.
+// Design (cdna_hip_programming.md, 256^2 tile at ~1 block/CU):
+//  * 256(n) x 256(k) output tile per block, 8 waves as 2(n) x 4(k), each wave
+//    128 x 64 (8 x 4 MFMA 16x16x32 tiles, 128 fp32 accumulators per lane);
+//  * the batch is split S ways (S % 8 == 0); every block of one split runs on
+//    one XCD so the split's rows of dY and X come from HBM once;
+//  * LDS-DMA staging (buffer_load ... lds, 16 B per lane, no VGPRs), BK = 32
+//    batch rows per stage, a ring of 4 stages (32 KiB each) with 3 in flight
+//    (counted vmcnt, raw s_barrier: the DMAs stay in flight across it), so
+//    ~3 stages of MFMA work cover the HBM latency;
+//  * the LDS image is batch-major, rows of 512 B; fragments are read with
+//    ds_read_b64_tr_b16 (transposing 4 x 16 blocks).  The 32-B chunks of a
+//    row are XOR-swizzled by (row & 7), applied on the per-lane SOURCE
+//    address (the DMA destination is lane-linear), so a transposed read's 4
+//    rows hit different banks (a 16-row read touches each bank twice: the floor);
+//  * out-of-range rows/columns are fetched at an out-of-range buffer offset
+//    and read as 0 (branch-free tails);
+//  * fp32 split partials go to a slab [S][N][ldc] (summed by splitk_reduce).
+#include "dcnr_internal.h"
+
+// tools/dw_lab.hip rebuilds this file with DW_LAB_MODE bits (1: no MFMA,
+// 2: no stage loads, 4: no epilogue stores); the library builds mode 0.
+#ifndef DW_LAB_MODE
+#define DW_LAB_MODE 0
+#endif
+
+namespace dcnr {
+namespace {
+
+constexpr int TNW = 256, TKW = 256, BKW = 32, NTW = 512, NSTAGE = 4;
+constexpr int ROWB = TNW * 2;                 // bytes per LDS row (256 bf16)
+constexpr int OPB = BKW * ROWB;               // bytes per operand per stage (16 KiB)
+constexpr int STAGEB = 2 * OPB;               // A + B per stage (32 KiB)
+constexpr int LDS_DW = NSTAGE * STAGEB;       // ring of 4 stages (128 KiB)
+
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// physical byte offset of logical (row, byte x) inside one operand image
+__device__ __forceinline__ int swz(int row, int x) {
+  return row * ROWB + ((((x >> 5) ^ (row & 7)) << 5) | (x & 31));
+}
+
+// LDS-DMA of 16 B per lane into lds_dst + 16 * lane (lds_dst wave-uniform),
+// from byte offset `off` of the buffer (an out-of-range offset writes 0).
+// Inline asm on purpose: hipcc tracks builtin LDS-DMAs as pending LDS writes
+// and drains them (vmcnt(0)) before every ds_read, which would serialise the
+// stage ring; here the counted vmcnt waits below are the only synchronisation.
+// M0 is saved and restored inside the statement (it is compiler-reserved).
+__device__ __forceinline__ void dma16(u32x4 rsrc, int off, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(off), "s"(rsrc), "s"(lds_dst)
+      : "memory");
+}
+
+__device__ __forceinline__ u32x4 rsrc_words(const void* p, int64_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  return u32x4{(uint32_t)a, (uint32_t)(a >> 32) & 0xFFFFu, p ? (uint32_t)bytes : 0u, 0x00020000u};
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
+// One stage: rows kb..kb+31 of A (cols n0..n0+255) and B (cols c0..c0+255).
+// Each wave-instruction fills 1 KiB = 2 rows; 16 instructions per operand,
+// 2 per wave per operand (4 DMAs per wave per stage).
+__device__ __forceinline__ void stage_load(u32x4 ar, u32x4 br, int64_t lda, int64_t ldb,
+                                           int64_t kb, int64_t kend, int n0, int N, int c0, int K,
+                                           char* lds_stage, int wave, int lane) {
+  const int rsub = lane >> 5, p = lane & 31;   // row in the pair, 16-B position in the row
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (wave * 2 + i) * 2 + rsub;   // 0..31
+    const int chunk = ((p >> 1) ^ (row & 7)) * 2 + (p & 1);   // logical 16-B chunk here
+    const int64_t b = kb + row;
+    const int na = n0 + chunk * 8, ka = c0 + chunk * 8;
+    const bool okr = b < kend;
+    const int offa = (okr && na < N) ? (int)((b * lda + na) * 2) : OOR;
+    const int offb = (okr && ka < K) ? (int)((b * ldb + ka) * 2) : OOR;
+    const uint32_t dsta = lds_addr(lds_stage) + (wave * 2 + i) * 1024;
+    if constexpr (!(DW_LAB_MODE & 2)) {
+      dma16(ar, offa, dsta);
+      dma16(br, offb, dsta + OPB);
+    }
+  }
+}
+
+// A-operand fragment (16 columns starting at cb, batch rows kk..kk+31):
+// lane l gets X[kk + 8*(l>>4) + j][cb + (l&15)], j = 0..7, from the
+// batch-major image via two transposed 4x16 block reads.
+__device__ __forceinline__ bf16x8 frag_t(const char* img, int cb, int kk, int lane) {
+  const int rk = kk + 8 * (lane >> 4) + ((lane & 15) >> 2);
+  const int x = (cb + 4 * (lane & 3)) * 2;
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + swz(rk, x)));
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + swz(rk + 4, x)));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+__global__ __launch_bounds__(NTW, 1) void gemm_dw_kernel(DwArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tiles = g.tiles_n * g.tiles_k;
+  const int bid = blockIdx.x;
+  const int split = (bid % 8) + 8 * (bid / (8 * tiles));
+  const int t = (bid / 8) % tiles;
+  const int n0 = (t / g.tiles_k) * TNW, c0 = (t % g.tiles_k) * TKW;
+  const int64_t kbeg = (int64_t)split * g.k_per_split;
+  const int64_t kend = min(g.Btot, kbeg + g.k_per_split);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wn = wave >> 2, wk = wave & 3;    // wave tile: n wn*128.., k wk*64..
+
+  const u32x4 ar = rsrc_words(g.A, g.Btot * g.lda * 2);
+  const u32x4 br = rsrc_words(g.B, g.Btot * g.ldb * 2);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nst = kend > kbeg ? (int)((kend - kbeg + BKW - 1) / BKW) : 0;
+#pragma unroll
+  for (int p = 0; p < NSTAGE - 1; ++p)
+    if (p < nst)
+      stage_load(ar, br, g.lda, g.ldb, kbeg + (int64_t)p * BKW, kend, n0, g.N, c0, g.K,
+                 lds + p * STAGEB, wave, lane);
+  for (int st = 0; st < nst; ++st) {
+    // this wave's DMAs of stage st are done (the younger stages stay in
+    // flight), then the barrier makes every wave's part visible and retires
+    // stage st-1's reads, so its buffer can be refilled with stage st+3
+    if (st + 2 < nst) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + NSTAGE - 1 < nst)
+      stage_load(ar, br, g.lda, g.ldb, kbeg + (int64_t)(st + NSTAGE - 1) * BKW, kend, n0, g.N, c0,
+                 g.K, lds + ((st + NSTAGE - 1) % NSTAGE) * STAGEB, wave, lane);
+    const char* ai = lds + (st % NSTAGE) * STAGEB;
+    const char* bi = ai + OPB;
+    bf16x8 af[8], bf[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = frag_t(ai, wn * 128 + i * 16, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bf[j] = frag_t(bi, wk * 64 + j * 16, 0, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if constexpr (!(DW_LAB_MODE & 1))
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        else
+          acc[i][j][0] += (float)af[i][0] * (float)bf[j][1];
+  }
+
+  // epilogue: acc[i][j][r] = dW[n0 + wn*128 + i*16 + (lane>>4)*4 + r][c0 + wk*64 + j*16 + (lane&15)]
+  float* out = g.C + (int64_t)split * g.slab_stride;
+  const __amdgpu_buffer_rsrc_t cr = buf_rsrc(out, (int64_t)g.N * g.ldc * 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = c0 + wk * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4 + r;
+        const bool ok = n < g.N && k < g.K;
+        if (!(DW_LAB_MODE & 4) || acc[i][j][r] == 1234.5f)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), cr,
+                                                ok ? (n * g.ldc + k) * 4 : OOR, 0, 0);
+      }
+    }
+}
+
+}  // namespace
+
+bool gemm_dw_supported(int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t Btot) {
+  return N % 8 == 0 && K % 8 == 0 && lda % 8 == 0 && ldb % 8 == 0 &&
+         Btot * lda * 2 < (int64_t(1) << 31) && Btot * ldb * 2 < (int64_t(1) << 31);
+}
+
+int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot) {
+  const int64_t tiles = cdiv(N, TNW) * cdiv(K, TKW);
+  int64_t s = std::max<int64_t>(8, (256 / tiles) / 8 * 8);
+  while (s > 8 && cdiv(Btot, s) < 2 * BKW) s -= 8;   // at least two stages per split
+  return (int)s;
+}
+
+dcnr_status gemm_dw(const DwArgs& a0, hipStream_t s) {
+  DwArgs a = a0;
+  if (!gemm_dw_supported(a.N, a.K, a.lda, a.ldb, a.Btot) || a.splits % 8 || a.splits < 8) {
+    set_error("gemm_dw: unsupported N=%d K=%d splits=%d", a.N, a.K, a.splits);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  static bool attr_set = false;
+  if (!attr_set) {
+    DCNR_HIP(hipFuncSetAttribute((const void*)gemm_dw_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DW));
+    attr_set = true;
+  }
+  a.tiles_n = (int)cdiv(a.N, TNW);
+  a.tiles_k = (int)cdiv(a.K, TKW);
+  const int grid = a.tiles_n * a.tiles_k * a.splits;
+  hipLaunchKernelGGL(gemm_dw_kernel, dim3(grid), dim3(NTW), LDS_DW, s, a);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+}  // namespace dcnr

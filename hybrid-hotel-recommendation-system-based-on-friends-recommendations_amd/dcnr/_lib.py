@@ -71,6 +71,10 @@ _SIGS = {
     "dcnr_check_errors": (ctypes.c_int, [_P, ctypes.c_size_t, _P]),
     "dcnr_linear_bf16": (ctypes.c_int, [_P, _I64, _I64, ctypes.c_int32, _P, _I64, ctypes.c_int32,
                                         _P, _P, _I64, ctypes.c_int, _P]),
+    "dcnr_linear_wgrad_workspace_size": (ctypes.c_size_t, [ctypes.c_int32, ctypes.c_int32, _I64]),
+    "dcnr_linear_wgrad_bf16": (ctypes.c_int, [_P, _I64, _P, _I64, _I64, ctypes.c_int32,
+                                              ctypes.c_int32, _P, ctypes.c_int, _P,
+                                              ctypes.c_size_t, _P]),
     "dcnr_profile_enable": (None, [ctypes.c_int]),
     "dcnr_profile_collect": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
 }

@@ -170,6 +170,16 @@ dcnr_status dcnr_linear_bf16(const void* X, int64_t ldx, int64_t M, int32_t K, c
                              int64_t ldw, int32_t N, const float* bias, void* C, int64_t ldc,
                              int out_f32, dcnr_stream_t stream);
 
+/* The deep tower's weight gradient as a standalone bf16 call (backward of
+ * nn.Linear, train.py:225): dW[N][K] (fp32) (+)= sum_b dY[b][n] * X[b][k],
+ * dY [B][ldy] and X [B][ldx] bf16 row-major (N, K, ldy, ldx multiples of 8).
+ * Workspace: dcnr_linear_wgrad_workspace_size bytes.  Used by the deep tower
+ * internally; exported for unit tests and kernel benchmarks. */
+size_t dcnr_linear_wgrad_workspace_size(int32_t N, int32_t K, int64_t B);
+dcnr_status dcnr_linear_wgrad_bf16(const void* dY, int64_t ldy, const void* X, int64_t ldx,
+                                   int64_t B, int32_t N, int32_t K, float* dW, int accumulate,
+                                   void* ws, size_t ws_bytes, dcnr_stream_t stream);
+
 /* Kernel-timing instrumentation (measurement only, off by default): when
  * enabled, every launch the library makes is bracketed by HIP events on its
  * stream and attributed to one of these classes. */

@@ -430,3 +430,24 @@ def test_linear_bf16_vs_torch(dev, M, K, N, out_f32):
     err = (C.float() - ref).abs().max().item()
     tol = 1e-3 if out_f32 else 1.6e-2 * ref.abs().max().item()
     assert err <= tol, err
+
+
+@pytest.mark.parametrize("B,N,K,acc", [(131072, 512, 512, 0), (131072, 512, 456, 1),
+                                       (37, 96, 64, 0), (5000, 264, 160, 0)])
+def test_linear_wgrad_bf16_vs_torch(dev, B, N, K, acc):
+    """dcnr_linear_wgrad_bf16 (256x256 LDS-DMA weight-gradient GEMM + split
+    reduction) vs a torch fp32 reference of the same bf16 operands."""
+    from dcnr import _lib
+    g = torch.Generator(device=dev).manual_seed(B + N + K)
+    dY = torch.randn(B, N, device=dev, generator=g).to(torch.bfloat16)
+    X = torch.randn(B, K, device=dev, generator=g).to(torch.bfloat16)
+    dW = torch.randn(N, K, device=dev, generator=g) if acc else torch.empty(N, K, device=dev)
+    base = dW.clone()
+    lib = _lib.load()
+    ws = torch.empty(lib.dcnr_linear_wgrad_workspace_size(N, K, B), dtype=torch.uint8, device=dev)
+    _lib.check(lib.dcnr_linear_wgrad_bf16(dY.data_ptr(), N, X.data_ptr(), K, B, N, K, dW.data_ptr(),
+                                          acc, ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)),
+               "wgrad")
+    ref = dY.float().t() @ X.float() + (base if acc else 0)
+    err = ((dW - ref).norm() / ref.norm()).item()
+    assert err <= 1e-5, err

@@ -40,3 +40,35 @@ if __name__ == "__main__":
     for K in (512, 456):
         run(K=K)
     run(M=131072, K=512, N=128)
+
+
+def run_dw(M=131072, N=512, K=512, iters=20):
+    """dW = dY^T X over the batch (the backward weight GEMM) with torch/hipBLASLt."""
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(0)
+    dY = torch.randn(M, N, device=dev, generator=g).to(torch.bfloat16)
+    X = torch.randn(M, K, device=dev, generator=g).to(torch.bfloat16)
+    for _ in range(3): torch.mm(dY.t(), X)
+    e0, e1 = torch.cuda.Event(True), torch.cuda.Event(True)
+    e0.record()
+    for _ in range(iters): torch.mm(dY.t(), X)
+    e1.record(); torch.cuda.synchronize()
+    t = e0.elapsed_time(e1) / iters
+    lib = _lib.load()
+    dW = torch.empty(N, K, device=dev)
+    ws = torch.empty(lib.dcnr_linear_wgrad_workspace_size(N, K, M), dtype=torch.uint8, device=dev)
+    call = lambda: _lib.check(lib.dcnr_linear_wgrad_bf16(dY.data_ptr(), N, X.data_ptr(), K, M, N, K,
+                                                         dW.data_ptr(), 0, ws.data_ptr(), ws.numel(),
+                                                         _lib.stream_ptr(dev)), "wgrad")
+    for _ in range(3): call()
+    e0.record()
+    for _ in range(iters): call()
+    e1.record(); torch.cuda.synchronize()
+    t2 = e0.elapsed_time(e1) / iters
+    print(f"dW {N}x{K} over {M}: ours {t2*1e3:.1f} us ({2*M*N*K/t2/1e9:.0f} TF/s); torch/hipBLASLt "
+          f"{t*1e3:.1f} us ({2*M*N*K/t/1e9:.0f} TF/s), HBM floor {(M*N*2+M*K*2)/6.3e12*1e6:.1f} us")
+
+
+if __name__ == "__main__":
+    run_dw()
+    run_dw(K=456)

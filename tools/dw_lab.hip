@@ -1,0 +1,44 @@
+// Kernel lab for gemm_dw_kernel: rebuilds csrc/gemm_dw.hip with DW_LAB_MODE
+// (1: no MFMA, 2: no stage loads, 4: no epilogue stores) and times it alone.
+#include "../hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd/csrc/gemm_dw.hip"
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+namespace dcnr {
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfprintf(stderr, fmt, ap);
+  va_end(ap);
+  fprintf(stderr, "\n");
+}
+}  // namespace dcnr
+
+int main() {
+  const int64_t B = 131072;
+  const int N = 512, K = 512;
+  dcnr::bf16 *A, *X;
+  float* slab;
+  const int S = dcnr::gemm_dw_splits(N, K, B);
+  (void)hipMalloc(&A, B * N * 2); (void)hipMalloc(&X, B * K * 2);
+  (void)hipMalloc(&slab, (size_t)S * N * K * 4);
+  (void)hipMemset(A, 0x3c, B * N * 2); (void)hipMemset(X, 0x3c, B * K * 2);
+  dcnr::DwArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.A = A; a.lda = N; a.B = X; a.ldb = K; a.C = slab; a.ldc = K; a.slab_stride = (int64_t)N * K;
+  a.Btot = B; a.k_per_split = (B + S - 1) / S; a.N = N; a.K = K; a.splits = S;
+  for (int i = 0; i < 3; ++i) dcnr::gemm_dw(a, 0);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, 0);
+  for (int i = 0; i < 20; ++i) dcnr::gemm_dw(a, 0);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  printf("dw mode %d  S=%d  %.1f us  %.0f TF/s  %s\n", DW_LAB_MODE, S, ms * 1e3 / 20,
+         2.0 * B * N * K / (ms * 1e3 / 20) / 1e6, hipGetErrorString(hipGetLastError()));
+  return 0;
+}
