@@ -395,6 +395,44 @@ dcnr_status linear_fwd(const Dims& d, const void* A, int lda, const void* W, int
   return gemm_nn(d.prec, EPI_STORE, g, 1, s);
 }
 
+// Stats epilogues of the streaming GEMM (BN column partials produced by the
+// GEMM that writes the BN input / the BN output gradient) -- bf16 only.
+bool epi_stats_ok(const Dims& d) {
+  static const bool off = getenv("DCNR_DISABLE_EPI_STATS") != nullptr ||
+                          getenv("DCNR_DISABLE_GEMM_NT") != nullptr;
+  return d.prec == DCNR_PREC_BF16 && !off && gemm_nt_supported(d.Hp, d.Hp);
+}
+
+// t = A W^T + b  and  part = BN column partials of t, shifted by b
+dcnr_status linear_fwd_stats(const Dims& d, const Layout& L, const void* A, int lda,
+                             const void* W, int K, const float* bias, void* out, int64_t B,
+                             int* nc, hipStream_t s) {
+  NtArgs a;
+  memset(&a, 0, sizeof(a));
+  a.X = (const bf16*)A; a.ldx = lda; a.M = B; a.K = K;
+  a.W = (const bf16*)W; a.ldw = K; a.N = d.Hp;
+  a.C = out; a.ldc = d.Hp; a.bias = bias;
+  a.part = L.part;
+  return gemm_nt(NT_EPI_BIAS_STATS, a, s, nc);
+}
+
+// C = mask(H) * (X W^T [+ R]) and part = [sum C, sum C*xhat(T)] (BN backward)
+dcnr_status linear_dx_bn(const Dims& d, const Layout& L, int epi, const void* X, const void* Wt,
+                         const void* R, void* C, const void* H, float hscale, const void* T,
+                         const BnBufs& bn, int64_t B, int* nc, hipStream_t s) {
+  NtArgs a;
+  memset(&a, 0, sizeof(a));
+  a.X = (const bf16*)X; a.ldx = d.Hp; a.M = B; a.K = d.Hp;
+  a.W = (const bf16*)Wt; a.ldw = d.Hp; a.N = d.Hp;
+  a.C = C; a.ldc = d.Hp;
+  a.R = R; a.ldr = d.Hp;
+  a.H = (const bf16*)H; a.ldh = d.Hp; a.hscale = hscale;
+  a.T = (const bf16*)T; a.ldt = d.Hp;
+  a.mean = bn.mean; a.invstd = bn.invstd;
+  a.part = L.part;
+  return gemm_nt(epi, a, s, nc);
+}
+
 // dW[N][Kc] = sum_b dY[b][n] X[b][k]   (real extents Nr x Kr written to out)
 // bf16: the 256x256 LDS-DMA weight-gradient kernel (gemm_dw.hip), S batch
 // splits, fp32 slabs summed by splitk_reduce
@@ -460,22 +498,28 @@ RedFinal red_init(const Layout& L, int mode, double count, int accumulate) {
   return rf;
 }
 
+// nc_pre > 0: the partials of t are already in L.part (from the GEMM epilogue),
+// shifted by shiftf (the Linear bias); otherwise a stats pass over t makes them.
 dcnr_status bn_layer_fwd(const dcnr_model_desc* desc, const Dims& d, const Layout& L,
                          const void* t, int64_t B, bool train, const float* gamma,
                          const float* beta, float* rm, float* rv, int64_t* nbt,
-                         const BnBufs& bb, hipStream_t s) {
+                         const BnBufs& bb, hipStream_t s, int nc_pre = 0,
+                         const float* shiftf = nullptr) {
   BnFinal f{gamma, beta, rm, rv, nbt, bb.scale, bb.shift, bb.mean, bb.invstd};
   if (train) {
-    int nc = 0;
-    TRYP(DCNR_K_ROWWISE, col_stats(d.prec, t, B, d.Hp, d.Hp, L.part, &nc, s));
+    int nc = nc_pre;
+    const void* shift = nc_pre ? nullptr : t;
+    if (!nc_pre) TRYP(DCNR_K_ROWWISE, col_stats(d.prec, t, B, d.Hp, d.Hp, L.part, &nc, s));
     if (!desc->bn_allreduce) {  // local BN: reduce + finalize in one launch
       RedFinal rf = red_init(L, RED_BN_FWD, (double)B, 0);
       rf.f = f;
-      TRYP(DCNR_K_REDUCE, reduce_fused(d.prec, L.part, nc, 2, d.Hp, d.H, t, rf, s));
+      rf.shiftf = shiftf;
+      TRYP(DCNR_K_REDUCE, reduce_fused(d.prec, L.part, nc, 2, d.Hp, d.H, shift, rf, s));
       return DCNR_OK;
     }
     RedFinal rf = red_init(L, RED_SUMS, (double)B, 0);
-    TRYP(DCNR_K_REDUCE, reduce_fused(d.prec, L.part, nc, 2, d.Hp, d.H, t, rf, s));
+    rf.shiftf = shiftf;
+    TRYP(DCNR_K_REDUCE, reduce_fused(d.prec, L.part, nc, 2, d.Hp, d.H, shift, rf, s));
     TRY(hook(desc, d, L, s));
   }
   TRYP(DCNR_K_REDUCE, bn_finalize2(L.sums, d.Hp, d.H, train ? 1 : 0, f, s));
@@ -578,15 +622,25 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   const float p = train ? d.dropout : 0.f;
   for (int j = 0; j < d.R; ++j) {
     const auto& Bk = P.blk[j];
-    TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
+    const bool fuse = train && epi_stats_ok(d);   // BN partials from the GEMM epilogue
+    int nc = 0;
+    if (fuse)
+      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j],
+                                             B, &nc, s));
+    else
+      TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
     TRY(bn_layer_fwd(desc, d, L, L.t1[j], B, train, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
-                     L.bn[2 * j], s));
+                     L.bn[2 * j], s, nc, fuse ? L.b1p[j] : nullptr));
     void* a1 = train ? L.a1s[j] : L.a1;
     TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
                      dropout_seed, j, s));
-    TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
+    if (fuse)
+      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B,
+                                             &nc, s));
+    else
+      TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
     TRY(bn_layer_fwd(desc, d, L, L.t2[j], B, train, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
-                     L.bn[2 * j + 1], s));
+                     L.bn[2 * j + 1], s, nc, fuse ? L.b2p[j] : nullptr));
     const bool head = j == d.R - 1 && bn_add_relu_head_supported(d.prec, d.Hp);
     if (head)   // last block: residual + ReLU + deep head dot + logits in one pass
       TRYP(DCNR_K_ROWWISE, bn_add_relu_head(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
@@ -634,6 +688,8 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   }
 
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
+  const bool fuse = epi_stats_ok(d);   // BN partials from the dX GEMM epilogues
+  int nc_du = 0;   // > 0: L.du and its BN2 partials were made by the previous dX GEMM
   for (int j = d.R - 1; j >= 0; --j) {
     const auto& Bk = P.blk[j];
     auto& Gk = Gr.blk[j];
@@ -641,40 +697,58 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     const BnBufs& bn2 = L.bn[2 * j + 1];
     int nc = 0;
     // ---- out = relu(BN2(t2) + h_j):  du, BN2 backward
-    TRYP(DCNR_K_ROWWISE, bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean, bn2.invstd, B, Hp,
-                       Hp, L.du, L.part, &nc, s));
-    // dbeta2, dgamma2 and (last block only) dW_f[:H]
-    TRY(bn_bwd_reduce(desc, d, L, nc, 3, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, Gin ? nullptr : Gr.wf,
-                      Gk.b2, accumulate, s));
+    if (nc_du) {
+      TRY(bn_bwd_reduce(desc, d, L, nc_du, 2, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, nullptr,
+                        Gk.b2, accumulate, s));
+    } else {
+      TRYP(DCNR_K_ROWWISE, bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean,
+                                          bn2.invstd, B, Hp, Hp, L.du, L.part, &nc, s));
+      // dbeta2, dgamma2 and (last block only) dW_f[:H]
+      TRY(bn_bwd_reduce(desc, d, L, nc, 3, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2,
+                        Gin ? nullptr : Gr.wf, Gk.b2, accumulate, s));
+    }
     TRYP(DCNR_K_ROWWISE, bwd_bn2_apply2(d.prec, L.du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
                        L.dt2, L.part, &nc, s));
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
     TRY(linear_dw(d, L, L.dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s));
-    {
+    if (fuse) {
+      // dy1 = (dt2 W2) * [a1 != 0] / (1-p): relu and dropout masks from the
+      // saved activation, BN1 partials in the same pass
+      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(d, L, NT_EPI_DROP_BN, L.dt2, L.W2t[j], nullptr, L.da,
+                                        L.a1s[j], p > 0.f ? 1.f / (1.f - p) : 1.f, L.t1[j], bn1,
+                                        B, &nc, s));
+    } else {
       GemmArgs g;
       memset(&g, 0, sizeof(g));
       g.A = L.dt2; g.lda = Hp; g.B = L.W2t[j]; g.ldb = Hp; g.C = L.da; g.ldc = Hp;
       g.M = B; g.N = Hp; g.K = Hp; g.k_per_split = Hp;
       TRYP(DCNR_K_GEMM_DX, gemm_nn(d.prec, EPI_STORE, g, 1, s));
+      // ---- relu/dropout + BN1 backward
+      TRYP(DCNR_K_ROWWISE, bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean,
+                                         bn1.invstd, B, Hp, Hp, p, dropout_seed, j, L.part, &nc, s));
     }
-    // ---- relu/dropout + BN1 backward
-    TRYP(DCNR_K_ROWWISE, bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean, bn1.invstd, B, Hp, Hp,
-                      p, dropout_seed, j, L.part, &nc, s));
     TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
                       accumulate, s));
     TRYP(DCNR_K_ROWWISE, bwd_bn1_apply2(d.prec, L.da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, L.a1,
                        L.part, &nc, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
     TRY(linear_dw(d, L, L.a1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s));
-    {
+    if (fuse && j > 0) {
+      // G is only consumed by block j-1's BN2 backward: emit its du = G * [h_j > 0]
+      // (in place over this block's du, the residual operand) and the partials
+      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(d, L, NT_EPI_RESID_BN, L.a1, L.W1t[j], L.du, L.du, L.h[j],
+                                        1.f, L.t2[j - 1], L.bn[2 * (j - 1) + 1], B, &nc_du, s));
+      Gin = L.du;
+    } else {
       GemmArgs g;
       memset(&g, 0, sizeof(g));
       g.A = L.a1; g.lda = Hp; g.B = L.W1t[j]; g.ldb = Hp; g.C = L.G; g.ldc = Hp;
       g.resid = L.du; g.ldr = Hp;
       g.M = B; g.N = Hp; g.K = Hp; g.k_per_split = Hp;
       TRYP(DCNR_K_GEMM_DX, gemm_nn(d.prec, EPI_STORE_RESID, g, 1, s));
+      Gin = L.G;
+      nc_du = 0;
     }
-    Gin = L.G;
   }
   // ---- initial layer
   int nc = 0;

@@ -191,17 +191,29 @@ enum NtEpi : int {
   NT_EPI_BIAS = 0,    // C bf16 = acc + bias[n] (bias padded to N, may be null)
   NT_EPI_F32 = 1,     // C f32  = acc
   NT_EPI_RESID = 2,   // C bf16 = acc + R[m][n] (bf16)
+  // epilogues that also emit BatchNorm column partials part[group][2][N]
+  // (f32; one row per workgroup group, reduced by reduce_fused):
+  NT_EPI_BIAS_STATS = 3,   // C = acc + bias; part = [sum(c - bias), sum((c - bias)^2)]
+  NT_EPI_RESID_BN = 4,     // C = (acc + R) * [H > 0]; part = [sum c, sum c*xhat(T)]
+  NT_EPI_DROP_BN = 5,      // C = acc * [H != 0] * hscale; part = [sum c, sum c*xhat(T)]
 };
+// (c is the stored bf16 value; xhat(T) = (T[m][n] - mean[n]) * invstd[n])
 struct NtArgs {
   const bf16* X; int64_t ldx; int64_t M; int K;
   const bf16* W; int64_t ldw; int N;
   void* C; int64_t ldc;
   const float* bias;
   const void* R; int64_t ldr;
+  const bf16* H; int64_t ldh; float hscale;         // mask source (RESID_BN, DROP_BN)
+  const bf16* T; int64_t ldt;                       // BN input for xhat
+  const float* mean; const float* invstd;
+  float* part;                                      // column partials (stats epilogues)
   int nslices, groups; int64_t mtiles;   // filled by gemm_nt
 };
 bool gemm_nt_supported(int64_t K, int64_t N);
-dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s);
+// nparts (stats epilogues): rows of part written (the nchunks of reduce_fused)
+dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
+inline bool nt_epi_stats(int epi) { return epi >= NT_EPI_BIAS_STATS; }
 
 // bf16 weight-gradient GEMM (gemm_dw.hip): slab[split][n][k] = sum over the
 // split's batch rows of A[b][n] * B[b][k]; A = dY [Btot][lda], B = X [Btot][ldb]
@@ -304,6 +316,7 @@ struct RedFinal {
   float* dgamma; float* dbeta; float* dwf; float* coef;
   float* dbias_pre;                            // Linear bias in front of the BN: grad = 0
   float* grad;                                 // RED_BIAS
+  const float* shiftf;                         // f32 shift of the stats partials (or null)
 };
 dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, int N, int Nr,
                          const void* shift, const RedFinal& rf, hipStream_t s);

@@ -509,8 +509,8 @@ __global__ __launch_bounds__(NT) void reduce_fused_kernel(const float* part, int
   double v2 = ((red[2 * 64 + tx] + red[5 * 64 + tx]) + red[8 * 64 + tx]) + red[11 * 64 + tx];
   const double cnt = rf.count;
   const bool real = n < Nr;
-  if (shift) {  // unshift
-    double K = (double)(float)shift[n];
+  if (shift || rf.shiftf) {  // unshift
+    double K = rf.shiftf ? (double)rf.shiftf[n] : (double)(float)shift[n];
     v1 = v1 + 2.0 * K * v0 + cnt * K * K;
     v0 = v0 + cnt * K;
   }

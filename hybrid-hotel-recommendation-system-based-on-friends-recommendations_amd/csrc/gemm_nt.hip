@@ -25,7 +25,8 @@
 
 // tools/gemm_lab.hip rebuilds this file with NT_LAB_MODE bits set to time
 // parts of the kernel in isolation (1: no C stores, 2: no X loads in the
-// k-loop, 4: no MFMAs).  The library always builds mode 0.
+// k-loop, 4: no MFMAs, 8: C stores into a 4096-row window, 16: X loads from a
+// 4096-row window).  The library always builds mode 0.
 #ifndef NT_LAB_MODE
 #define NT_LAB_MODE 0
 #endif
@@ -33,14 +34,35 @@
 namespace dcnr {
 namespace {
 
-// 8 waves (2 per SIMD: one wave's epilogue overlaps the other's MFMAs), 32 rows each
-constexpr int NT = 512, TM = 256, TN = 128, BK = 32, WROWS = TM / 8;
+// NT_WAVES waves of NT_RB 16-row blocks each (tools/gemm_lab.hip sweeps both)
+#ifndef NT_WAVES
+#define NT_WAVES 8
+#endif
+#ifndef NT_RB
+#define NT_RB 2
+#endif
+#ifndef NT_STORE_AUX
+#define NT_STORE_AUX 0
+#endif
+#ifndef NT_DEPTH
+#define NT_DEPTH 8
+#endif
+#ifndef NT_WAVES_STATS
+#define NT_WAVES_STATS 4
+#endif
+constexpr int RB = NT_RB, WROWS = 16 * RB, TN = 128, BK = 32;
+// stats epilogues hold more live state: one wave per SIMD (512 registers)
+template <int EPI> struct Geo {
+  static constexpr int NWAVE = EPI >= NT_EPI_BIAS_STATS ? NT_WAVES_STATS : NT_WAVES;
+  static constexpr int NT = 64 * NWAVE, TM = NWAVE * WROWS;
+};
+constexpr int TM_MIN = 64 * WROWS / 16;   // smallest TM of any epilogue (4 waves)
 
 template <int KTP> struct NtCfg {
   static constexpr int WCH = KTP * (BK / 8);                 // 16-B chunks per W row
-  static constexpr int DEPTH = KTP < 8 ? KTP : 8;            // prefetch ring depth (k-steps)
+  static constexpr int DEPTH = KTP < NT_DEPTH ? KTP : NT_DEPTH;            // prefetch ring depth (k-steps)
   static constexpr int W_LDS = TN * WCH;                     // uint4 units
-  static constexpr int BIAS_LDS = TN / 4;                    // uint4 units (128 fp32)
+  static constexpr int BIAS_LDS = 3 * TN / 4;                // uint4 units (bias, mean, invstd)
   static constexpr size_t LDS_BYTES = (size_t)(W_LDS + BIAS_LDS) * 16;
 };
 
@@ -54,19 +76,35 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
 }
 
 // X fragments of one k-step for this wave: rows r0 + i*16 + (lane&15), k = kt*32 + 8*(lane>>4)
-__device__ __forceinline__ void load_x(u32x4 (&f)[2], __amdgpu_buffer_rsrc_t xr, int64_t ldx,
+__device__ __forceinline__ void load_x(u32x4 (&f)[RB], __amdgpu_buffer_rsrc_t xr, int64_t ldx,
                                        int64_t M, int K, int64_t r0, int kt, int lane, bool valid) {
   const int k = kt * BK + 8 * (lane >> 4);
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int64_t m = r0 + i * 16 + (lane & 15);
+  for (int i = 0; i < RB; ++i) {
+    int64_t m = r0 + i * 16 + (lane & 15);
+    if constexpr (NT_LAB_MODE & 16) m &= 4095;   // lab: X reads from a 4096-row window
     const bool ok = valid && m < M && k < K;
     f[i] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? (int)((m * ldx + k) * 2) : OOR, 0, 0);
   }
 }
 
+// One reduce-scatter step over lane pairs (lane, partner(lane)) given by the
+// DPP control: x[u] (u < H) becomes the pair-sum of x[u] (hi = false) or of
+// x[u + H] (hi = true); partners have opposite `hi`.
+template <int H, int CTRL>
+__device__ __forceinline__ void bfly_step(float (&x)[64], bool hi) {
+#pragma unroll
+  for (int u = 0; u < H; ++u) {
+    const float give = hi ? x[u] : x[u + H];
+    const float keep = hi ? x[u + H] : x[u];
+    x[u] = keep + dpp<CTRL>(give);
+  }
+}
+
 template <int KTP, int EPI>
-__global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
+__global__ __launch_bounds__(Geo<EPI>::NT, 1) void gemm_nt_kernel(NtArgs a) {
+  constexpr bool STATS = EPI >= NT_EPI_BIAS_STATS;
+  constexpr int NT = Geo<EPI>::NT, TM = Geo<EPI>::TM, NWAVE = Geo<EPI>::NWAVE;
   using C = NtCfg<KTP>;
   constexpr int DEPTH = C::DEPTH;
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];
@@ -85,11 +123,18 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
   const int es = EPI == NT_EPI_F32 ? 4 : 2;
   const __amdgpu_buffer_rsrc_t cr =
       __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, (int)(a.M * a.ldc * es), 0x00020000);
+  constexpr bool HAS_R = EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN;
+  constexpr bool HAS_HT = EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN;
   const __amdgpu_buffer_rsrc_t rr_ = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.R, (short)0, EPI == NT_EPI_RESID ? (int)(a.M * a.ldr * 2) : 0, 0x00020000);
+      (void*)a.R, (short)0, HAS_R ? (int)(a.M * a.ldr * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.H, (short)0, HAS_HT ? (int)(a.M * a.ldh * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.T, (short)0, HAS_HT ? (int)(a.M * a.ldt * 2) : 0, 0x00020000);
+  float tot[4] = {0.f, 0.f, 0.f, 0.f};   // stats epilogues: this lane's share over all tiles
 
   // start the X stream before the W slice load so both are in flight
-  u32x4 ring[DEPTH][2];
+  u32x4 ring[DEPTH][RB];
 #pragma unroll
   for (int d = 0; d < DEPTH; ++d)
     load_x(ring[d], xr, a.ldx, a.M, a.K, (int64_t)group * TM + wave * WROWS, d, lane,
@@ -105,11 +150,18 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
     Ws[w_slot<C::WCH>(row, ch)] = v;
   }
 
-  // bias slice in LDS (read per tile in the epilogue; registers go to the ring)
+  // bias (and BN mean / invstd) slices in LDS, read per tile in the
+  // epilogue (registers go to the ring)
   float* bias_s = reinterpret_cast<float*>(lds + C::W_LDS);
+  float* mean_s = bias_s + TN;
+  float* istd_s = bias_s + 2 * TN;
   for (int c = tid; c < TN; c += NT) {
     const int n = n0 + c;
     bias_s[c] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+    if constexpr (HAS_HT) {
+      mean_s[c] = n < a.N ? a.mean[n] : 0.f;
+      istd_s[c] = n < a.N ? a.invstd[n] : 0.f;
+    }
   }
   __syncthreads();
 
@@ -124,10 +176,10 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
     const int64_t r0 = mt * TM + wave * WROWS;
     // residual operand of this tile, issued ahead of the k-loop's refills so
     // that waiting for it in the epilogue does not drain the prefetch ring
-    u32x2 resid[2][8];
-    if constexpr (EPI == NT_EPI_RESID) {
+    u32x2 resid[RB][8];
+    if constexpr (HAS_R) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < RB; ++i)
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           const int n = n0 + j * 16 + (lane >> 4) * 4;
@@ -137,9 +189,9 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
               rr_, ok ? (int)((m * a.ldr + n) * 2) : OOR, 0, 0);
         }
     }
-    f32x4 acc[2][8];
+    f32x4 acc[RB][8];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < RB; ++i)
 #pragma unroll
       for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -147,13 +199,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
     for (int kt = 0; kt < KTP; ++kt) {
       const int slot = kt % DEPTH;
       const int kn = (kt + 1) % KTP;   // next k-step (wraps to the next M-tile: W is tile-independent)
-      bf16x8 xf[2];
+      bf16x8 xf[RB];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) xf[i] = __builtin_bit_cast(bf16x8, ring[slot][i]);
+      for (int i = 0; i < RB; ++i) xf[i] = __builtin_bit_cast(bf16x8, ring[slot][i]);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < RB; ++i)
           if constexpr (!(NT_LAB_MODE & 4))
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[j], xf[i], acc[i][j], 0, 0, 0);
           else
@@ -167,13 +219,13 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
         load_x(ring[slot], xr, a.ldx, a.M, a.K, mtn * TM + wave * WROWS, kd % KTP, lane,
                mtn < a.mtiles);
       }
-      // pin the order: per j, 2 MFMAs then the fragment's re-read
+      // pin the order: per j, RB MFMAs then the fragment's re-read
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x008, RB, 0);  // MFMA
         __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
       }
-      __builtin_amdgcn_sched_group_barrier(0x020, 2, 0);     // VMEM read (ring refill)
+      __builtin_amdgcn_sched_group_barrier(0x020, RB, 0);    // VMEM read (ring refill)
       __builtin_amdgcn_sched_barrier(0);
     }
 
@@ -182,10 +234,30 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
     // v_permlane16_swap so every lane stores 8 consecutive columns (16 B) and
     // each store instruction writes 64 contiguous bytes per output row.
     const int q = lane >> 4;
+    float st[2][8][4];   // stats epilogues: per-lane column partials of this tile
+    if constexpr (STATS) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) st[k][j][r] = 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < RB; ++i) {
       const int64_t m = r0 + i * 16 + (lane & 15);
       const bool mok = m < a.M;
+      // mask source and BN input of this row block (one wait for all 16 loads)
+      u32x2 hv[8], tv[8];
+      if constexpr (EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int n = n0 + j * 16 + q * 4;
+          const bool ok = n < a.N && mok;
+          hv[j] = __builtin_amdgcn_raw_buffer_load_b64(hr, ok ? (int)((m * a.ldh + n) * 2) : OOR, 0, 0);
+          tv[j] = __builtin_amdgcn_raw_buffer_load_b64(tr, ok ? (int)((m * a.ldt + n) * 2) : OOR, 0, 0);
+        }
+      }
 #pragma unroll
       for (int jp = 0; jp < 4; ++jp) {
         u32x2 o[2];
@@ -196,15 +268,53 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
           const float4 bj = *reinterpret_cast<const float4*>(bias_s + j * 16 + q * 4);
           float v[4] = {acc[i][j][0] + bj.x, acc[i][j][1] + bj.y, acc[i][j][2] + bj.z,
                         acc[i][j][3] + bj.w};
-          if constexpr (EPI == NT_EPI_RESID) {
+          if constexpr (EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN) {
             const u32x2 rv = resid[i][j];
             const bf16* rb = reinterpret_cast<const bf16*>(&rv);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += (float)rb[r];
           }
+          if constexpr (EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN) {
+            const u32x2 hw = hv[j];
+            const uint16_t* hb = reinterpret_cast<const uint16_t*>(&hw);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              // RESID_BN: [h > 0] on the bf16 bits (sign clear, not +-0);
+              // DROP_BN: [h != 0] (the saved dropout activation)
+              const bool keep = EPI == NT_EPI_RESID_BN ? (hb[r] != 0 && hb[r] < 0x8000u)
+                                                       : (hb[r] & 0x7fffu) != 0;
+              v[r] = keep ? (EPI == NT_EPI_DROP_BN ? v[r] * a.hscale : v[r]) : 0.f;
+            }
+          }
           o[h] = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
           of[h] = u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
                         __float_as_uint(v[3])};
+          if constexpr (STATS) {
+            // sums of the stored (bf16-rounded) values
+            float c[4] = {__uint_as_float(o[h][0] << 16), __uint_as_float(o[h][0] & 0xffff0000u),
+                          __uint_as_float(o[h][1] << 16), __uint_as_float(o[h][1] & 0xffff0000u)};
+            if constexpr (EPI == NT_EPI_BIAS_STATS) {
+              const float bb[4] = {bj.x, bj.y, bj.z, bj.w};
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float d = c[r] - bb[r];
+                st[0][j][r] += d;
+                st[1][j][r] += d * d;
+              }
+            } else {
+              const float4 mu = *reinterpret_cast<const float4*>(mean_s + j * 16 + q * 4);
+              const float4 is = *reinterpret_cast<const float4*>(istd_s + j * 16 + q * 4);
+              const float mm[4] = {mu.x, mu.y, mu.z, mu.w}, ii[4] = {is.x, is.y, is.z, is.w};
+              const u32x2 tw = tv[j];
+              const bf16* tb = reinterpret_cast<const bf16*>(&tw);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) {
+                const float xh = ((float)tb[r] - mm[r]) * ii[r];
+                st[0][j][r] += c[r];
+                st[1][j][r] += c[r] * xh;
+              }
+            }
+          }
         }
         if constexpr (EPI == NT_EPI_F32) {
 #pragma unroll
@@ -222,22 +332,63 @@ __global__ __launch_bounds__(NT, 1) void gemm_nt_kernel(NtArgs a) {
             o[0][d] = sw[0];
             o[1][d] = sw[1];
           }
-          const u32x4 st = {o[0][0], o[0][1], o[1][0], o[1][1]};
+          const u32x4 stv = {o[0][0], o[0][1], o[1][0], o[1][1]};
           const int n = n0 + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8;
-          const int off = (mok && n < a.N) ? (int)((m * a.ldc + n) * 2) : OOR;
+          const int64_t ms = (NT_LAB_MODE & 8) ? (m & 4095) : m;   // lab: C writes to a window
+          const int off = (mok && n < a.N) ? (int)((ms * a.ldc + n) * 2) : OOR;
           if constexpr (!(NT_LAB_MODE & 1))
-            __builtin_amdgcn_raw_buffer_store_b128(st, cr, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(stv, cr, off, 0, NT_STORE_AUX);
           else if (acc[i][0][0] == 12345.f)
-            __builtin_amdgcn_raw_buffer_store_b128(st, cr, off, 0, 0);
+            __builtin_amdgcn_raw_buffer_store_b128(stv, cr, off, 0, NT_STORE_AUX);
         }
       }
+    }
+    if constexpr (STATS) {
+      // reduce-scatter the 64 per-lane partials over the 16 lanes of a lane
+      // row (same columns, different rows): 4 DPP butterfly steps, each lane
+      // keeps half of what it holds (selected by one lane bit) and adds the
+      // partner's copy.  Value index v = k*32 + j*4 + r.
+      float x[64];
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) x[k * 32 + j * 4 + r] = st[k][j][r];
+      bfly_step<32, 0x141>(x, (lane & 4) != 0);   // partner lane^7, keep by bit 2
+      bfly_step<16, 0x128>(x, (lane & 8) != 0);   // lane^8 (row_ror:8), bit 3
+      bfly_step<8, 0xB1>(x, (lane & 1) != 0);     // lane^1, bit 0
+      bfly_step<4, 0x4E>(x, (lane & 2) != 0);     // lane^2, bit 1
+#pragma unroll
+      for (int u = 0; u < 4; ++u) tot[u] += x[u];
+    }
+  }
+  if constexpr (STATS) {
+    // lane (q, m) holds k = bit2(m), j = bit1(m) + 2 bit0(m) + 4 bit3(m),
+    // columns 16j + 4q + u.  Sum the waves in fixed order and write this
+    // workgroup's partial row part[group][k][n0 + col].
+    __syncthreads();   // every wave is done with the W slice: reuse its LDS
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) red[(wave * 64 + lane) * 4 + u] = tot[u];
+    __syncthreads();
+    for (int t = tid; t < 2 * TN; t += NT) {
+      const int k = t / TN, col = t % TN;
+      const int j = col >> 4, qq = (col >> 2) & 3, u = col & 3;
+      const int mm = (k << 2) | (((j >> 2) & 1) << 3) | ((j >> 1) & 1) | ((j & 1) << 1);
+      const int ln = qq * 16 + mm;
+      float sum = 0.f;
+      for (int w = 0; w < NWAVE; ++w) sum += red[(w * 64 + ln) * 4 + u];
+      const int n = n0 + col;
+      if (n < a.N) a.part[((int64_t)group * 2 + k) * a.N + n] = sum;
     }
   }
 }
 
 template <int KTP, int EPI>
-dcnr_status launch_nt(NtArgs a, hipStream_t s) {
+dcnr_status launch_nt(NtArgs a, hipStream_t s, int* nparts) {
   using C = NtCfg<KTP>;
+  constexpr int NT = Geo<EPI>::NT, TM = Geo<EPI>::TM;
   static bool attr_set = false;
   if (!attr_set) {
     DCNR_HIP(hipFuncSetAttribute((const void*)gemm_nt_kernel<KTP, EPI>,
@@ -246,18 +397,26 @@ dcnr_status launch_nt(NtArgs a, hipStream_t s) {
   }
   a.nslices = (int)cdiv(a.N, TN);
   // 32-bit buffer offsets: launch in M-chunks of < 2^29 bytes per operand
-  const int64_t maxld = std::max<int64_t>({a.ldx, a.ldc * 2, a.R ? a.ldr : 0});
+  const int64_t maxld = std::max<int64_t>({a.ldx, a.ldc * 2, a.R ? a.ldr : 0, a.H ? a.ldh : 0,
+                                           a.T ? a.ldt : 0});
   const int64_t mchunk = std::max<int64_t>(TM, ((int64_t(1) << 29) / (maxld * 2)) / TM * TM);
   if (a.M > mchunk) {
+    int total = 0;
     for (int64_t m0 = 0; m0 < a.M; m0 += mchunk) {
       NtArgs b = a;
       b.M = std::min(mchunk, a.M - m0);
       b.X = a.X + m0 * a.ldx;
       b.C = (char*)a.C + m0 * a.ldc * (EPI == NT_EPI_F32 ? 4 : 2);
       if (a.R) b.R = (const char*)a.R + m0 * a.ldr * 2;
-      dcnr_status st = launch_nt<KTP, EPI>(b, s);
+      if (a.H) b.H = a.H + m0 * a.ldh;
+      if (a.T) b.T = a.T + m0 * a.ldt;
+      if (a.part) b.part = a.part + (int64_t)total * 2 * a.N;
+      int np = 0;
+      dcnr_status st = launch_nt<KTP, EPI>(b, s, &np);
       if (st != DCNR_OK) return st;
+      total += np;
     }
+    if (nparts) *nparts = total;
     return DCNR_OK;
   }
   a.mtiles = cdiv(a.M, TM);
@@ -267,33 +426,48 @@ dcnr_status launch_nt(NtArgs a, hipStream_t s) {
   const int64_t need = a.mtiles * a.nslices;
   if (need < grid) grid = (int)(cdiv(need, unit) * unit);
   a.groups = grid / a.nslices;
+  if (nparts) *nparts = a.groups;
   hipLaunchKernelGGL((gemm_nt_kernel<KTP, EPI>), dim3(grid), dim3(NT), C::LDS_BYTES, s, a);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
 
 template <int EPI>
-dcnr_status dispatch_k(const NtArgs& a, hipStream_t s) {
-  if (a.K <= 128) return launch_nt<4, EPI>(a, s);
-  if (a.K <= 256) return launch_nt<8, EPI>(a, s);
-  return launch_nt<16, EPI>(a, s);
+dcnr_status dispatch_k(const NtArgs& a, hipStream_t s, int* nparts) {
+  if (a.K <= 128) return launch_nt<4, EPI>(a, s, nparts);
+  if (a.K <= 256) return launch_nt<8, EPI>(a, s, nparts);
+  return launch_nt<16, EPI>(a, s, nparts);
 }
 
 }  // namespace
 
 bool gemm_nt_supported(int64_t K, int64_t N) { return K <= 512 && K % 8 == 0 && N % 8 == 0; }
 
-dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s) {
+// Upper bound of the part rows a stats epilogue writes (workspace sizing).
+int gemm_nt_max_parts(int64_t M, int N) {
+  const int64_t chunks =
+      cdiv(M, std::max<int64_t>(TM_MIN, ((int64_t(1) << 29) / (1024 * 2)) / TM_MIN * TM_MIN)) + 1;
+  return (int)(chunks * std::max<int64_t>(256 / (8 * cdiv(N, TN)), 1) * 8);
+}
+
+dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
+  if (nparts) *nparts = 0;
   if (a.M <= 0 || a.N <= 0) return DCNR_OK;
+  const bool ht = epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN;
   if (!gemm_nt_supported(a.K, a.N) || a.ldx % 8 || a.ldw % 8 || a.ldc % 8 ||
-      (epi == NT_EPI_RESID && a.ldr % 8)) {
-    set_error("gemm_nt: unsupported K=%d N=%d", a.K, a.N);
+      ((epi == NT_EPI_RESID || epi == NT_EPI_RESID_BN) && (a.ldr % 8 || !a.R)) ||
+      (ht && (!a.H || !a.T || !a.mean || !a.invstd || a.ldh % 4 || a.ldt % 4)) ||
+      (nt_epi_stats(epi) && !a.part)) {
+    set_error("gemm_nt: unsupported K=%d N=%d / missing epilogue operand", a.K, a.N);
     return DCNR_UNSUPPORTED_SHAPE;
   }
   switch (epi) {
-    case NT_EPI_BIAS: return dispatch_k<NT_EPI_BIAS>(a, s);
-    case NT_EPI_F32: return dispatch_k<NT_EPI_F32>(a, s);
-    case NT_EPI_RESID: return dispatch_k<NT_EPI_RESID>(a, s);
+    case NT_EPI_BIAS: return dispatch_k<NT_EPI_BIAS>(a, s, nparts);
+    case NT_EPI_F32: return dispatch_k<NT_EPI_F32>(a, s, nparts);
+    case NT_EPI_RESID: return dispatch_k<NT_EPI_RESID>(a, s, nparts);
+    case NT_EPI_BIAS_STATS: return dispatch_k<NT_EPI_BIAS_STATS>(a, s, nparts);
+    case NT_EPI_RESID_BN: return dispatch_k<NT_EPI_RESID_BN>(a, s, nparts);
+    case NT_EPI_DROP_BN: return dispatch_k<NT_EPI_DROP_BN>(a, s, nparts);
   }
   set_error("gemm_nt: bad epilogue");
   return DCNR_BAD_ARG;

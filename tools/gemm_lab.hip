@@ -20,14 +20,26 @@ void set_error(const char* fmt, ...) {
 int main(int argc, char** argv) {
   const int64_t M = argc > 1 ? atol(argv[1]) : 131072;
   const int K = argc > 2 ? atoi(argv[2]) : 512, N = argc > 3 ? atoi(argv[3]) : 512;
+  const int ldx = argc > 4 ? atoi(argv[4]) : K, ldc = argc > 5 ? atoi(argv[5]) : N;
   dcnr::bf16 *X, *W, *C;
   float* b;
-  hipMalloc(&X, M * K * 2); hipMalloc(&W, (size_t)N * K * 2); hipMalloc(&C, M * N * 2);
+  hipMalloc(&X, M * ldx * 2); hipMalloc(&W, (size_t)N * K * 2); hipMalloc(&C, M * ldc * 2);
   hipMalloc(&b, N * 4);
-  hipMemset(X, 0x3c, M * K * 2); hipMemset(W, 0x3c, (size_t)N * K * 2); hipMemset(b, 0, N * 4);
+  {  // random bf16 in [-1, 1): MFMA power (and so clocks) depend on the data
+    std::vector<uint16_t> h(std::max<size_t>(M * ldx, (size_t)N * K));
+    uint32_t st = 12345;
+    for (auto& v : h) {
+      st = st * 1664525u + 1013904223u;
+      const float f = (float)(st >> 8) / 8388608.f - 1.f;
+      v = (uint16_t)(__builtin_bit_cast(uint32_t, f) >> 16);
+    }
+    hipMemcpy(X, h.data(), M * ldx * 2, hipMemcpyHostToDevice);
+    hipMemcpy(W, h.data(), (size_t)N * K * 2, hipMemcpyHostToDevice);
+    hipMemset(b, 0, N * 4);
+  }
   dcnr::NtArgs a;
   std::memset(&a, 0, sizeof(a));
-  a.X = X; a.ldx = K; a.M = M; a.K = K; a.W = W; a.ldw = K; a.N = N; a.C = C; a.ldc = N; a.bias = b;
+  a.X = X; a.ldx = ldx; a.M = M; a.K = K; a.W = W; a.ldw = K; a.N = N; a.C = C; a.ldc = ldc; a.bias = b;
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   for (int i = 0; i < 3; ++i) dcnr::gemm_nt(dcnr::NT_EPI_BIAS, a, 0);
@@ -39,7 +51,7 @@ int main(int argc, char** argv) {
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
   double us = ms * 1e3 / it;
-  printf("mode %d  M=%ld K=%d N=%d  %.1f us  %.0f TF/s  %.2f TB/s\n", NT_LAB_MODE, (long)M, K, N, us,
+  printf("waves %d rb %d depth %d  mode %d  M=%ld K=%d N=%d ldx=%d ldc=%d  %.1f us  %.0f TF/s  %.2f TB/s\n", NT_WAVES, NT_RB, NT_DEPTH, NT_LAB_MODE, (long)M, K, N, ldx, ldc, us,
          2.0 * M * N * K / us / 1e6, (M * K * 2.0 + M * N * 2.0) / us / 1e6);
   return 0;
 }
