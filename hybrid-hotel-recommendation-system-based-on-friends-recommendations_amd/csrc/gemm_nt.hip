@@ -44,23 +44,39 @@ namespace {
 #ifndef NT_STORE_AUX
 #define NT_STORE_AUX 0
 #endif
+#ifndef NT_EPI_SPREAD
+#define NT_EPI_SPREAD 0
+#endif
+#ifndef NT_R_EARLY
+#define NT_R_EARLY 0
+#endif
 #ifndef NT_DEPTH
 #define NT_DEPTH 8
+#endif
+#ifndef NT_DEPTH_STATS
+#define NT_DEPTH_STATS 4
 #endif
 #ifndef NT_WAVES_STATS
 #define NT_WAVES_STATS 4
 #endif
 constexpr int RB = NT_RB, WROWS = 16 * RB, TN = 128, BK = 32;
 // stats epilogues hold more live state: one wave per SIMD (512 registers)
+//  * plain epilogues: 8 waves (2 per SIMD), ring depth 8;
+//  * BIAS_STATS: 8 waves, ring depth 4 (registers for the per-tile partials);
+//  * RESID_BN / DROP_BN: 4 waves (512 registers each) -- the mask/BN operands
+//    and partials kept over all tiles.
 template <int EPI> struct Geo {
-  static constexpr int NWAVE = EPI >= NT_EPI_BIAS_STATS ? NT_WAVES_STATS : NT_WAVES;
+  static constexpr bool HT = EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN;
+  static constexpr int NWAVE = HT ? NT_WAVES_STATS : NT_WAVES;
+  static constexpr int DEPTH = EPI == NT_EPI_BIAS_STATS ? NT_DEPTH_STATS : NT_DEPTH;
+  static constexpr bool PERSIST = HT && NWAVE == 4;
   static constexpr int NT = 64 * NWAVE, TM = NWAVE * WROWS;
 };
 constexpr int TM_MIN = 64 * WROWS / 16;   // smallest TM of any epilogue (4 waves)
 
 template <int KTP> struct NtCfg {
   static constexpr int WCH = KTP * (BK / 8);                 // 16-B chunks per W row
-  static constexpr int DEPTH = KTP < NT_DEPTH ? KTP : NT_DEPTH;            // prefetch ring depth (k-steps)
+  static constexpr int DEPTH = KTP;   // (capped per epilogue by Geo::DEPTH)
   static constexpr int W_LDS = TN * WCH;                     // uint4 units
   static constexpr int BIAS_LDS = 3 * TN / 4;                // uint4 units (bias, mean, invstd)
   static constexpr size_t LDS_BYTES = (size_t)(W_LDS + BIAS_LDS) * 16;
@@ -88,6 +104,40 @@ __device__ __forceinline__ void load_x(u32x4 (&f)[RB], __amdgpu_buffer_rsrc_t xr
   }
 }
 
+// An epilogue operand tile (rows r0 + 16i + (lane&15), 128 columns from n0)
+// loaded in the store layout: 16 B per lane, columns 16(2jp + (q&1)) +
+// 8(q>>1) .. +7 -- 64 contiguous bytes per row and instruction.
+__device__ __forceinline__ u32x4 load_epi1(__amdgpu_buffer_rsrc_t r, int64_t ld, int64_t r0, int i,
+                                           int jp, int n0, int N, int64_t M, int lane) {
+  const int q = lane >> 4;
+  const int64_t m = r0 + i * 16 + (lane & 15);
+  const int n = n0 + (2 * jp + (q & 1)) * 16 + (q >> 1) * 8;
+  const bool ok = n < N && m < M;
+  return __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (int)((m * ld + n) * 2) : OOR, 0, 0);
+}
+__device__ __forceinline__ void load_epi(u32x4 (&o)[RB][4], __amdgpu_buffer_rsrc_t r, int64_t ld,
+                                         int64_t r0, int n0, int N, int64_t M, int lane) {
+#pragma unroll
+  for (int i = 0; i < RB; ++i)
+#pragma unroll
+    for (int jp = 0; jp < 4; ++jp) o[i][jp] = load_epi1(r, ld, r0, i, jp, n0, N, M, lane);
+}
+// store layout -> accumulator layout of fragments 2jp, 2jp+1 (columns
+// 16j + 4q .. +3): the inverse of the epilogue's v_permlane16_swap (an involution)
+__device__ __forceinline__ void to_acc_layout(const u32x4& L, u32x2 (&f)[2]) {
+  auto a = __builtin_amdgcn_permlane16_swap(L[0], L[2], false, false);
+  auto b = __builtin_amdgcn_permlane16_swap(L[1], L[3], false, false);
+  f[0] = u32x2{a[0], b[0]};
+  f[1] = u32x2{a[1], b[1]};
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// bf16 pair (low half = first) -> two floats
+__device__ __forceinline__ f2v unpack2(uint32_t w) {
+  return f2v{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+
 // One reduce-scatter step over lane pairs (lane, partner(lane)) given by the
 // DPP control: x[u] (u < H) becomes the pair-sum of x[u] (hi = false) or of
 // x[u + H] (hi = true); partners have opposite `hi`.
@@ -101,12 +151,34 @@ __device__ __forceinline__ void bfly_step(float (&x)[64], bool hi) {
   }
 }
 
+// Reduce-scatter the 64 per-lane partials over the 16 lanes of a lane row
+// (same columns, different rows): 4 DPP butterfly steps, each lane keeps half
+// of what it holds (selected by one lane bit) and adds the partner's copy.
+// Value index v = k*32 + j*4 + r; the lane's 4 results are added to tot.
+__device__ __forceinline__ void stats_reduce(const f2v (&st)[2][8][2], float (&tot)[4], int lane) {
+  float x[64];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) x[k * 32 + j * 4 + r] = st[k][j][r >> 1][r & 1];
+  bfly_step<32, 0x141>(x, (lane & 4) != 0);   // partner lane^7, keep by bit 2
+  bfly_step<16, 0x128>(x, (lane & 8) != 0);   // lane^8 (row_ror:8), bit 3
+  bfly_step<8, 0xB1>(x, (lane & 1) != 0);     // lane^1, bit 0
+  bfly_step<4, 0x4E>(x, (lane & 2) != 0);     // lane^2, bit 1
+#pragma unroll
+  for (int u = 0; u < 4; ++u) tot[u] += x[u];
+}
+
 template <int KTP, int EPI>
 __global__ __launch_bounds__(Geo<EPI>::NT, 1) void gemm_nt_kernel(NtArgs a) {
   constexpr bool STATS = EPI >= NT_EPI_BIAS_STATS;
   constexpr int NT = Geo<EPI>::NT, TM = Geo<EPI>::TM, NWAVE = Geo<EPI>::NWAVE;
+  constexpr bool PERSIST = Geo<EPI>::PERSIST;
+  constexpr bool HAS_BIAS = EPI <= NT_EPI_BIAS_STATS;
   using C = NtCfg<KTP>;
-  constexpr int DEPTH = C::DEPTH;
+  constexpr int DEPTH = KTP < Geo<EPI>::DEPTH ? KTP : Geo<EPI>::DEPTH;   // prefetch ring (k-steps)
   extern __shared__ __attribute__((aligned(16))) uint4 lds[];
   uint4* Ws = lds;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -132,6 +204,17 @@ __global__ __launch_bounds__(Geo<EPI>::NT, 1) void gemm_nt_kernel(NtArgs a) {
   const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.T, (short)0, HAS_HT ? (int)(a.M * a.ldt * 2) : 0, 0x00020000);
   float tot[4] = {0.f, 0.f, 0.f, 0.f};   // stats epilogues: this lane's share over all tiles
+  // per-lane column partials [sum, sum2][fragment j][column pair]: per tile, or
+  // (PERSIST, one wave per SIMD: registers to spare) over all of the WG's tiles
+  f2v st[2][8][2];
+  if constexpr (STATS && PERSIST) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) st[k][j][r] = f2v{0.f, 0.f};
+  }
 
   // start the X stream before the W slice load so both are in flight
   u32x4 ring[DEPTH][RB];
@@ -153,13 +236,13 @@ __global__ __launch_bounds__(Geo<EPI>::NT, 1) void gemm_nt_kernel(NtArgs a) {
   // bias (and BN mean / invstd) slices in LDS, read per tile in the
   // epilogue (registers go to the ring)
   float* bias_s = reinterpret_cast<float*>(lds + C::W_LDS);
-  float* mean_s = bias_s + TN;
+  float* nmi_s = bias_s + TN;    // -mean * invstd
   float* istd_s = bias_s + 2 * TN;
   for (int c = tid; c < TN; c += NT) {
     const int n = n0 + c;
     bias_s[c] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
     if constexpr (HAS_HT) {
-      mean_s[c] = n < a.N ? a.mean[n] : 0.f;
+      nmi_s[c] = n < a.N ? -a.mean[n] * a.invstd[n] : 0.f;
       istd_s[c] = n < a.N ? a.invstd[n] : 0.f;
     }
   }
@@ -174,21 +257,12 @@ __global__ __launch_bounds__(Geo<EPI>::NT, 1) void gemm_nt_kernel(NtArgs a) {
 
   for (int64_t mt = group; mt < a.mtiles; mt += groups) {
     const int64_t r0 = mt * TM + wave * WROWS;
-    // residual operand of this tile, issued ahead of the k-loop's refills so
-    // that waiting for it in the epilogue does not drain the prefetch ring
-    u32x2 resid[RB][8];
-    if constexpr (HAS_R) {
-#pragma unroll
-      for (int i = 0; i < RB; ++i)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int n = n0 + j * 16 + (lane >> 4) * 4;
-          const int64_t m = r0 + i * 16 + (lane & 15);
-          const bool ok = n < a.N && m < a.M;
-          resid[i][j] = __builtin_amdgcn_raw_buffer_load_b64(
-              rr_, ok ? (int)((m * a.ldr + n) * 2) : OOR, 0, 0);
-        }
-    }
+    // epilogue operands of this tile: residual, mask source, BN input
+    u32x4 resid[RB][4], hv[RB][4], tv[RB][4];
+#if NT_R_EARLY
+    // (issued ahead of the k-loop's refills)
+    if constexpr (HAS_R) load_epi(resid, rr_, a.ldr, r0, n0, a.N, a.M, lane);
+#endif
     f32x4 acc[RB][8];
 #pragma unroll
     for (int i = 0; i < RB; ++i)
@@ -212,6 +286,22 @@ __global__ __launch_bounds__(Geo<EPI>::NT, 1) void gemm_nt_kernel(NtArgs a) {
             acc[i][j][0] += (float)xf[i][j] + (float)wf[j][0];
         wf[j] = __builtin_bit_cast(bf16x8, Ws[w_slot<C::WCH>(j * 16 + (lane & 15), kn * 4 + (lane >> 4))]);
       }
+#if NT_EPI_SPREAD
+      // this tile's epilogue operands, spread evenly over the k-steps (a
+      // steady trickle beside the ring refills instead of a burst at the end)
+      if constexpr (HAS_R || HAS_HT) {
+        constexpr int NOP = (HAS_R ? 1 : 0) + (HAS_HT ? 2 : 0), NL = NOP * RB * 4;
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+          if (l * KTP / NL != kt) continue;
+          const int op = l / (RB * 4), i = (l / 4) % RB, jp = l % 4;
+          const int which = HAS_R ? op : op + 1;   // 0: R, 1: H, 2: T
+          if (which == 0) resid[i][jp] = load_epi1(rr_, a.ldr, r0, i, jp, n0, a.N, a.M, lane);
+          else if (which == 1) hv[i][jp] = load_epi1(hr, a.ldh, r0, i, jp, n0, a.N, a.M, lane);
+          else tv[i][jp] = load_epi1(tr, a.ldt, r0, i, jp, n0, a.N, a.M, lane);
+        }
+      }
+#endif
       // refill the slot with the k-step DEPTH ahead (same or next M-tile)
       if constexpr (!(NT_LAB_MODE & 2)) {
         const int kd = kt + DEPTH;
@@ -234,84 +324,92 @@ __global__ __launch_bounds__(Geo<EPI>::NT, 1) void gemm_nt_kernel(NtArgs a) {
     // v_permlane16_swap so every lane stores 8 consecutive columns (16 B) and
     // each store instruction writes 64 contiguous bytes per output row.
     const int q = lane >> 4;
-    float st[2][8][4];   // stats epilogues: per-lane column partials of this tile
-    if constexpr (STATS) {
+#if !NT_R_EARLY && !NT_EPI_SPREAD
+    if constexpr (HAS_R) load_epi(resid, rr_, a.ldr, r0, n0, a.N, a.M, lane);
+#endif
+#if !NT_EPI_SPREAD
+    if constexpr (HAS_HT) {
+      load_epi(hv, hr, a.ldh, r0, n0, a.N, a.M, lane);
+      load_epi(tv, tr, a.ldt, r0, n0, a.N, a.M, lane);
+    }
+#endif
+    if constexpr (STATS && !PERSIST) {
 #pragma unroll
       for (int k = 0; k < 2; ++k)
 #pragma unroll
         for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) st[k][j][r] = 0.f;
+          for (int r = 0; r < 2; ++r) st[k][j][r] = f2v{0.f, 0.f};
     }
 #pragma unroll
     for (int i = 0; i < RB; ++i) {
       const int64_t m = r0 + i * 16 + (lane & 15);
       const bool mok = m < a.M;
-      // mask source and BN input of this row block (one wait for all 16 loads)
-      u32x2 hv[8], tv[8];
-      if constexpr (EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const int n = n0 + j * 16 + q * 4;
-          const bool ok = n < a.N && mok;
-          hv[j] = __builtin_amdgcn_raw_buffer_load_b64(hr, ok ? (int)((m * a.ldh + n) * 2) : OOR, 0, 0);
-          tv[j] = __builtin_amdgcn_raw_buffer_load_b64(tr, ok ? (int)((m * a.ldt + n) * 2) : OOR, 0, 0);
-        }
-      }
 #pragma unroll
       for (int jp = 0; jp < 4; ++jp) {
         u32x2 o[2];
         u32x4 of[2];
+        u32x2 rf[2], hf[2], tf[2];   // epilogue operands of fragments 2jp, 2jp+1
+        if constexpr (HAS_R) to_acc_layout(resid[i][jp], rf);
+        if constexpr (HAS_HT) {
+          to_acc_layout(hv[i][jp], hf);
+          to_acc_layout(tv[i][jp], tf);
+        }
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int j = 2 * jp + h;
-          const float4 bj = *reinterpret_cast<const float4*>(bias_s + j * 16 + q * 4);
-          float v[4] = {acc[i][j][0] + bj.x, acc[i][j][1] + bj.y, acc[i][j][2] + bj.z,
-                        acc[i][j][3] + bj.w};
-          if constexpr (EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN) {
-            const u32x2 rv = resid[i][j];
-            const bf16* rb = reinterpret_cast<const bf16*>(&rv);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += (float)rb[r];
+          // two column pairs (4q, 4q+1) and (4q+2, 4q+3) of fragment j
+          f2v v[2] = {f2v{acc[i][j][0], acc[i][j][1]}, f2v{acc[i][j][2], acc[i][j][3]}};
+          f2v bb[2];
+          if constexpr (HAS_BIAS) {
+            const float4 bj = *reinterpret_cast<const float4*>(bias_s + j * 16 + q * 4);
+            bb[0] = f2v{bj.x, bj.y};
+            bb[1] = f2v{bj.z, bj.w};
+            v[0] += bb[0];
+            v[1] += bb[1];
           }
-          if constexpr (EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN) {
-            const u32x2 hw = hv[j];
-            const uint16_t* hb = reinterpret_cast<const uint16_t*>(&hw);
+          if constexpr (HAS_R) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              // RESID_BN: [h > 0] on the bf16 bits (sign clear, not +-0);
-              // DROP_BN: [h != 0] (the saved dropout activation)
-              const bool keep = EPI == NT_EPI_RESID_BN ? (hb[r] != 0 && hb[r] < 0x8000u)
-                                                       : (hb[r] & 0x7fffu) != 0;
-              v[r] = keep ? (EPI == NT_EPI_DROP_BN ? v[r] * a.hscale : v[r]) : 0.f;
+            for (int d = 0; d < 2; ++d) v[d] += unpack2(rf[h][d]);
+          }
+          if constexpr (EPI == NT_EPI_DROP_BN) {
+            v[0] *= a.hscale;
+            v[1] *= a.hscale;
+          }
+          o[h] = u32x2{pack2(v[0][0], v[0][1]), pack2(v[1][0], v[1][1])};
+          of[h] = u32x4{__float_as_uint(v[0][0]), __float_as_uint(v[0][1]),
+                        __float_as_uint(v[1][0]), __float_as_uint(v[1][1])};
+          if constexpr (HAS_HT) {
+            // RESID_BN: keep where h > 0 (bf16 bits: magnitude != 0, sign clear);
+            // DROP_BN: keep where h != 0 (the saved dropout activation)
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+              const uint32_t hw = hf[h][d];
+              uint32_t keep = ((hw & 0x7fff7fffu) + 0x7fff7fffu) & 0x80008000u;
+              if constexpr (EPI == NT_EPI_RESID_BN) keep &= ~hw;
+              o[h][d] &= (keep >> 15) * 0xffffu;
             }
           }
-          o[h] = u32x2{pack2(v[0], v[1]), pack2(v[2], v[3])};
-          of[h] = u32x4{__float_as_uint(v[0]), __float_as_uint(v[1]), __float_as_uint(v[2]),
-                        __float_as_uint(v[3])};
           if constexpr (STATS) {
-            // sums of the stored (bf16-rounded) values
-            float c[4] = {__uint_as_float(o[h][0] << 16), __uint_as_float(o[h][0] & 0xffff0000u),
-                          __uint_as_float(o[h][1] << 16), __uint_as_float(o[h][1] & 0xffff0000u)};
+            // sums of the stored (bf16-rounded) values, two columns per op
+            const f2v c[2] = {unpack2(o[h][0]), unpack2(o[h][1])};
             if constexpr (EPI == NT_EPI_BIAS_STATS) {
-              const float bb[4] = {bj.x, bj.y, bj.z, bj.w};
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float d = c[r] - bb[r];
-                st[0][j][r] += d;
-                st[1][j][r] += d * d;
+              for (int d = 0; d < 2; ++d) {
+                const f2v dd = c[d] - bb[d];
+                st[0][j][d] += dd;
+                st[1][j][d] += dd * dd;
               }
             } else {
-              const float4 mu = *reinterpret_cast<const float4*>(mean_s + j * 16 + q * 4);
+              const float4 nm = *reinterpret_cast<const float4*>(nmi_s + j * 16 + q * 4);
               const float4 is = *reinterpret_cast<const float4*>(istd_s + j * 16 + q * 4);
-              const float mm[4] = {mu.x, mu.y, mu.z, mu.w}, ii[4] = {is.x, is.y, is.z, is.w};
-              const u32x2 tw = tv[j];
-              const bf16* tb = reinterpret_cast<const bf16*>(&tw);
+              const f2v nmv[2] = {f2v{nm.x, nm.y}, f2v{nm.z, nm.w}};
+              const f2v isv[2] = {f2v{is.x, is.y}, f2v{is.z, is.w}};
 #pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const float xh = ((float)tb[r] - mm[r]) * ii[r];
-                st[0][j][r] += c[r];
-                st[1][j][r] += c[r] * xh;
+              for (int d = 0; d < 2; ++d) {
+                const f2v xh = unpack2(tf[h][d]) * isv[d] + nmv[d];
+                st[0][j][d] += c[d];
+                st[1][j][d] += c[d] * xh;
               }
             }
           }
@@ -343,27 +441,10 @@ __global__ __launch_bounds__(Geo<EPI>::NT, 1) void gemm_nt_kernel(NtArgs a) {
         }
       }
     }
-    if constexpr (STATS) {
-      // reduce-scatter the 64 per-lane partials over the 16 lanes of a lane
-      // row (same columns, different rows): 4 DPP butterfly steps, each lane
-      // keeps half of what it holds (selected by one lane bit) and adds the
-      // partner's copy.  Value index v = k*32 + j*4 + r.
-      float x[64];
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) x[k * 32 + j * 4 + r] = st[k][j][r];
-      bfly_step<32, 0x141>(x, (lane & 4) != 0);   // partner lane^7, keep by bit 2
-      bfly_step<16, 0x128>(x, (lane & 8) != 0);   // lane^8 (row_ror:8), bit 3
-      bfly_step<8, 0xB1>(x, (lane & 1) != 0);     // lane^1, bit 0
-      bfly_step<4, 0x4E>(x, (lane & 2) != 0);     // lane^2, bit 1
-#pragma unroll
-      for (int u = 0; u < 4; ++u) tot[u] += x[u];
-    }
+    if constexpr (STATS && !PERSIST) stats_reduce(st, tot, lane);
   }
   if constexpr (STATS) {
+    if constexpr (PERSIST) stats_reduce(st, tot, lane);
     // lane (q, m) holds k = bit2(m), j = bit1(m) + 2 bit0(m) + 4 bit3(m),
     // columns 16j + 4q + u.  Sum the waves in fixed order and write this
     // workgroup's partial row part[group][k][n0 + col].

@@ -8,8 +8,8 @@ for v in ${VARIANTS:-8:2:8}; do
   IFS=: read w r d <<< "$v"
   for m in ${MODES:-0}; do
     hipcc --offload-arch=gfx950 -O3 -std=c++17 -Wno-unused-value -Wno-unused-result \
-      -DNT_WAVES=$w -DNT_RB=$r -DNT_DEPTH=$d -DNT_LAB_MODE=$m gemm_lab.hip \
-      -o lab_bin/gemm_lab_${w}_${r}_${d}_$m &
+      -DNT_WAVES=$w -DNT_RB=$r -DNT_DEPTH=$d -DNT_LAB_MODE=$m $EXTRA gemm_lab.hip \
+      -o lab_bin/gemm_lab_${w}_${r}_${d}_$m$SUFFIX &
   done
 done
 wait
