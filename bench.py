@@ -42,6 +42,11 @@ GEMM_FLOP = {  # algorithmic FLOPs per sample per step (13.98 MFLO
 }
 # gather + x0 + 3 cross: 14 idx x 8 B + 14 rows x 128 B + 8 x 4 B read; x0 bf16 + zc written
 GATHER_BYTES = 14 * 8 + 14 * 32 * 4 + 8 * 4 + D * 2 + 4
+# algorithmic HBM bytes of the forward Linear class per step: X read + C write
+# (bf16) per sample, 9 launches (initial D -> H, then 2 x R H -> H), plus the
+# bf16 weights once per launch
+GEMM_FWD_BYTES_PER_SAMPLE = 2 * (D + H) + 2 * R * 2 * (H + H)
+GEMM_FWD_W_BYTES = 2 * (H * D + 2 * R * H * H)
 PEAK_BF16 = 2.5e15     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12
 
@@ -196,10 +201,16 @@ def main():
         samples = world * B * args.steps
         per_step_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1]}
         launches = {k: v[1] / args.steps for k, v in prof.items() if v[1]}
-        gemm_cls = "gemm_fwd"   # 9 launches/step, all gemm_nt_kernel<16,0> (the largest kernel)
+        # dominant kernel class: the 9 forward Linears per step (gemm_ws_kernel,
+        # 8 with the BN-statistics epilogue).  K = 512, N = 512 bf16 is below
+        # the MFMA/HBM ridge (256 < 312 FLOP/B): the binding roof is HBM.
+        gemm_cls = "gemm_fwd"
         ms, cnt = prof[gemm_cls]
         flop_launch = GEMM_FLOP[gemm_cls] * B * args.steps / cnt
-        achieved = flop_launch / (ms / cnt / 1e3) / 1e12
+        bytes_launch = (GEMM_FWD_BYTES_PER_SAMPLE * B + GEMM_FWD_W_BYTES) * args.steps / cnt
+        t_launch = ms / cnt / 1e3
+        achieved = flop_launch / t_launch / 1e12
+        achieved_gbs = bytes_launch / t_launch / 1e9
         g_ms, g_cnt = prof["gather_cross"]
         gather_gbs = GATHER_BYTES * B * args.steps / g_cnt / (g_ms / g_cnt / 1e3) / 1e9
         traffic = pmc_traffic(gemm_cls)
@@ -225,15 +236,17 @@ def main():
                        "deep": "3 cross + 4 x 512 residual", "parallelism": f"dp{world}"},
             "scored_pairs_per_sec": pairs_per_s,
             "final_loss": final_loss,
-            "roofline": {"bound": "mfma",
-                         "kernel": "gemm_nt_kernel<16,0> (deep-tower Linear fwd, class gemm_fwd)", "achieved": achieved / 1.0,
-                         "peak": PEAK_BF16 / 1e12 if args.precision == "bf16" else 157.3,
-                         "unit": "TFLOP/s",
-                         "frac": achieved / ((PEAK_BF16 / 1e12) if args.precision == "bf16"
-                                             else 157.3),
+            "roofline": {"bound": "hbm",
+                         "kernel": "gemm_ws_kernel (deep-tower Linear fwd, class gemm_fwd)",
+                         "achieved": achieved_gbs, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                         "frac": achieved_gbs / (PEAK_HBM / 1e9),
                          "traffic": traffic,
-                         "flop_per_launch": flop_launch,
-                         "avg_launch_ms": ms / cnt},
+                         "bytes_per_launch": bytes_launch,
+                         "avg_launch_ms": ms / cnt,
+                         "mfma_view": {"achieved_tflops": achieved,
+                                       "peak_tflops": PEAK_BF16 / 1e12 if args.precision == "bf16"
+                                       else 157.3,
+                                       "flop_per_launch": flop_launch}},
             "roofline_gather": {"bound": "hbm", "kernel": "gather_cross", "achieved": gather_gbs,
                                 "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                                 "frac": gather_gbs / (PEAK_HBM / 1e9),

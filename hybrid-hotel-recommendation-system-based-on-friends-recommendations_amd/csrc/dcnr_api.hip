@@ -367,6 +367,13 @@ dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train
   return DCNR_OK;
 }
 
+// The bf16 streaming GEMM: weight-stationary kernel (gemm_ws.hip), or the
+// weight-in-LDS one (gemm_nt.hip) when DCNR_GEMM_NT is set (A/B comparisons).
+dcnr_status gemm_stream(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr) {
+  static const bool nt = getenv("DCNR_GEMM_NT") != nullptr;
+  return nt ? gemm_nt(epi, a, s, nparts) : gemm_ws(epi, a, s, nparts);
+}
+
 // C = A . B^T with k-contiguous operands: bf16 -> the weight-resident streaming
 // kernel (gemm_nt.hip) when the weight fits LDS; otherwise the generic tiled
 // MFMA kernel (fp32 parity path, K > 512).
@@ -380,7 +387,7 @@ dcnr_status gemm_nn(int prec, int epi, const GemmArgs& g, int splits, hipStream_
     a.C = g.C; a.ldc = g.ldc; a.bias = g.bias;
     a.R = g.resid; a.ldr = g.ldr;
     int ne = epi == EPI_STORE_RESID ? NT_EPI_RESID : (g.out_f32 ? NT_EPI_F32 : NT_EPI_BIAS);
-    return gemm_nt(ne, a, s);
+    return gemm_stream(ne, a, s);
   }
   return gemm(prec, false, false, epi, g, splits, s);
 }
@@ -413,7 +420,7 @@ dcnr_status linear_fwd_stats(const Dims& d, const Layout& L, const void* A, int 
   a.W = (const bf16*)W; a.ldw = K; a.N = d.Hp;
   a.C = out; a.ldc = d.Hp; a.bias = bias;
   a.part = L.part;
-  return gemm_nt(NT_EPI_BIAS_STATS, a, s, nc);
+  return gemm_stream(NT_EPI_BIAS_STATS, a, s, nc);
 }
 
 // C = mask(H) * (X W^T [+ R]) and part = [sum C, sum C*xhat(T)] (BN backward)
@@ -430,7 +437,7 @@ dcnr_status linear_dx_bn(const Dims& d, const Layout& L, int epi, const void* X,
   a.T = (const bf16*)T; a.ldt = d.Hp;
   a.mean = bn.mean; a.invstd = bn.invstd;
   a.part = L.part;
-  return gemm_nt(epi, a, s, nc);
+  return gemm_stream(epi, a, s, nc);
 }
 
 // dW[N][Kc] = sum_b dY[b][n] X[b][k]   (real extents Nr x Kr written to out)

@@ -53,6 +53,35 @@ template <> struct St<bf16> {
 // ------------------------------------------------ buffer loads / hand-off
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+
+// LDS-DMA of 16 B per lane into lds_dst + 16 * lane (lds_dst wave-uniform),
+// from byte offset `off` of the buffer (an out-of-range offset writes 0).
+// Inline asm on purpose: hipcc tracks builtin LDS-DMAs as pending LDS writes
+// and drains them (vmcnt(0)) before every ds_read, which would serialise a stage ring;
+// the caller's counted vmcnt waits are the only synchronisation.
+// M0 is saved and restored inside the statement (it is compiler-reserved).
+__device__ __forceinline__ void dma16(u32x4 rsrc, int off, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(off), "s"(rsrc), "s"(lds_dst)
+      : "memory");
+}
+
+__device__ __forceinline__ u32x4 rsrc_words(const void* p, int64_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  return u32x4{(uint32_t)a, (uint32_t)(a >> 32) & 0xFFFFu, p ? (uint32_t)bytes : 0u, 0x00020000u};
+}
+
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
+}
+
 constexpr int OOR = 0x7fffff00;  // a buffer offset past num_records: loads 0, stores dropped
 
 // Raw buffer descriptor over [p, p + bytes) (bytes < 2^31).  Out-of-range
@@ -213,6 +242,8 @@ struct NtArgs {
 bool gemm_nt_supported(int64_t K, int64_t N);
 // nparts (stats epilogues): rows of part written (the nchunks of reduce_fused)
 dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
+// the same contract, weight-stationary kernel (gemm_ws.hip)
+dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
 inline bool nt_epi_stats(int epi) { return epi >= NT_EPI_BIAS_STATS; }
 
 // bf16 weight-gradient GEMM (gemm_dw.hip): slab[split][n][k] = sum over the

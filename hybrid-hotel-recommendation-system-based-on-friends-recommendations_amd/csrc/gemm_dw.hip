@@ -45,34 +45,6 @@ __device__ __forceinline__ int swz(int row, int x) {
   return row * ROWB + ((((x >> 5) ^ (row & 7)) << 5) | (x & 31));
 }
 
-// LDS-DMA of 16 B per lane into lds_dst + 16 * lane (lds_dst wave-uniform),
-// from byte offset `off` of the buffer (an out-of-range offset writes 0).
-// Inline asm on purpose: hipcc tracks builtin LDS-DMAs as pending LDS writes
-// and drains them (vmcnt(0)) before every ds_read, which would serialise the
-// stage ring; here the counted vmcnt waits below are the only synchronisation.
-// M0 is saved and restored inside the statement (it is compiler-reserved).
-__device__ __forceinline__ void dma16(u32x4 rsrc, int off, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(off), "s"(rsrc), "s"(lds_dst)
-      : "memory");
-}
-
-__device__ __forceinline__ u32x4 rsrc_words(const void* p, int64_t bytes) {
-  const uint64_t a = (uint64_t)p;
-  return u32x4{(uint32_t)a, (uint32_t)(a >> 32) & 0xFFFFu, p ? (uint32_t)bytes : 0u, 0x00020000u};
-}
-
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)p;
-}
-
 // One stage: rows kb..kb+31 of A (cols n0..n0+255) and B (cols c0..c0+255).
 // Each wave-instruction fills 1 KiB = 2 rows; 16 instructions per operand,
 // 2 per wave per operand (4 DMAs per wave per stage).

@@ -1,0 +1,439 @@
+// Weight-stationary streaming GEMM for the bf16 deep tower (gfx950):
+//
+//   C[M, N] = X[M, K] . W[N, K]^T  (+ epilogue),  K <= 512
+//
+// The deep tower's Linear layers (train.py:143,105,109) have a huge M (the
+// batch) and a small N x K weight: one pass over the activations.  Compared
+// with gemm_nt.hip (W slice in LDS, X fragments streamed per wave) this
+// kernel halves the X bytes each CU has to pull per FLOP:
+//  * a workgroup owns a 256-column slice of W and keeps it in REGISTERS for
+//    its whole lifetime: each of the 8 waves holds 32 columns x K as MFMA
+//    A-operand fragments (K = 512: 128 VGPRs per lane);
+//  * the X tile (64 rows x K) is staged once per workgroup into LDS by
+//    LDS-DMA (buffer_load ... lds, double-buffered, one barrier per tile) and
+//    read by all 8 waves as MFMA B-operand fragments (ds_read_b128, chunk
+//    XOR-swizzled by row: conflict-free);
+//  * so X is read from L2 twice for N = 512 (two slices, on one XCD), not
+//    four times, and the per-CU vector-memory traffic per FLOP halves;
+//  * v_mfma_f32_16x16x32_bf16 with W as A: each lane accumulates 4
+//    consecutive output columns of one row; the epilogue pairs the wave's two
+//    16-column blocks with v_permlane16_swap into 16-byte row-contiguous
+//    stores (and loads its operands the same way);
+//  * the BatchNorm-statistics epilogues keep per-lane column partials in
+//    registers over all of the workgroup's tiles (each wave owns its columns:
+//    no cross-wave reduction) and write one partial row per workgroup.
+#include "dcnr_internal.h"
+
+#ifndef WS_LAB_MODE
+#define WS_LAB_MODE 0   // tools/ws_lab.hip: 1 no C stores, 2 no X DMAs, 4 no MFMAs
+#endif
+
+namespace dcnr {
+namespace {
+
+// Per-epilogue tile rows and operand-load placement (measured with
+// tools/ws_lab.hip, M = 131072, K = N = 512): 64-row tiles where registers
+// allow; RESID_BN (three operands) needs 32-row tiles to have its operands in
+// flight during the MFMAs ("early"); RESID and DROP_BN load theirs one row
+// block ahead of use ("late").
+#ifndef WS_TM_PLAIN
+#define WS_TM_PLAIN 64
+#endif
+constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
+
+template <int EPI> constexpr int ws_tm() {
+  return EPI == NT_EPI_RESID ? 32 : EPI == NT_EPI_RESID_BN ? 32 : EPI == NT_EPI_DROP_BN ? 64 : WS_TM_PLAIN;
+}
+template <int EPI> constexpr bool ws_ops_early() { return EPI == NT_EPI_RESID_BN; }
+
+template <int KTP, int TM> struct WsCfg {
+  static constexpr int P = KTP * 64;                      // LDS bytes per X row
+  static constexpr int CPR = KTP * 4;                     // 16-B chunks per row
+  static constexpr int TILE = TM * P;                     // bytes per X buffer
+  static constexpr int RPD = 1024 / P;                    // rows per DMA wave-instruction
+  static constexpr int DPW = TM / RPD / WS_WAVES;         // DMAs per wave per tile
+  static constexpr int RB = TM / 16;                      // 16-row blocks per tile
+  static constexpr size_t LDS_BYTES = 2 * (size_t)TILE + 3 * WS_TN * 4;
+};
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  bf16 x = (bf16)a, y = (bf16)b;
+  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+}
+__device__ __forceinline__ f2v unpack2(uint32_t w) {
+  return f2v{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
+}
+// store layout (16 B per lane: columns 16(q&1) + 8(q>>1) .. +7 of the wave's
+// 32) <-> accumulator layout of the two column blocks (columns 16cb + 4q ..)
+__device__ __forceinline__ void to_acc_layout(const u32x4& L, u32x2 (&f)[2]) {
+  auto a = __builtin_amdgcn_permlane16_swap(L[0], L[2], false, false);
+  auto b = __builtin_amdgcn_permlane16_swap(L[1], L[3], false, false);
+  f[0] = u32x2{a[0], b[0]};
+  f[1] = u32x2{a[1], b[1]};
+}
+template <int H, int CTRL>
+__device__ __forceinline__ void bfly(float (&x)[16], bool hi) {
+#pragma unroll
+  for (int u = 0; u < H; ++u) {
+    const float give = hi ? x[u] : x[u + H];
+    const float keep = hi ? x[u + H] : x[u];
+    x[u] = keep + dpp<CTRL>(give);
+  }
+}
+
+// X tile rows m0 .. m0+63 -> LDS buffer `dst` (row r at r*P, 16-B chunk c at
+// position c ^ (r & 15)); xr covers rows from m0 on (rows >= M read 0).
+// (Lane offsets recomputed per tile: registers are the scarce resource here.)
+template <int KTP, int TM>
+__device__ __forceinline__ void issue_tile(u32x4 xr, int64_t ldx, int K, uint32_t dst, int wave,
+                                           int lane) {
+  using C = WsCfg<KTP, TM>;
+#pragma unroll
+  for (int d = 0; d < C::DPW; ++d) {
+    const int r = (wave * C::DPW + d) * C::RPD + lane / C::CPR;
+    const int c = (lane % C::CPR) ^ (r & 15);
+    const int off = c * 8 < K ? (int)(((int64_t)r * ldx + c * 8) * 2) : OOR;
+    if constexpr (!(WS_LAB_MODE & 2)) dma16(xr, off, dst + (wave * C::DPW + d) * 1024);
+  }
+}
+
+template <int KTP, int EPI>
+__global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
+  constexpr int WS_TM = ws_tm<EPI>();
+  using C = WsCfg<KTP, WS_TM>;
+  constexpr int WS_RB = C::RB;
+  constexpr bool STATS = EPI >= NT_EPI_BIAS_STATS;
+  constexpr bool HAS_R = EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN;
+  constexpr bool HAS_HT = EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN;
+  constexpr bool HAS_BIAS = EPI <= NT_EPI_BIAS_STATS;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, l15 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nsl = a.nslices, bid = blockIdx.x;
+  const int slice = (bid / 8) % nsl;
+  const int group = (bid % 8) + 8 * (bid / (8 * nsl));
+  const int groups = a.groups;
+  const int n0 = slice * WS_TN;
+  const int nw = n0 + wave * WS_WC;   // this wave's first column
+
+  // first tile's DMA goes out before anything else
+  auto tile_rsrc = [&](int64_t mt) {
+    const int64_t m0 = mt * WS_TM;
+    const int64_t rows = a.M - m0;
+    return rsrc_words(a.X + m0 * a.ldx, rows > 0 ? rows * a.ldx * 2 : 0);
+  };
+  const uint32_t lbase = lds_addr(lds);
+  if (group < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(group), a.ldx, a.K, lbase, wave, lane);
+
+  // resident W: fragments (column block cb, k-step kt) of columns nw + 16cb + l15
+  bf16x8 wf[2][KTP];
+  {
+    const __amdgpu_buffer_rsrc_t wr =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.W, (short)0, (int)((int64_t)a.N * a.ldw * 2), 0x00020000);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const int n = nw + cb * 16 + l15;
+#pragma unroll
+      for (int kt = 0; kt < KTP; ++kt) {
+        const int k = kt * 32 + 8 * q;
+        const bool ok = n < a.N && k < a.K;
+        wf[cb][kt] = __builtin_bit_cast(
+            bf16x8, __builtin_amdgcn_raw_buffer_load_b128(wr, ok ? (int)(((int64_t)n * a.ldw + k) * 2) : OOR, 0, 0));
+      }
+    }
+  }
+  // per-column constants of the slice: bias, -mean*invstd, invstd
+  float* bias_s = reinterpret_cast<float*>(lds + 2 * C::TILE);
+  float* nmi_s = bias_s + WS_TN;
+  float* istd_s = bias_s + 2 * WS_TN;
+  for (int c = tid; c < WS_TN; c += WS_NT) {
+    const int n = n0 + c;
+    bias_s[c] = (HAS_BIAS && a.bias && n < a.N) ? a.bias[n] : 0.f;
+    if constexpr (HAS_HT) {
+      nmi_s[c] = n < a.N ? -a.mean[n] * a.invstd[n] : 0.f;
+      istd_s[c] = n < a.N ? a.invstd[n] : 0.f;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int es = EPI == NT_EPI_F32 ? 4 : 2;
+  const __amdgpu_buffer_rsrc_t cr =
+      __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, (int)(a.M * a.ldc * es), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rr_ = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.R, (short)0, HAS_R ? (int)(a.M * a.ldr * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.H, (short)0, HAS_HT ? (int)(a.M * a.ldh * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.T, (short)0, HAS_HT ? (int)(a.M * a.ldt * 2) : 0, 0x00020000);
+
+  // per-lane column partials [sum, sum2][cb][column pair], over all tiles
+  f2v st[2][2][2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int r = 0; r < 2; ++r) st[k][cb][r] = f2v{0.f, 0.f};
+
+  // fragment read offsets: row rb*16 + l15, chunk (4kt + q) ^ l15
+  const uint32_t rowoff = (uint32_t)l15 * C::P;
+  int buf = 0;
+  for (int64_t mt = group; mt < a.mtiles; mt += groups, buf ^= 1) {
+    const int64_t mn = mt + groups;
+    if (mn < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + (buf ^ 1) * C::TILE, wave, lane);
+    const int64_t m0 = mt * WS_TM;
+    const int nst = nw + (q & 1) * 16 + (q >> 1) * 8;   // store-layout column
+    // epilogue operands (WS_OPS_EARLY: all issued before the MFMAs, else one
+    // row block ahead of their use)
+    constexpr bool WS_OPS_EARLY = ws_ops_early<EPI>();
+    constexpr int NSLOT = WS_OPS_EARLY ? WS_RB : 2;
+    u32x4 rv[NSLOT], hv[NSLOT], tv[NSLOT];
+    auto load_ops = [&](int rb, int slot) {
+      const int64_t m = m0 + rb * 16 + l15;
+      const bool ok = m < a.M && nst < a.N;
+      if constexpr (HAS_R)
+        rv[slot] = __builtin_amdgcn_raw_buffer_load_b128(rr_, ok ? (int)((m * a.ldr + nst) * 2) : OOR, 0, 0);
+      if constexpr (HAS_HT) {
+        hv[slot] = __builtin_amdgcn_raw_buffer_load_b128(hr, ok ? (int)((m * a.ldh + nst) * 2) : OOR, 0, 0);
+        tv[slot] = __builtin_amdgcn_raw_buffer_load_b128(tr, ok ? (int)((m * a.ldt + nst) * 2) : OOR, 0, 0);
+      }
+    };
+    if constexpr (WS_OPS_EARLY) {
+#pragma unroll
+      for (int rb = 0; rb < WS_RB; ++rb) load_ops(rb, rb);
+    } else {
+      load_ops(0, 0);
+    }
+    const char* xb = lds + buf * C::TILE + rowoff;
+
+    f32x4 acc[WS_RB][2];
+#pragma unroll
+    for (int rb = 0; rb < WS_RB; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 xf[2][WS_RB];
+#pragma unroll
+    for (int rb = 0; rb < WS_RB; ++rb)
+      xf[0][rb] = *reinterpret_cast<const bf16x8*>(xb + rb * 16 * C::P + ((q ^ l15) & 15) * 16);
+#pragma unroll
+    for (int kt = 0; kt < KTP; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < KTP) {
+        const int ch = ((4 * (kt + 1) + q) ^ l15);
+#pragma unroll
+        for (int rb = 0; rb < WS_RB; ++rb)
+          xf[cur ^ 1][rb] = *reinterpret_cast<const bf16x8*>(xb + rb * 16 * C::P + ch * 16);
+      }
+#pragma unroll
+      for (int rb = 0; rb < WS_RB; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          if constexpr (!(WS_LAB_MODE & 4))
+            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][kt], xf[cur][rb], acc[rb][cb], 0, 0, 0);
+          else
+            acc[rb][cb][0] += (float)xf[cur][rb][cb] + (float)wf[cb][kt][0];
+    }
+
+    // ---- epilogue: lane holds C[m][nw + 16cb + 4q .. +3], m = m0 + 16rb + l15
+#pragma unroll
+    for (int rb = 0; rb < WS_RB; ++rb) {
+      const int64_t m = m0 + rb * 16 + l15;
+      const bool mok = m < a.M;
+      if (!WS_OPS_EARLY && rb + 1 < WS_RB) load_ops(rb + 1, (rb + 1) & 1);
+      const int slot = WS_OPS_EARLY ? rb : rb & 1;
+      u32x2 o[2], rf[2], hf[2], tf[2];
+      u32x4 of[2];
+      if constexpr (HAS_R) to_acc_layout(rv[slot], rf);
+      if constexpr (HAS_HT) {
+        to_acc_layout(hv[slot], hf);
+        to_acc_layout(tv[slot], tf);
+      }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int cl = wave * WS_WC + cb * 16 + q * 4;   // column within the slice
+        f2v v[2] = {f2v{acc[rb][cb][0], acc[rb][cb][1]}, f2v{acc[rb][cb][2], acc[rb][cb][3]}};
+        f2v bb[2];
+        if constexpr (HAS_BIAS) {
+          const float4 bj = *reinterpret_cast<const float4*>(bias_s + cl);
+          bb[0] = f2v{bj.x, bj.y};
+          bb[1] = f2v{bj.z, bj.w};
+          v[0] += bb[0];
+          v[1] += bb[1];
+        }
+        if constexpr (HAS_R) {
+#pragma unroll
+          for (int d = 0; d < 2; ++d) v[d] += unpack2(rf[cb][d]);
+        }
+        if constexpr (EPI == NT_EPI_DROP_BN) {
+          v[0] *= a.hscale;
+          v[1] *= a.hscale;
+        }
+        o[cb] = u32x2{pack2(v[0][0], v[0][1]), pack2(v[1][0], v[1][1])};
+        of[cb] = u32x4{__float_as_uint(v[0][0]), __float_as_uint(v[0][1]),
+                       __float_as_uint(v[1][0]), __float_as_uint(v[1][1])};
+        if constexpr (HAS_HT) {
+          // RESID_BN: keep where h > 0 (bf16 bits: magnitude != 0, sign clear);
+          // DROP_BN: keep where h != 0 (the saved dropout activation)
+#pragma unroll
+          for (int d = 0; d < 2; ++d) {
+            const uint32_t hw = hf[cb][d];
+            uint32_t keep = ((hw & 0x7fff7fffu) + 0x7fff7fffu) & 0x80008000u;
+            if constexpr (EPI == NT_EPI_RESID_BN) keep &= ~hw;
+            o[cb][d] &= (keep >> 15) * 0xffffu;
+          }
+        }
+        if constexpr (STATS) {
+          // sums of the stored (bf16-rounded) values
+          if (mok) {
+            const f2v c[2] = {unpack2(o[cb][0]), unpack2(o[cb][1])};
+            if constexpr (EPI == NT_EPI_BIAS_STATS) {
+#pragma unroll
+              for (int d = 0; d < 2; ++d) {
+                const f2v dd = c[d] - bb[d];
+                st[0][cb][d] += dd;
+                st[1][cb][d] += dd * dd;
+              }
+            } else {
+              const float4 nm = *reinterpret_cast<const float4*>(nmi_s + cl);
+              const float4 is = *reinterpret_cast<const float4*>(istd_s + cl);
+              const f2v nmv[2] = {f2v{nm.x, nm.y}, f2v{nm.z, nm.w}};
+              const f2v isv[2] = {f2v{is.x, is.y}, f2v{is.z, is.w}};
+#pragma unroll
+              for (int d = 0; d < 2; ++d) {
+                const f2v xh = unpack2(tf[cb][d]) * isv[d] + nmv[d];
+                st[0][cb][d] += c[d];
+                st[1][cb][d] += c[d] * xh;
+              }
+            }
+          }
+        }
+      }
+      if constexpr (EPI == NT_EPI_F32) {
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          const int n = nw + cb * 16 + q * 4;
+          __builtin_amdgcn_raw_buffer_store_b128(
+              of[cb], cr, (mok && n < a.N) ? (int)((m * a.ldc + n) * 4) : OOR, 0, 0);
+        }
+      } else {
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+          auto sw = __builtin_amdgcn_permlane16_swap(o[0][d], o[1][d], false, false);
+          o[0][d] = sw[0];
+          o[1][d] = sw[1];
+        }
+        const u32x4 sv = {o[0][0], o[0][1], o[1][0], o[1][1]};
+        const int off = (mok && nst < a.N) ? (int)((m * a.ldc + nst) * 2) : OOR;
+        if constexpr (!(WS_LAB_MODE & 1))
+          __builtin_amdgcn_raw_buffer_store_b128(sv, cr, off, 0, 0);
+        else if (acc[rb][0][0] == 12345.f)
+          __builtin_amdgcn_raw_buffer_store_b128(sv, cr, off, 0, 0);
+      }
+    }
+    // next tile's X landed (this wave's DMAs are older than its epilogue's
+    // stores) and every wave is done reading this buffer
+    constexpr int NSTORE = (EPI == NT_EPI_F32 ? 2 : 1) * WS_RB;
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NSTORE) : "memory");
+  }
+  if constexpr (STATS) {
+    // 16-lane butterfly: lane (q, m) ends with k = bit2(m), cb = bit3(m),
+    // column pair element r = 2 bit0(m) + bit1(m) of columns nw + 16cb + 4q
+    float x[16];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) x[k * 8 + cb * 4 + r] = st[k][cb][r >> 1][r & 1];
+    bfly<8, 0x141>(x, (lane & 4) != 0);   // partner lane^7, keep by bit 2
+    bfly<4, 0x128>(x, (lane & 8) != 0);   // lane^8, bit 3
+    bfly<2, 0xB1>(x, (lane & 1) != 0);    // lane^1, bit 0
+    bfly<1, 0x4E>(x, (lane & 2) != 0);    // lane^2, bit 1
+    const int k = (lane >> 2) & 1, cb = (lane >> 3) & 1, r = 2 * (lane & 1) + ((lane >> 1) & 1);
+    const int n = nw + cb * 16 + q * 4 + r;
+    if (n < a.N) a.part[((int64_t)group * 2 + k) * a.N + n] = x[0];
+  }
+}
+
+template <int KTP, int EPI>
+dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
+  constexpr int WS_TM = ws_tm<EPI>();
+  using C = WsCfg<KTP, WS_TM>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    DCNR_HIP(hipFuncSetAttribute((const void*)gemm_ws_kernel<KTP, EPI>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES));
+    attr_set = true;
+  }
+  a.nslices = (int)cdiv(a.N, WS_TN);
+  // 32-bit buffer offsets: launch in M-chunks of < 2^29 bytes per operand
+  const int64_t maxld = std::max<int64_t>({a.ldx, a.ldc * 2, a.R ? a.ldr : 0, a.H ? a.ldh : 0,
+                                           a.T ? a.ldt : 0});
+  const int64_t mchunk = std::max<int64_t>(WS_TM, ((int64_t(1) << 29) / (maxld * 2)) / WS_TM * WS_TM);
+  if (a.M > mchunk) {
+    int total = 0;
+    for (int64_t m0 = 0; m0 < a.M; m0 += mchunk) {
+      NtArgs b = a;
+      b.M = std::min(mchunk, a.M - m0);
+      b.X = a.X + m0 * a.ldx;
+      b.C = (char*)a.C + m0 * a.ldc * (EPI == NT_EPI_F32 ? 4 : 2);
+      if (a.R) b.R = (const char*)a.R + m0 * a.ldr * 2;
+      if (a.H) b.H = a.H + m0 * a.ldh;
+      if (a.T) b.T = a.T + m0 * a.ldt;
+      if (a.part) b.part = a.part + (int64_t)total * 2 * a.N;
+      int np = 0;
+      dcnr_status st = launch_ws<KTP, EPI>(b, s, &np);
+      if (st != DCNR_OK) return st;
+      total += np;
+    }
+    if (nparts) *nparts = total;
+    return DCNR_OK;
+  }
+  a.mtiles = cdiv(a.M, WS_TM);
+  const int unit = 8 * a.nslices;
+  int grid = std::max(unit, (256 / unit) * unit);
+  const int64_t need = a.mtiles * a.nslices;
+  if (need < grid) grid = (int)(cdiv(need, unit) * unit);
+  a.groups = grid / a.nslices;
+  if (nparts) *nparts = a.groups;
+  hipLaunchKernelGGL((gemm_ws_kernel<KTP, EPI>), dim3(grid), dim3(WS_NT), C::LDS_BYTES, s, a);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+template <int EPI>
+dcnr_status dispatch_ws(const NtArgs& a, hipStream_t s, int* nparts) {
+  if (a.K <= 128) return launch_ws<4, EPI>(a, s, nparts);
+  if (a.K <= 256) return launch_ws<8, EPI>(a, s, nparts);
+  return launch_ws<16, EPI>(a, s, nparts);
+}
+
+}  // namespace
+
+dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
+  if (nparts) *nparts = 0;
+  if (a.M <= 0 || a.N <= 0) return DCNR_OK;
+  const bool ht = epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN;
+  if (!gemm_nt_supported(a.K, a.N) || a.ldx % 8 || a.ldw % 8 || a.ldc % 8 ||
+      ((epi == NT_EPI_RESID || epi == NT_EPI_RESID_BN) && (a.ldr % 8 || !a.R)) ||
+      (ht && (!a.H || !a.T || !a.mean || !a.invstd || a.ldh % 8 || a.ldt % 8)) ||
+      (nt_epi_stats(epi) && !a.part)) {
+    set_error("gemm_ws: unsupported K=%d N=%d / missing epilogue operand", a.K, a.N);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  switch (epi) {
+    case NT_EPI_BIAS: return dispatch_ws<NT_EPI_BIAS>(a, s, nparts);
+    case NT_EPI_F32: return dispatch_ws<NT_EPI_F32>(a, s, nparts);
+    case NT_EPI_RESID: return dispatch_ws<NT_EPI_RESID>(a, s, nparts);
+    case NT_EPI_BIAS_STATS: return dispatch_ws<NT_EPI_BIAS_STATS>(a, s, nparts);
+    case NT_EPI_RESID_BN: return dispatch_ws<NT_EPI_RESID_BN>(a, s, nparts);
+    case NT_EPI_DROP_BN: return dispatch_ws<NT_EPI_DROP_BN>(a, s, nparts);
+  }
+  set_error("gemm_ws: bad epilogue");
+  return DCNR_BAD_ARG;
+}
+
+}  // namespace dcnr

@@ -14,12 +14,14 @@ import json
 import re
 from collections import defaultdict
 
-# libdcnr kernel-name patterns -> the bench's kernel classes
+# libdcnr kernel-name patterns (regular expressions) -> the bench's kernel classes
 CLASSES = [
-    ("gemm_fwd", r"gemm_nt_kernel<16, 0>"),
-    ("gemm_nt_resid", r"gemm_nt_kernel<16, 2>"),
-    ("gemm_nt_f32", r"gemm_nt_kernel<16, 1>"),
-    ("gemm_dw", r"gemm_kernel<"),
+    # deep-tower forward Linears: initial layer (EPI 0) + 8 BN-input layers (EPI 3)
+    ("gemm_fwd", r"gemm_ws_kernel<16, [03]>"),
+    ("gemm_dx_bn", r"gemm_ws_kernel<16, [45]>"),
+    ("gemm_resid", r"gemm_ws_kernel<16, 2>"),
+    ("gemm_f32", r"gemm_ws_kernel<16, 1>"),
+    ("gemm_dw", r"gemm_dw_kernel"),
     ("gather_cross", r"gather_cross_fwd_kernel"),
     ("cross_bwd", r"cross_bwd_kernel"),
     ("adam", r"adam_kernel"),
@@ -64,7 +66,7 @@ def main():
         print(f"{n:8d} {fb / 1e6:10.2f} {wb / 1e6:10.2f}  {short(name)}")
     out = {}
     for cls, pat in CLASSES:
-        sel = [r for r in rows if re.search(re.escape(pat) if "<" in pat else pat, r[0])]
+        sel = [r for r in rows if re.search(pat, r[0])]
         if sel:
             n = sum(r[1] for r in sel)
             out[cls] = sum((r[2] + r[3]) * r[1] for r in sel) / max(n, 1)
