@@ -252,6 +252,29 @@ __global__ __launch_bounds__(NT) void gather_cross_fwd_kernel(GatherDesc g, Cros
 
 // --------------------------------------------------------------- backward
 // part layout per block: [L][D] dw | [L][D] db | [D] dwf | [1] dbf
+// Per-lane transposed LDS images: element e = lane + 64r of a D-vector sits
+// at [lane][r] (RM consecutive floats per lane: two ds_read_b128 per vector),
+// zero for e >= D, so the math below needs no per-element bounds tests.
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+template <int RM>
+__device__ __forceinline__ void lds_vec(const float* img, int lane, f2v (&v)[RM / 2]) {
+  const float4* p4 = reinterpret_cast<const float4*>(img + lane * RM);
+#pragma unroll
+  for (int i = 0; i < RM / 4; ++i) {
+    const float4 t = p4[i];
+    v[2 * i] = f2v{t.x, t.y};
+    v[2 * i + 1] = f2v{t.z, t.w};
+  }
+}
+template <int RM>
+__device__ __forceinline__ void lds_store_vec(float* img, int lane, const f2v (&v)[RM / 2]) {
+  float4* p4 = reinterpret_cast<float4*>(img + lane * RM);
+#pragma unroll
+  for (int i = 0; i < RM / 4; ++i)
+    p4[i] = float4{v[2 * i][0], v[2 * i][1], v[2 * i + 1][0], v[2 * i + 1][1]};
+}
+
 template <int RM, int L, int SPW>
 __global__ __launch_bounds__(NT, 2) void cross_bwd_kernel(GatherDesc g, CrossBwdParams p,
                                                         const int64_t* user, const int64_t* item,
@@ -259,36 +282,37 @@ __global__ __launch_bounds__(NT, 2) void cross_bwd_kernel(GatherDesc g, CrossBwd
                                                         const float* dz, int64_t B,
                                                         const float* dx0_deep, int ld_dx,
                                                         float* part) {
-  constexpr int S = SPW * WPB;
+  constexpr int S = SPW * WPB, V = RM * WAVE, H2 = RM / 2;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ TabLds tl;
   const int D = g.D;
-  float* sw = smem;
-  float* sb = sw + L * D;
-  float* swf = sb + L * D;
-  float* red = swf + D;                                   // [(2L+1)D+1] block partial
-  int* ids = reinterpret_cast<int*>(red + (2 * L + 1) * D + 1);  // [S][n_tab]
-  // per-wave cross activations x_0..x_L of the sample in flight (LDS instead
-  // of 32+ registers: keeps the kernel at 2 waves/SIMD without spills)
-  float* xsl = reinterpret_cast<float*>(ids + S * g.n_tab) + (threadIdx.x >> 6) * (L + 1) * RM * WAVE;
-  for (int i = threadIdx.x; i < L * D; i += NT) {
-    sw[i] = p.cp.w[i / D][i % D];
-    sb[i] = p.cp.b[i / D][i % D];
+  float* sw = smem;                 // [L][V] transposed images
+  float* sb = sw + L * V;           // [L][V]
+  float* swf = sb + L * V;          // [V]
+  float* red = swf + V;             // [(2L+1)D+1] block partial (16-B padded)
+  int* ids = reinterpret_cast<int*>(red + (((2 * L + 1) * D + 1 + 3) & ~3));  // [S][n_tab]
+  // per-wave cross activations x_0..x_{L-1} of the sample in flight (LDS
+  // instead of registers: keeps the kernel at 2 waves/SIMD without spills)
+  float* xsl = reinterpret_cast<float*>(ids + ((S * g.n_tab + 3) & ~3)) + (threadIdx.x >> 6) * L * V;
+  for (int i = threadIdx.x; i < (2 * L + 1) * V; i += NT) {
+    const int l = i / V, pos = i % V, ln = pos / RM, r = pos % RM, e = ln + WAVE * r;
+    float v = 0.f;
+    if (e < D) v = l < L ? p.cp.w[l][e] : l < 2 * L ? p.cp.b[l - L][e] : p.cp.wf_cross[e];
+    sw[i] = v;
   }
-  for (int i = threadIdx.x; i < D; i += NT) swf[i] = p.cp.wf_cross[i];
   fill_tab_lds(g, tl, p.emb_grad);
   __syncthreads();
 
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   LaneMap<RM> m;
   make_lanes<RM>(g, tl, num, lane, m);
-  float dwa[L > 0 ? L : 1][RM], dba[L > 0 ? L : 1][RM], dwfa[RM];
+  f2v dwa[L > 0 ? L : 1][H2], dba[L > 0 ? L : 1][H2], dwfa[H2];
   float dbf = 0.f;
 #pragma unroll
-  for (int r = 0; r < RM; ++r) {
-    dwfa[r] = 0.f;
+  for (int h = 0; h < H2; ++h) {
+    dwfa[h] = f2v{0.f, 0.f};
 #pragma unroll
-    for (int l = 0; l < L; ++l) { dwa[l][r] = 0.f; dba[l][r] = 0.f; }
+    for (int l = 0; l < L; ++l) { dwa[l][h] = f2v{0.f, 0.f}; dba[l][h] = f2v{0.f, 0.f}; }
   }
   const int64_t ntiles = (B + S - 1) / S;
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
@@ -316,49 +340,53 @@ __global__ __launch_bounds__(NT, 2) void cross_bwd_kernel(GatherDesc g, CrossBwd
       const int64_t b = b0 + s;
       if (b >= B) break;
       float sl[L > 0 ? L : 1];
-      float xc[RM];
+      f2v xc[H2];
 #pragma unroll
-      for (int r = 0; r < RM; ++r) xc[r] = x[u][r];
+      for (int h = 0; h < H2; ++h)   // elements past D are 0 (the images are 0 there too)
+        xc[h] = f2v{m.tab[2 * h] != NO_ELEM ? x[u][2 * h] : 0.f,
+                    m.tab[2 * h + 1] != NO_ELEM ? x[u][2 * h + 1] : 0.f};
 #pragma unroll
       for (int l = 0; l < ((GC_LAB_MODE & 16) ? 0 : L); ++l) {
-        float d = 0.f;
+        lds_store_vec<RM>(xsl + l * V, lane, xc);
+        f2v wv[H2], bv[H2];
+        lds_vec<RM>(sw + l * V, lane, wv);
+        lds_vec<RM>(sb + l * V, lane, bv);
+        f2v d2 = f2v{0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < RM; ++r) {
-          const int e = lane + WAVE * r;
-          xsl[(l * RM + r) * WAVE + lane] = xc[r];
-          if (e < D) d += xc[r] * sw[l * D + e];
-        }
-        sl[l] = wave_sum_dpp(d);
+        for (int h = 0; h < H2; ++h) d2 += xc[h] * wv[h];
+        sl[l] = wave_sum_dpp(d2[0] + d2[1]);
+        const f2v sv = f2v{sl[l], sl[l]};
 #pragma unroll
-        for (int r = 0; r < RM; ++r) {
-          const int e = lane + WAVE * r;
-          xc[r] = e < D ? (xc[r] + xc[r] * sl[l]) + sb[l * D + e] : 0.f;
-        }
+        for (int h = 0; h < H2; ++h) xc[h] = (xc[h] + xc[h] * sv) + bv[h];
       }
       const float dzb = dzv[u];
       dbf += dzb;
-      float gr[RM];
+      const f2v dzv2 = f2v{dzb, dzb};
+      f2v gr[H2];
+      {
+        f2v fv[H2];
+        lds_vec<RM>(swf, lane, fv);
 #pragma unroll
-      for (int r = 0; r < RM; ++r) {
-        const int e = lane + WAVE * r;
-        gr[r] = e < D ? dzb * swf[e] : 0.f;
-        dwfa[r] += dzb * xc[r];
+        for (int h = 0; h < H2; ++h) {
+          gr[h] = dzv2 * fv[h];
+          dwfa[h] += dzv2 * xc[h];
+        }
       }
 #pragma unroll
       for (int l = ((GC_LAB_MODE & 16) ? -1 : L - 1); l >= 0; --l) {
-        float xl[RM];
+        f2v xl[H2], wv[H2];
+        lds_vec<RM>(xsl + l * V, lane, xl);
+        lds_vec<RM>(sw + l * V, lane, wv);
+        f2v d2 = f2v{0.f, 0.f};
 #pragma unroll
-        for (int r = 0; r < RM; ++r) xl[r] = xsl[(l * RM + r) * WAVE + lane];
-        float d = 0.f;
+        for (int h = 0; h < H2; ++h) d2 += gr[h] * xl[h];
+        const float gx = wave_sum_dpp(d2[0] + d2[1]);
+        const f2v gxv = f2v{gx, gx}, s1 = f2v{1.f + sl[l], 1.f + sl[l]};
 #pragma unroll
-        for (int r = 0; r < RM; ++r) d += gr[r] * xl[r];
-        const float gx = wave_sum_dpp(d);
-#pragma unroll
-        for (int r = 0; r < RM; ++r) {
-          const int e = lane + WAVE * r;
-          dba[l][r] += gr[r];
-          dwa[l][r] += gx * xl[r];
-          gr[r] = e < D ? gr[r] * (1.f + sl[l]) + gx * sw[l * D + e] : 0.f;
+        for (int h = 0; h < H2; ++h) {
+          dba[l][h] += gr[h];
+          dwa[l][h] += gxv * xl[h];
+          gr[h] = gr[h] * s1 + gxv * wv[h];
         }
       }
       // dx0 = cross part + deep part -> embedding grads
@@ -366,7 +394,7 @@ __global__ __launch_bounds__(NT, 2) void cross_bwd_kernel(GatherDesc g, CrossBwd
 #pragma unroll
       for (int r = 0; r < RM; ++r) {
         const int t = m.tab[r];
-        const float v = gr[r] + dd[u][r];
+        const float v = gr[r >> 1][r & 1] + dd[u][r];
         if constexpr (!(GC_LAB_MODE & 8))
           if (t >= 0) atomicAdd(tl.grad[t] + (int64_t)ids_s[t] * tl.width[t] + m.col[r], v);
       }
@@ -383,10 +411,10 @@ __global__ __launch_bounds__(NT, 2) void cross_bwd_kernel(GatherDesc g, CrossBwd
         if (e >= D) continue;
 #pragma unroll
         for (int l = 0; l < L; ++l) {
-          red[l * D + e] = (ww ? red[l * D + e] : 0.f) + dwa[l][r];
-          red[(L + l) * D + e] = (ww ? red[(L + l) * D + e] : 0.f) + dba[l][r];
+          red[l * D + e] = (ww ? red[l * D + e] : 0.f) + dwa[l][r >> 1][r & 1];
+          red[(L + l) * D + e] = (ww ? red[(L + l) * D + e] : 0.f) + dba[l][r >> 1][r & 1];
         }
-        red[2 * L * D + e] = (ww ? red[2 * L * D + e] : 0.f) + dwfa[r];
+        red[2 * L * D + e] = (ww ? red[2 * L * D + e] : 0.f) + dwfa[r >> 1][r & 1];
       }
       if (lane == 0) red[(2 * L + 1) * D] = (ww ? red[(2 * L + 1) * D] : 0.f) + dbf;
     }
@@ -472,8 +500,9 @@ dcnr_status launch_bwd(const GatherDesc& g, const CrossBwdParams& p, const int64
                        int64_t B, const float* dx0, int ld_dx, float* part, int64_t nb,
                        hipStream_t s) {
   constexpr int S = BWD_SPW * WPB;
-  size_t lds = (size_t)(2 * (2 * L + 1) * g.D + 1) * sizeof(float) +
-               (size_t)S * g.n_tab * sizeof(int) + (size_t)WPB * (L + 1) * RM * WAVE * sizeof(float);
+  size_t lds = (size_t)((2 * L + 1) * RM * WAVE + (((2 * L + 1) * g.D + 1 + 3) & ~3)) * sizeof(float) +
+               (size_t)((S * g.n_tab + 3) & ~3) * sizeof(int) +
+               (size_t)WPB * (L > 0 ? L : 1) * RM * WAVE * sizeof(float);
   static size_t attr_lds = 0;   // raise the dynamic-LDS limit once per size class
   if (lds > 64 * 1024 && lds > attr_lds) {
     DCNR_HIP(hipFuncSetAttribute((const void*)cross_bwd_kernel<RM, L, BWD_SPW>,
