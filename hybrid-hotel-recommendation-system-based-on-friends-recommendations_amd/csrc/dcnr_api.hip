@@ -411,22 +411,41 @@ bool epi_stats_ok(const Dims& d) {
 }
 
 // t = A W^T + b  and  part = BN column partials of t, shifted by b
-dcnr_status linear_fwd_stats(const Dims& d, const Layout& L, const void* A, int lda,
-                             const void* W, int K, const float* bias, void* out, int64_t B,
-                             int* nc, hipStream_t s) {
+// In-kernel BN finalize (gemm_ws last-arriver) when no SyncBN hook has to see
+// the sums first and the GEMM is one launch.
+bool gemm_final_ok(const dcnr_model_desc* desc, const NtArgs& a, int epi) {
+  // opt-in: the last-arriver tail costs more than the reduce launch it saves
+  // (its fixed-order reduction is a serial chain of dependent loads)
+  static const bool off = getenv("DCNR_GEMM_NT") != nullptr ||
+                          getenv("DCNR_GEMM_FINAL") == nullptr;
+  return !off && !desc->bn_allreduce && gemm_ws_single_launch(a, epi);
+}
+
+// *fin_done = 1 when rf was applied inside the GEMM (else the caller reduces
+// the nc partial rows in L.part)
+dcnr_status linear_fwd_stats(const dcnr_model_desc* desc, const Dims& d, const Layout& L,
+                             const void* A, int lda, const void* W, int K, const float* bias,
+                             void* out, int64_t B, const RedFinal& rf, int* nc, int* fin_done,
+                             hipStream_t s) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
   a.X = (const bf16*)A; a.ldx = lda; a.M = B; a.K = K;
   a.W = (const bf16*)W; a.ldw = K; a.N = d.Hp;
   a.C = out; a.ldc = d.Hp; a.bias = bias;
   a.part = L.part;
+  *fin_done = gemm_final_ok(desc, a, NT_EPI_BIAS_STATS) ? 1 : 0;
+  if (*fin_done) {
+    a.fin = 1; a.fin_shift = 1; a.fin_nr = d.H; a.rf = rf;
+    a.rf.counter = L.red_cnt + RED_MAX_CGRP;
+  }
   return gemm_stream(NT_EPI_BIAS_STATS, a, s, nc);
 }
 
 // C = mask(H) * (X W^T [+ R]) and part = [sum C, sum C*xhat(T)] (BN backward)
-dcnr_status linear_dx_bn(const Dims& d, const Layout& L, int epi, const void* X, const void* Wt,
-                         const void* R, void* C, const void* H, float hscale, const void* T,
-                         const BnBufs& bn, int64_t B, int* nc, hipStream_t s) {
+dcnr_status linear_dx_bn(const dcnr_model_desc* desc, const Dims& d, const Layout& L, int epi,
+                         const void* X, const void* Wt, const void* R, void* C, const void* H,
+                         float hscale, const void* T, const BnBufs& bn, int64_t B,
+                         const RedFinal& rf, int* nc, int* fin_done, hipStream_t s) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
   a.X = (const bf16*)X; a.ldx = d.Hp; a.M = B; a.K = d.Hp;
@@ -437,6 +456,11 @@ dcnr_status linear_dx_bn(const Dims& d, const Layout& L, int epi, const void* X,
   a.T = (const bf16*)T; a.ldt = d.Hp;
   a.mean = bn.mean; a.invstd = bn.invstd;
   a.part = L.part;
+  *fin_done = gemm_final_ok(desc, a, epi) ? 1 : 0;
+  if (*fin_done) {
+    a.fin = 1; a.fin_shift = 0; a.fin_nr = d.H; a.rf = rf;
+    a.rf.counter = L.red_cnt + RED_MAX_CGRP;
+  }
   return gemm_stream(epi, a, s, nc);
 }
 
@@ -507,6 +531,22 @@ RedFinal red_init(const Layout& L, int mode, double count, int accumulate) {
 
 // nc_pre > 0: the partials of t are already in L.part (from the GEMM epilogue),
 // shifted by shiftf (the Linear bias); otherwise a stats pass over t makes them.
+RedFinal bn_fwd_rf(const Layout& L, int64_t B, const float* gamma, const float* beta, float* rm,
+                   float* rv, int64_t* nbt, const BnBufs& bb) {
+  RedFinal rf = red_init(L, RED_BN_FWD, (double)B, 0);
+  rf.f = BnFinal{gamma, beta, rm, rv, nbt, bb.scale, bb.shift, bb.mean, bb.invstd};
+  return rf;
+}
+
+RedFinal bn_bwd_rf(const Layout& L, int64_t B, const float* gamma, const float* invstd,
+                   float* dgamma, float* dbeta, float* dwf, float* dbias_pre, int accumulate) {
+  RedFinal rf = red_init(L, RED_BN_BWD, (double)B, accumulate);
+  rf.gamma = gamma; rf.invstd = invstd; rf.dgamma = dgamma; rf.dbeta = dbeta; rf.dwf = dwf;
+  rf.coef = L.coef;
+  rf.dbias_pre = dbias_pre;
+  return rf;
+}
+
 dcnr_status bn_layer_fwd(const dcnr_model_desc* desc, const Dims& d, const Layout& L,
                          const void* t, int64_t B, bool train, const float* gamma,
                          const float* beta, float* rm, float* rv, int64_t* nbt,
@@ -542,10 +582,7 @@ dcnr_status bn_bwd_reduce(const dcnr_model_desc* desc, const Dims& d, const Layo
                           int accumulate, hipStream_t s) {
   const int Hp = d.Hp, H = d.H;
   if (!desc->bn_allreduce) {
-    RedFinal rf = red_init(L, RED_BN_BWD, (double)B, accumulate);
-    rf.gamma = gamma; rf.invstd = invstd; rf.dgamma = dgamma; rf.dbeta = dbeta; rf.dwf = dwf;
-    rf.coef = L.coef;
-    rf.dbias_pre = dbias_pre;
+    RedFinal rf = bn_bwd_rf(L, B, gamma, invstd, dgamma, dbeta, dwf, dbias_pre, accumulate);
     TRYP(DCNR_K_REDUCE, reduce_fused(DCNR_PREC_FP32, L.part, nc, NK, Hp, H, nullptr, rf, s));
     return DCNR_OK;
   }
@@ -630,24 +667,32 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   for (int j = 0; j < d.R; ++j) {
     const auto& Bk = P.blk[j];
     const bool fuse = train && epi_stats_ok(d);   // BN partials from the GEMM epilogue
-    int nc = 0;
+    int nc = 0, fin = 0;
     if (fuse)
-      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j],
-                                             B, &nc, s));
+      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(desc, d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j],
+                                             L.t1[j], B,
+                                             bn_fwd_rf(L, B, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
+                                                       L.bn[2 * j]),
+                                             &nc, &fin, s));
     else
       TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
-    TRY(bn_layer_fwd(desc, d, L, L.t1[j], B, train, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
-                     L.bn[2 * j], s, nc, fuse ? L.b1p[j] : nullptr));
+    if (!fin)
+      TRY(bn_layer_fwd(desc, d, L, L.t1[j], B, train, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
+                       L.bn[2 * j], s, nc, fuse ? L.b1p[j] : nullptr));
     void* a1 = train ? L.a1s[j] : L.a1;
     TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
                      dropout_seed, j, s));
     if (fuse)
-      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B,
-                                             &nc, s));
+      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(desc, d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j],
+                                             L.t2[j], B,
+                                             bn_fwd_rf(L, B, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
+                                                       L.bn[2 * j + 1]),
+                                             &nc, &fin, s));
     else
       TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
-    TRY(bn_layer_fwd(desc, d, L, L.t2[j], B, train, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
-                     L.bn[2 * j + 1], s, nc, fuse ? L.b2p[j] : nullptr));
+    if (!fin)
+      TRY(bn_layer_fwd(desc, d, L, L.t2[j], B, train, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
+                       L.bn[2 * j + 1], s, nc, fuse ? L.b2p[j] : nullptr));
     const bool head = j == d.R - 1 && bn_add_relu_head_supported(d.prec, d.Hp);
     if (head)   // last block: residual + ReLU + deep head dot + logits in one pass
       TRYP(DCNR_K_ROWWISE, bn_add_relu_head(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
@@ -697,6 +742,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   const bool fuse = epi_stats_ok(d);   // BN partials from the dX GEMM epilogues
   int nc_du = 0;   // > 0: L.du and its BN2 partials were made by the previous dX GEMM
+  int fin_du = 0;  // ... and that GEMM also finalised them (BN2 backward done)
   for (int j = d.R - 1; j >= 0; --j) {
     const auto& Bk = P.blk[j];
     auto& Gk = Gr.blk[j];
@@ -705,8 +751,9 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     int nc = 0;
     // ---- out = relu(BN2(t2) + h_j):  du, BN2 backward
     if (nc_du) {
-      TRY(bn_bwd_reduce(desc, d, L, nc_du, 2, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, nullptr,
-                        Gk.b2, accumulate, s));
+      if (!fin_du)
+        TRY(bn_bwd_reduce(desc, d, L, nc_du, 2, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, nullptr,
+                          Gk.b2, accumulate, s));
     } else {
       TRYP(DCNR_K_ROWWISE, bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean,
                                           bn2.invstd, B, Hp, Hp, L.du, L.part, &nc, s));
@@ -718,12 +765,17 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
                        L.dt2, L.part, &nc, s));
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
     TRY(linear_dw(d, L, L.dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s));
+    int fin1 = 0;
     if (fuse) {
       // dy1 = (dt2 W2) * [a1 != 0] / (1-p): relu and dropout masks from the
-      // saved activation, BN1 partials in the same pass
-      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(d, L, NT_EPI_DROP_BN, L.dt2, L.W2t[j], nullptr, L.da,
+      // saved activation, BN1 partials (and, without SyncBN, its backward
+      // coefficients and dgamma/dbeta) in the same pass
+      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(desc, d, L, NT_EPI_DROP_BN, L.dt2, L.W2t[j], nullptr, L.da,
                                         L.a1s[j], p > 0.f ? 1.f / (1.f - p) : 1.f, L.t1[j], bn1,
-                                        B, &nc, s));
+                                        B,
+                                        bn_bwd_rf(L, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr,
+                                                  Gk.b1, accumulate),
+                                        &nc, &fin1, s));
     } else {
       GemmArgs g;
       memset(&g, 0, sizeof(g));
@@ -734,8 +786,9 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRYP(DCNR_K_ROWWISE, bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean,
                                          bn1.invstd, B, Hp, Hp, p, dropout_seed, j, L.part, &nc, s));
     }
-    TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
-                      accumulate, s));
+    if (!fin1)
+      TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
+                        accumulate, s));
     TRYP(DCNR_K_ROWWISE, bwd_bn1_apply2(d.prec, L.da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, L.a1,
                        L.part, &nc, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
@@ -743,8 +796,13 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     if (fuse && j > 0) {
       // G is only consumed by block j-1's BN2 backward: emit its du = G * [h_j > 0]
       // (in place over this block's du, the residual operand) and the partials
-      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(d, L, NT_EPI_RESID_BN, L.a1, L.W1t[j], L.du, L.du, L.h[j],
-                                        1.f, L.t2[j - 1], L.bn[2 * (j - 1) + 1], B, &nc_du, s));
+      const BnBufs& bp = L.bn[2 * (j - 1) + 1];
+      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(desc, d, L, NT_EPI_RESID_BN, L.a1, L.W1t[j], L.du, L.du,
+                                        L.h[j], 1.f, L.t2[j - 1], bp, B,
+                                        bn_bwd_rf(L, B, P.blk[j - 1].g2, bp.invstd,
+                                                  Gr.blk[j - 1].g2, Gr.blk[j - 1].be2, nullptr,
+                                                  Gr.blk[j - 1].b2, accumulate),
+                                        &nc_du, &fin_du, s));
       Gin = L.du;
     } else {
       GemmArgs g;
@@ -755,6 +813,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRYP(DCNR_K_GEMM_DX, gemm_nn(d.prec, EPI_STORE_RESID, g, 1, s));
       Gin = L.G;
       nc_du = 0;
+      fin_du = 0;
     }
   }
   // ---- initial layer

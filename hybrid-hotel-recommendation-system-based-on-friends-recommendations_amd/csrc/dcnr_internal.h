@@ -215,6 +215,91 @@ struct GemmArgs {
 dcnr_status gemm(int precision, bool a_t, bool b_t, int epi, const GemmArgs& a, int splits,
                  hipStream_t s);
 
+struct BnFinal {   // per BN layer
+  const float* gamma; const float* beta; float* rmean; float* rvar; int64_t* nbt;
+  float* scale; float* shift;   // y = t*scale + shift  (N)
+  float* mean; float* invstd;   // saved for backward
+};
+// N = padded width, Nr = real width (parameters have Nr entries; pads -> 0)
+dcnr_status bn_finalize2(const double* sums, int N, int Nr, int train, const BnFinal& f,
+                         hipStream_t s);
+// Fused reduce + consumer (used when no SyncBN hook must see the sums)
+enum RedMode : int { RED_BN_FWD = 0, RED_BN_BWD = 1, RED_BIAS = 2, RED_SUMS = 3 };
+constexpr int RED_G = 32;          // chunk groups per column group
+constexpr int RED_MAX_CGRP = 64;   // column groups of 64 -> N <= 4096
+constexpr int CNT_SLOTS = 512;     // hand-off counters in the workspace (zeroed by pack_all)
+struct RedFinal {
+  int mode; int accumulate; double count;
+  double* red2;                                // workspace [RED_G][3][N] fp64
+  int* counter;                                // workspace [RED_MAX_CGRP], zero at rest
+  double* sums;                                // RED_SUMS: [3][N] + count
+
+  BnFinal f;                                   // RED_BN_FWD (train)
+  const float* gamma; const float* invstd;     // RED_BN_BWD
+  float* dgamma; float* dbeta; float* dwf; float* coef;
+  float* dbias_pre;                            // Linear bias in front of the BN: grad = 0
+  float* grad;                                 // RED_BIAS
+  const float* shiftf;                         // f32 shift of the stats partials (or null)
+};
+
+
+constexpr float BN_EPS = 1e-5f;
+constexpr double BN_MOM = 0.1;
+
+// Consumer of reduced column sums v0, v1, v2 (fp64) of column n: BN forward
+// statistics (+ running stats), BN backward coefficients and parameter
+// gradients, a bias gradient, or the raw sums for a SyncBN hook.  K (when
+// has_k) is the shift the partials were taken relative to.
+__device__ inline void red_finalize(const RedFinal& rf, int n, int N, int Nr, double v0, double v1,
+                                    double v2, bool has_k, double K) {
+  const double cnt = rf.count;
+  const bool real = n < Nr;
+  if (has_k) {  // unshift
+    v1 = v1 + 2.0 * K * v0 + cnt * K * K;
+    v0 = v0 + cnt * K;
+  }
+  if (rf.mode == RED_SUMS) {  // raw sums for the SyncBN hook (+ count at [3N])
+    rf.sums[n] = v0;
+    rf.sums[N + n] = v1;
+    rf.sums[2 * N + n] = v2;
+    if (n == 0) rf.sums[3 * N] = cnt;
+  } else if (rf.mode == RED_BN_FWD) {
+    const BnFinal& f = rf.f;
+    if (!real) {
+      f.scale[n] = 0.f; f.shift[n] = 0.f; f.mean[n] = 0.f; f.invstd[n] = 0.f;
+      return;
+    }
+    double mean = v0 / cnt;
+    double var = v1 / cnt - mean * mean;
+    if (var < 0) var = 0;
+    f.rmean[n] = (float)((1.0 - BN_MOM) * (double)f.rmean[n] + BN_MOM * mean);
+    f.rvar[n] = (float)((1.0 - BN_MOM) * (double)f.rvar[n] + BN_MOM * var * cnt / (cnt - 1.0));
+    if (n == 0 && f.nbt) f.nbt[0] += 1;
+    float inv = (float)(1.0 / sqrt(var + (double)BN_EPS));
+    float sc = f.gamma[n] * inv;
+    f.scale[n] = sc;
+    f.shift[n] = f.beta[n] - (float)mean * sc;
+    f.mean[n] = (float)mean;
+    f.invstd[n] = inv;
+  } else if (rf.mode == RED_BN_BWD) {
+    // v0 = sum dy, v1 = sum dy*xhat, v2 = sum dz*out (deep half of dW_f)
+    const float a = real ? rf.gamma[n] * rf.invstd[n] : 0.f;
+    rf.coef[n] = a;
+    rf.coef[N + n] = (float)((double)a * v1 / cnt);
+    rf.coef[2 * N + n] = (float)((double)a * v0 / cnt);
+    if (real) {
+      rf.dgamma[n] = rf.accumulate ? rf.dgamma[n] + (float)v1 : (float)v1;
+      rf.dbeta[n] = rf.accumulate ? rf.dbeta[n] + (float)v0 : (float)v0;
+      if (rf.dwf) rf.dwf[n] = rf.accumulate ? rf.dwf[n] + (float)v2 : (float)v2;
+      // the Linear bias in front of a train-mode BatchNorm has an exactly zero
+      // gradient (sum_b dt = gamma*invstd*(sum du - sum du - sum(xhat)*..) = 0)
+      if (rf.dbias_pre && !rf.accumulate) rf.dbias_pre[n] = 0.f;
+    }
+  } else {  // RED_BIAS
+    if (real) rf.grad[n] = rf.accumulate ? rf.grad[n] + (float)v0 : (float)v0;
+  }
+}
+
 // bf16 weight-resident streaming GEMM (gemm_nt.hip): C[M,N] = X[M,K] W[N,K]^T
 enum NtEpi : int {
   NT_EPI_BIAS = 0,    // C bf16 = acc + bias[n] (bias padded to N, may be null)
@@ -237,6 +322,10 @@ struct NtArgs {
   const bf16* T; int64_t ldt;                       // BN input for xhat
   const float* mean; const float* invstd;
   float* part;                                      // column partials (stats epilogues)
+  // gemm_ws only: fin != 0 -> the last workgroup of each column slice reduces
+  // the partials (fp64, fixed order) and runs red_finalize itself (fin_shift:
+  // forward partials are relative to the bias); counters at rf.counter[slice]
+  int fin; int fin_shift; int fin_nr; RedFinal rf;
   int nslices, groups; int64_t mtiles;   // filled by gemm_nt
 };
 bool gemm_nt_supported(int64_t K, int64_t N);
@@ -244,6 +333,8 @@ bool gemm_nt_supported(int64_t K, int64_t N);
 dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
 // the same contract, weight-stationary kernel (gemm_ws.hip)
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
+// whether gemm_ws runs as one launch (a requirement for fin)
+bool gemm_ws_single_launch(const NtArgs& a, int epi);
 inline bool nt_epi_stats(int epi) { return epi >= NT_EPI_BIAS_STATS; }
 
 // bf16 weight-gradient GEMM (gemm_dw.hip): slab[split][n][k] = sum over the
@@ -323,32 +414,6 @@ dcnr_status col_sum(int precision, const void* x, int64_t B, int N, int ld, floa
                     int* nchunks, hipStream_t s);                    // NK=1
 // (col_stats partials are shifted by K = t[0][n]; reduce_fused unshifts them.)
 
-struct BnFinal {   // per BN layer
-  const float* gamma; const float* beta; float* rmean; float* rvar; int64_t* nbt;
-  float* scale; float* shift;   // y = t*scale + shift  (N)
-  float* mean; float* invstd;   // saved for backward
-};
-// N = padded width, Nr = real width (parameters have Nr entries; pads -> 0)
-dcnr_status bn_finalize2(const double* sums, int N, int Nr, int train, const BnFinal& f,
-                         hipStream_t s);
-// Fused reduce + consumer (used when no SyncBN hook must see the sums)
-enum RedMode : int { RED_BN_FWD = 0, RED_BN_BWD = 1, RED_BIAS = 2, RED_SUMS = 3 };
-constexpr int RED_G = 32;          // chunk groups per column group
-constexpr int RED_MAX_CGRP = 64;   // column groups of 64 -> N <= 4096
-constexpr int CNT_SLOTS = 512;     // hand-off counters in the workspace (zeroed by pack_all)
-struct RedFinal {
-  int mode; int accumulate; double count;
-  double* red2;                                // workspace [RED_G][3][N] fp64
-  int* counter;                                // workspace [RED_MAX_CGRP], zero at rest
-  double* sums;                                // RED_SUMS: [3][N] + count
-
-  BnFinal f;                                   // RED_BN_FWD (train)
-  const float* gamma; const float* invstd;     // RED_BN_BWD
-  float* dgamma; float* dbeta; float* dwf; float* coef;
-  float* dbias_pre;                            // Linear bias in front of the BN: grad = 0
-  float* grad;                                 // RED_BIAS
-  const float* shiftf;                         // f32 shift of the stats partials (or null)
-};
 dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, int N, int Nr,
                          const void* shift, const RedFinal& rf, hipStream_t s);
 // coef[3][N] for dt = coef0*dy - coef1*xhat - coef2

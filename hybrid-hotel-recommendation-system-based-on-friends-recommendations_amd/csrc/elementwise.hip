@@ -20,8 +20,6 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int UNROLL = 4;
-constexpr float BN_EPS = 1e-5f;
-constexpr double BN_MOM = 0.1;
 constexpr int TARGET_CHUNKS = 2048;  // 8 blocks/CU in flight for HBM latency hiding
 
 template <typename T> constexpr int VE = 16 / (int)sizeof(T);
@@ -507,55 +505,56 @@ __global__ __launch_bounds__(NT) void reduce_fused_kernel(const float* part, int
   double v0 = ((red[0 * 64 + tx] + red[3 * 64 + tx]) + red[6 * 64 + tx]) + red[9 * 64 + tx];
   double v1 = ((red[1 * 64 + tx] + red[4 * 64 + tx]) + red[7 * 64 + tx]) + red[10 * 64 + tx];
   double v2 = ((red[2 * 64 + tx] + red[5 * 64 + tx]) + red[8 * 64 + tx]) + red[11 * 64 + tx];
-  const double cnt = rf.count;
-  const bool real = n < Nr;
-  if (shift || rf.shiftf) {  // unshift
-    double K = rf.shiftf ? (double)rf.shiftf[n] : (double)(float)shift[n];
-    v1 = v1 + 2.0 * K * v0 + cnt * K * K;
-    v0 = v0 + cnt * K;
-  }
-  if (rf.mode == RED_SUMS) {  // raw sums for the SyncBN hook (+ count at [3N])
-    rf.sums[n] = v0;
-    rf.sums[N + n] = v1;
-    rf.sums[2 * N + n] = v2;
-    if (n == 0) rf.sums[3 * N] = cnt;
-  } else if (rf.mode == RED_BN_FWD) {
-    const BnFinal& f = rf.f;
-    if (!real) {
-      f.scale[n] = 0.f; f.shift[n] = 0.f; f.mean[n] = 0.f; f.invstd[n] = 0.f;
-      return;
-    }
-    double mean = v0 / cnt;
-    double var = v1 / cnt - mean * mean;
-    if (var < 0) var = 0;
-    f.rmean[n] = (float)((1.0 - BN_MOM) * (double)f.rmean[n] + BN_MOM * mean);
-    f.rvar[n] = (float)((1.0 - BN_MOM) * (double)f.rvar[n] + BN_MOM * var * cnt / (cnt - 1.0));
-    if (n == 0 && f.nbt) f.nbt[0] += 1;
-    float inv = (float)(1.0 / sqrt(var + (double)BN_EPS));
-    float sc = f.gamma[n] * inv;
-    f.scale[n] = sc;
-    f.shift[n] = f.beta[n] - (float)mean * sc;
-    f.mean[n] = (float)mean;
-    f.invstd[n] = inv;
-  } else if (rf.mode == RED_BN_BWD) {
-    // v0 = sum dy, v1 = sum dy*xhat, v2 = sum dz*out (deep half of dW_f)
-    const float a = real ? rf.gamma[n] * rf.invstd[n] : 0.f;
-    rf.coef[n] = a;
-    rf.coef[N + n] = (float)((double)a * v1 / cnt);
-    rf.coef[2 * N + n] = (float)((double)a * v0 / cnt);
-    if (real) {
-      rf.dgamma[n] = rf.accumulate ? rf.dgamma[n] + (float)v1 : (float)v1;
-      rf.dbeta[n] = rf.accumulate ? rf.dbeta[n] + (float)v0 : (float)v0;
-      if (rf.dwf) rf.dwf[n] = rf.accumulate ? rf.dwf[n] + (float)v2 : (float)v2;
-      // the Linear bias in front of a train-mode BatchNorm has an exactly zero
-      // gradient (sum_b dt = gamma*invstd*(sum du - sum du - sum(xhat)*..) = 0)
-      if (rf.dbias_pre && !rf.accumulate) rf.dbias_pre[n] = 0.f;
-    }
-  } else {  // RED_BIAS
-    if (real) rf.grad[n] = rf.accumulate ? rf.grad[n] + (float)v0 : (float)v0;
-  }
+  const bool has_k = shift || rf.shiftf;
+  const double K = rf.shiftf ? (double)rf.shiftf[n] : shift ? (double)(float)shift[n] : 0.0;
+  red_finalize(rf, n, N, Nr, v0, v1, v2, has_k, K);
 }
 
+}  // namespace
+
+namespace {
+// Few partial rows (the GEMM epilogues' 64-128): one stage, one launch.
+// Block = 32 columns x 8 row groups; each lane sums its rows (all loads in
+// flight, fp64, fixed order), the 8 groups are combined in fixed order.
+constexpr int SMALL_ROWS = 256;
+template <typename T>
+__global__ __launch_bounds__(NT) void reduce_small_kernel(const float* part, int nchunks, int NK,
+                                                          int N, int Nr, const T* shift,
+                                                          RedFinal rf) {
+  __shared__ double red[8][3][32];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int n = blockIdx.x * 32 + tx;
+  const __amdgpu_buffer_rsrc_t pr = buf_rsrc(part, (int64_t)nchunks * NK * N * 4);
+  constexpr int U = SMALL_ROWS / 8;
+  double s3[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = ty * U + u;
+      const bool ok = n < N && c < nchunks && k < NK;
+      v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, ok ? ((c * NK + k) * N + n) * 4 : OOR, 0, 0));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) s3[k] += (double)v[u];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) red[ty][k][tx] = s3[k];
+  __syncthreads();
+  if (ty != 0 || n >= N) return;
+  double v[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    double t = 0.0;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) t += red[g][k][tx];
+    v[k] = t;
+  }
+  const bool has_k = shift || rf.shiftf;
+  const double K = rf.shiftf ? (double)rf.shiftf[n] : shift ? (double)(float)shift[n] : 0.0;
+  red_finalize(rf, n, N, Nr, v[0], v[1], v[2], has_k, K);
+}
 }  // namespace
 
 dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, int N, int Nr,
@@ -563,6 +562,17 @@ dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, 
   if (N <= 0 || N > 64 * RED_MAX_CGRP || NK < 1 || NK > 3) {
     set_error("reduce: unsupported width %d / components %d", N, NK);
     return DCNR_UNSUPPORTED_SHAPE;
+  }
+  if (nchunks <= SMALL_ROWS) {
+    const dim3 g((unsigned)cdiv(N, 32));
+    if (precision == DCNR_PREC_BF16)
+      hipLaunchKernelGGL(reduce_small_kernel<bf16>, g, dim3(NT), 0, s, part, nchunks, NK, N, Nr,
+                         (const bf16*)shift, rf);
+    else
+      hipLaunchKernelGGL(reduce_small_kernel<float>, g, dim3(NT), 0, s, part, nchunks, NK, N, Nr,
+                         (const float*)shift, rf);
+    DCNR_LAUNCH_CHECK();
+    return DCNR_OK;
   }
   dim3 grid((unsigned)cdiv(N, 64), RED_G);
   if (precision == DCNR_PREC_BF16)

@@ -533,6 +533,10 @@ int gemm_nt_max_parts(int64_t M, int N) {
 
 dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
   if (nparts) *nparts = 0;
+  if (a.fin) {
+    set_error("gemm_nt: no in-kernel finalize (use gemm_ws)");
+    return DCNR_BAD_ARG;
+  }
   if (a.M <= 0 || a.N <= 0) return DCNR_OK;
   const bool ht = epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN;
   if (!gemm_nt_supported(a.K, a.N) || a.ldx % 8 || a.ldw % 8 || a.ldc % 8 ||

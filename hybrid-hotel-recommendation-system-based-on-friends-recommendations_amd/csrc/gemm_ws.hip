@@ -53,7 +53,7 @@ template <int KTP, int TM> struct WsCfg {
   static constexpr int RPD = 1024 / P;                    // rows per DMA wave-instruction
   static constexpr int DPW = TM / RPD / WS_WAVES;         // DMAs per wave per tile
   static constexpr int RB = TM / 16;                      // 16-row blocks per tile
-  static constexpr size_t LDS_BYTES = 2 * (size_t)TILE + 3 * WS_TN * 4;
+  static constexpr size_t LDS_BYTES = 2 * (size_t)TILE + 3 * WS_TN * 4 + 16;   // + hand-off flag
 };
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -355,6 +355,35 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     const int k = (lane >> 2) & 1, cb = (lane >> 3) & 1, r = 2 * (lane & 1) + ((lane >> 1) & 1);
     const int n = nw + cb * 16 + q * 4 + r;
     if (n < a.N) a.part[((int64_t)group * 2 + k) * a.N + n] = x[0];
+    if (a.fin) {
+      // the last workgroup of this column slice to finish sums the slice's
+      // partial rows in fixed group order (fp64) and finalises the columns
+      int* flag = reinterpret_cast<int*>(lds + 2 * C::TILE + 3 * WS_TN * 4);
+      if (last_arriver(a.rf.counter + slice, groups, flag) && tid < WS_TN) {
+        const int nc = n0 + tid;
+        if (nc < a.N) {
+          const float* pp = a.part + nc;
+          double v0 = 0.0, v1 = 0.0;
+          int g2 = 0;
+          for (; g2 + 8 <= groups; g2 += 8) {
+            float u0[8], u1[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+              u0[i] = pp[(int64_t)(g2 + i) * 2 * a.N];
+              u1[i] = pp[((int64_t)(g2 + i) * 2 + 1) * a.N];
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) { v0 += (double)u0[i]; v1 += (double)u1[i]; }
+          }
+          for (; g2 < groups; ++g2) {
+            v0 += (double)pp[(int64_t)g2 * 2 * a.N];
+            v1 += (double)pp[((int64_t)g2 * 2 + 1) * a.N];
+          }
+          red_finalize(a.rf, nc, a.N, a.fin_nr, v0, v1, 0.0, a.fin_shift != 0,
+                       a.fin_shift ? (double)a.bias[nc] : 0.0);
+        }
+      }
+    }
   }
 }
 
@@ -374,6 +403,10 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
                                            a.T ? a.ldt : 0});
   const int64_t mchunk = std::max<int64_t>(WS_TM, ((int64_t(1) << 29) / (maxld * 2)) / WS_TM * WS_TM);
   if (a.M > mchunk) {
+    if (a.fin) {
+      set_error("gemm_ws: in-kernel finalize needs a single launch");
+      return DCNR_UNSUPPORTED_SHAPE;
+    }
     int total = 0;
     for (int64_t m0 = 0; m0 < a.M; m0 += mchunk) {
       NtArgs b = a;
@@ -412,6 +445,14 @@ dcnr_status dispatch_ws(const NtArgs& a, hipStream_t s, int* nparts) {
 }
 
 }  // namespace
+
+bool gemm_ws_single_launch(const NtArgs& a, int epi) {
+  (void)epi;   // (64-row rounding below is conservative for 32-row tiles too)
+  const int64_t maxld = std::max<int64_t>({a.ldx, a.ldc * 2, a.R ? a.ldr : 0, a.H ? a.ldh : 0,
+                                           a.T ? a.ldt : 0});
+  const int64_t mchunk = std::max<int64_t>(64, ((int64_t(1) << 29) / (maxld * 2)) / 64 * 64);
+  return a.M <= mchunk;
+}
 
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
   if (nparts) *nparts = 0;
