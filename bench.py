@@ -47,6 +47,11 @@ GATHER_BYTES = 14 * 8 + 14 * 32 * 4 + 8 * 4 + D * 2 + 4
 # bf16 weights once per launch
 GEMM_FWD_BYTES_PER_SAMPLE = 2 * (D + H) + 2 * R * 2 * (H + H)
 GEMM_FWD_W_BYTES = 2 * (H * D + 2 * R * H * H)
+# BASELINE configs[1] (gather + x0 + 3 cross forward, fp32, B=65536): SURVEY 8d
+# algorithmic bytes per sample = 14 ids x 8 B + 14 rows x 128 B + 8 x 4 B read
+# (1936 B) + the fp32 cross_out row written (456 x 4 = 1824 B)
+CFG2_B = 65536
+CFG2_BYTES = 14 * 8 + 14 * 32 * 4 + 8 * 4 + D * 4
 PEAK_BF16 = 2.5e15     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12
 
@@ -97,6 +102,45 @@ def cpu_baseline(B_cpu=32768, steps=4):
     return {"value": steps * B_cpu / el, "unit": "samples/s", "cores": cores, "kind": "port",
             "sample": f"{steps} train steps (fwd+BCE+bwd+AdamW) at batch {B_cpu} of the same "
                       f"model/tables, numpy fp32 oracle, {el:.1f} s"}
+
+
+def bench_cfg2(model, gen, dev, iters, world):
+    """BASELINE configs[1]: embedding gathers + x0 concat + 3 cross layers,
+    fp32 cross_out [65536, 456], on the bench model's tables
+    (DCN_RecSys.gather_cross -> dcnr_gather_cross).  Per-launch kernel time
+    from HIP events on the launch stream (libdcnr profiling); wall time over
+    `iters` back-to-back calls between synchronisations."""
+    from dcnr import _lib
+    batches = [make_batch(gen, CFG2_B, dev)[:4] for _ in range(4)]
+    out = torch.empty((CFG2_B, D), dtype=torch.float32, device=dev)
+    for k in range(3):
+        model.gather_cross(*batches[k % 4], out=out)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(iters):
+        model.gather_cross(*batches[k % 4], out=out)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    _lib.profile_enable(True)
+    _lib.profile_collect()
+    for k in range(iters):
+        model.gather_cross(*batches[k % 4], out=out)
+    _lib.profile_enable(False)
+    ms, cnt = _lib.profile_collect()["gather_cross"]
+    t_launch = ms / cnt / 1e3
+    achieved = CFG2_BYTES * CFG2_B / t_launch / 1e9
+    return {"workload": "BASELINE configs[1]: embedding gather + x0 + 3-layer cross forward, fp32, "
+                        "1M x 32 / 100k x 32 / 12 x 1000 x 32 tables, 8 dense",
+            "batch": CFG2_B, "dtype": "f32",
+            "pairs_per_sec": world * CFG2_B * iters / wall,
+            "kernel_pairs_per_sec": CFG2_B / t_launch,
+            "roofline": {"bound": "hbm", "kernel": "gather_cross_v4_kernel (dcnr_gather_cross)",
+                         "achieved": achieved, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                         "frac": achieved / (PEAK_HBM / 1e9),
+                         "traffic": pmc_traffic("gather_cross_cfg2"),
+                         "bytes_per_sample": CFG2_BYTES, "avg_launch_ms": ms / cnt}}
 
 
 def pmc_traffic(kernel_class):
@@ -196,6 +240,7 @@ def main():
     if world > 1:
         dist.all_reduce(ev, op=dist.ReduceOp.MAX)
     pairs_per_s = world * B * args.eval_steps / float(ev.item())
+    cfg2 = bench_cfg2(model, gen, dev, max(args.steps, 10), world)
 
     if rank == 0:
         samples = world * B * args.steps
@@ -251,6 +296,7 @@ def main():
                                 "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                                 "frac": gather_gbs / (PEAK_HBM / 1e9),
                                 "bytes_per_sample": GATHER_BYTES, "avg_launch_ms": g_ms / g_cnt},
+            "configs1": cfg2,
             "kernel_ms_per_step": per_step_ms,
             "kernel_launches_per_step": launches,
         }

@@ -630,6 +630,35 @@ dcnr_status dcnr_workspace_size(const dcnr_model_desc* desc, int64_t B, int mode
   return DCNR_OK;
 }
 
+dcnr_status dcnr_gather_cross(const dcnr_model_desc* desc, void* const* params,
+                              const int64_t* user_ids, const int64_t* item_ids,
+                              const int64_t* cat_features, const float* num_features, int64_t B,
+                              float* x0, int64_t ld_x0, float* cross_out, int64_t ld_cross,
+                              int32_t* oob_flag, dcnr_stream_t stream) {
+  Dims d;
+  TRY(make_dims(desc, &d));
+  hipStream_t s = (hipStream_t)stream;
+  if (!params || B < 0 || (B > 0 && (!user_ids || !item_ids)) ||
+      (d.K > 0 && B > 0 && !cat_features) || (desc->n_num > 0 && B > 0 && !num_features)) {
+    set_error("dcnr_gather_cross: null argument");
+    return DCNR_BAD_ARG;
+  }
+  if ((x0 && (ld_x0 < d.D || ld_x0 > INT32_MAX)) ||
+      (cross_out && (ld_cross < d.D || ld_cross > INT32_MAX))) {
+    set_error("dcnr_gather_cross: row stride below D=%d", d.D);
+    return DCNR_BAD_ARG;
+  }
+  if (B == 0 || (!x0 && !cross_out)) return DCNR_OK;
+  Params P = map_params(d, params);
+  GatherDesc g = make_gather(d, P, desc->n_num);
+  CrossParams cp = make_cross(d, P);
+  const GcOut o{cross_out, x0, nullptr, (int)ld_cross, (int)ld_x0};
+  const int check = oob_flag != nullptr;
+  TRYP(DCNR_K_GATHER_CROSS, gather_cross_out(g, cp, user_ids, item_ids, cat_features, num_features,
+                                             B, o, 0, oob_flag, check, s));
+  return DCNR_OK;
+}
+
 dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
                          const int64_t* user_ids, const int64_t* item_ids,
                          const int64_t* cat_features, const float* num_features, int64_t B,
@@ -660,8 +689,11 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   if (check) TRYP(DCNR_K_PACK, fill_zero(L.err, 4, s));
   GatherDesc g = make_gather(d, P, desc->n_num);
   CrossParams cp = make_cross(d, P);
-  TRYP(DCNR_K_GATHER_CROSS, gather_cross_fwd(d.prec, g, cp, user_ids, item_ids, cat_features, num_features, B, L.x0,
-                       d.Dp, L.zc, L.err, check, s));
+  {
+    const GcOut o{nullptr, L.x0, L.zc, 0, d.Dp};
+    TRYP(DCNR_K_GATHER_CROSS, gather_cross_out(g, cp, user_ids, item_ids, cat_features, num_features,
+                                               B, o, d.prec == DCNR_PREC_BF16, L.err, check, s));
+  }
   TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.x0, d.Dp, L.W0p, d.Dp, L.b0p, L.h[0], B, s));
   const float p = train ? d.dropout : 0.f;
   for (int j = 0; j < d.R; ++j) {

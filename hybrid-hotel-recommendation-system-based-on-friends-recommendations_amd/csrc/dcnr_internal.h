@@ -383,6 +383,18 @@ dcnr_status gather_cross_fwd(int precision, const GatherDesc& g, const CrossPara
                              const float* num, int64_t B, void* x0, int ldx, float* zc,
                              int* err, int check, hipStream_t s);
 
+// 16-byte-lane forward (gather_cross.hip): any subset of x0 (fp32 or bf16),
+// the cross output x_L (fp32, BASELINE configs[1]) and the head partial zc.
+struct GcOut {
+  float* cross;   // [B][ld_cross] fp32 x_L, or null
+  void* x0;       // [B][ld_x0] fp32 or bf16, or null
+  float* zc;      // [B] w_f[H:] . x_L, or null
+  int ld_cross, ld_x0;
+};
+dcnr_status gather_cross_out(const GatherDesc& g, const CrossParams& cp, const int64_t* user,
+                             const int64_t* item, const int64_t* cat, const float* num, int64_t B,
+                             const GcOut& o, int x0_bf16, int* err, int check, hipStream_t s);
+
 struct CrossBwdParams {
   CrossParams cp;
   float* dw[8]; float* db[8];      // grads (final)

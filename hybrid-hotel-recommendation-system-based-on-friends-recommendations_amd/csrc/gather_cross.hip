@@ -138,7 +138,7 @@ __global__ __launch_bounds__(NT) void gather_cross_fwd_kernel(GatherDesc g, Cros
                                                                const int64_t* cat,
                                                                const float* num, int64_t B, T* x0,
                                                                int ldx, float* zc, int* err,
-                                                               int check) {
+                                                               int check, float* cross, int ldc) {
   constexpr int S = SPW * WPB;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   __shared__ TabLds tl;
@@ -183,6 +183,7 @@ __global__ __launch_bounds__(NT) void gather_cross_fwd_kernel(GatherDesc g, Cros
 #pragma unroll
     for (int u = 0; u < SPW; ++u) {
       const int64_t b = b0 + w * SPW + u;
+      if (x0 == nullptr) continue;
       if constexpr (!(GC_LAB_MODE & 1)) {
         if constexpr (sizeof(T) == 2) {
 #pragma unroll
@@ -230,6 +231,18 @@ __global__ __launch_bounds__(NT) void gather_cross_fwd_kernel(GatherDesc g, Cros
           }
       }
     }
+    if (cross) {
+#pragma unroll
+      for (int u = 0; u < SPW; ++u) {
+        const int64_t b = b0 + w * SPW + u;
+#pragma unroll
+        for (int r = 0; r < RM; ++r) {
+          const int e = lane + WAVE * r;
+          if (b < B && e < ldc) cross[b * ldc + e] = x[u][r];
+        }
+      }
+    }
+    if (!zc) continue;
     float z[SPW];
 #pragma unroll
     for (int u = 0; u < SPW; ++u) {
@@ -246,6 +259,206 @@ __global__ __launch_bounds__(NT) void gather_cross_fwd_kernel(GatherDesc g, Cros
       const int64_t b = b0 + w * SPW + lane;
       const float zv = lane == 0 ? zs[0] : lane == 1 ? zs[1] : lane == 2 ? zs[2] : zs[3];
       if (b < B) zc[b] = zv;
+    }
+  }
+}
+
+// ------------------------------------------------ forward, 16-byte lanes
+// Fast path when every table width, n_num and D are multiples of 4 (cfg2/cfg3:
+// 32-wide tables, 8 dense features, D = 456): lane l of a wave owns the float4
+// chunk c = l + 64 r (elements 4c..4c+3) of a sample row, r < R4, so a 32-wide
+// table row is 8 lanes x 16 B and the whole x0 row of 456 floats is R4 = 2
+// dwordx4 gathers.  Each wave owns SPW consecutive samples per tile.  It loads
+// their row ids itself, one int64 per lane, coalesced (lane j: sample j / n_tab,
+// table j % n_tab).  ds_bpermute hands each lane the id of its table.  No block
+// barrier is taken inside the loop, and the next tile's ids are loaded before
+// this tile's rows are consumed (one-tile software pipeline).
+typedef __attribute__((ext_vector_type(4))) float v4f;
+
+__device__ __forceinline__ float dot4(v4f a, v4f b) {
+  return ((a[0] * b[0] + a[1] * b[1]) + a[2] * b[2]) + a[3] * b[3];
+}
+
+template <int IDR>
+__device__ __forceinline__ int lane_id_of(const int (&idr)[IDR], int src) {
+  const int v0 = __builtin_amdgcn_ds_bpermute((src & 63) << 2, idr[0]);
+  if constexpr (IDR == 1) return v0;
+  else {
+    const int v1 = __builtin_amdgcn_ds_bpermute((src & 63) << 2, idr[1]);
+    return src < 64 ? v0 : v1;
+  }
+}
+
+template <int R4, int SPW, int IDR, int X0BF16>
+__global__ __launch_bounds__(NT) void gather_cross_v4_kernel(GatherDesc g, CrossParams cp,
+                                                             const int64_t* user,
+                                                             const int64_t* item,
+                                                             const int64_t* cat, const float* num,
+                                                             int64_t B, GcOut out, int* err,
+                                                             int check) {
+  static_assert(SPW % 4 == 0, "dot products are reduced 4 samples at a time");
+  constexpr int C = R4 * WAVE;       // float4 chunks per image
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ TabLds tl;
+  const int D = g.D, L = cp.L, nt = g.n_tab;
+  v4f* sw = reinterpret_cast<v4f*>(smem);   // [L][C]  w_l chunks (0 past D)
+  v4f* sb = sw + L * C;                     // [L][C]  b_l
+  v4f* swf = sb + L * C;                    // [C]     w_f[H:]
+  for (int i = threadIdx.x; i < (2 * L + 1) * C * 4; i += NT) {
+    const int l = i / (C * 4), e = i % (C * 4);
+    float v = 0.f;
+    if (e < D) v = l < L ? cp.w[l][e] : l < 2 * L ? cp.b[l - L][e] : cp.wf_cross[e];
+    smem[i] = v;
+  }
+  fill_tab_lds(g, tl, nullptr);
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  // chunk map of this lane
+  const float* base[R4];
+  int stride[R4], tab[R4];
+#pragma unroll
+  for (int r = 0; r < R4; ++r) {
+    const int e = 4 * (lane + WAVE * r);
+    int t = NO_ELEM, col = 0;
+    if (e < D) {
+      t = NUM_TAB;
+      col = e - (D - g.n_num);
+      for (int q = 0; q < nt; ++q)
+        if (e >= tl.off[q] && e < tl.off[q] + tl.width[q]) { t = q; col = e - tl.off[q]; }
+    }
+    tab[r] = t;
+    base[r] = t >= 0 ? tl.tab[t] + col : (t == NUM_TAB ? num + col : tl.tab[0]);
+    stride[r] = t >= 0 ? tl.width[t] : (t == NUM_TAB ? g.n_num : 0);
+  }
+  // id map of this lane: id slot j = lane + 64 q -> (sample j / nt, table j % nt)
+  int ju[IDR], jt[IDR];
+  int64_t jrows[IDR];
+#pragma unroll
+  for (int q = 0; q < IDR; ++q) {
+    const int j = lane + WAVE * q;
+    ju[q] = j / nt;
+    jt[q] = j % nt;
+    jrows[q] = tl.rows[jt[q]];
+  }
+  auto load_ids = [&](int64_t b0, int (&idr)[IDR]) {
+#pragma unroll
+    for (int q = 0; q < IDR; ++q) {
+      const int64_t b = b0 + ju[q];
+      const bool ok = ju[q] < SPW && b < B;
+      const int t = jt[q];
+      const int64_t bc = ok ? b : 0;
+      const int64_t* src = t == 0 ? user + bc : t == 1 ? item + bc : cat + bc * (nt - 2) + (t - 2);
+      int64_t raw = ok ? *src : 0;
+      if (raw < 0 || raw >= jrows[q]) {
+        if (check && err) atomicOr(err, 1);
+        raw = raw < 0 ? 0 : jrows[q] - 1;
+      }
+      idr[q] = (int)raw;
+    }
+  };
+
+  const int64_t ntiles = (B + SPW - 1) / SPW;
+  const int64_t wave_id = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  const int64_t n_waves = (int64_t)gridDim.x * WPB;
+  int idc[IDR];
+  if (wave_id < ntiles) load_ids(wave_id * SPW, idc);
+  for (int64_t tile = wave_id; tile < ntiles; tile += n_waves) {
+    const int64_t b0 = tile * SPW;
+    v4f x[SPW][R4];
+#pragma unroll
+    for (int u = 0; u < SPW; ++u) {
+      const int64_t bc = b0 + u < B ? b0 + u : B - 1;
+#pragma unroll
+      for (int r = 0; r < R4; ++r) {
+        const int t = tab[r];
+        const int id = lane_id_of<IDR>(idc, u * nt + (t >= 0 ? t : 0));
+        const int64_t row = t >= 0 ? (int64_t)id : (t == NUM_TAB ? bc : 0);
+        x[u][r] = *reinterpret_cast<const v4f*>(base[r] + row * stride[r]);
+      }
+    }
+    if (tile + n_waves < ntiles) load_ids((tile + n_waves) * SPW, idc);
+#pragma unroll
+    for (int u = 0; u < SPW; ++u)
+#pragma unroll
+      for (int r = 0; r < R4; ++r)
+        if (tab[r] == NO_ELEM) x[u][r] = v4f{0.f, 0.f, 0.f, 0.f};
+    // x0 (A operand of the initial Linear), pad columns 0
+    if (out.x0) {
+#pragma unroll
+      for (int u = 0; u < SPW; ++u) {
+        const int64_t b = b0 + u;
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+          const int e = 4 * (lane + WAVE * r);
+          if (b < B && e < out.ld_x0) {
+            if constexpr (X0BF16) {
+              bf16x4 h = {(bf16)x[u][r][0], (bf16)x[u][r][1], (bf16)x[u][r][2], (bf16)x[u][r][3]};
+              *reinterpret_cast<bf16x4*>(static_cast<bf16*>(out.x0) + b * out.ld_x0 + e) = h;
+            } else {
+              *reinterpret_cast<v4f*>(static_cast<float*>(out.x0) + b * out.ld_x0 + e) = x[u][r];
+            }
+          }
+        }
+      }
+    }
+    // cross stack (CrossLayer, train.py:96-99): x <- (x + x*(x.w)) + b
+    for (int l = 0; l < L; ++l) {
+      v4f wv[R4], bv[R4];
+#pragma unroll
+      for (int r = 0; r < R4; ++r) {
+        wv[r] = sw[l * C + lane + WAVE * r];
+        bv[r] = sb[l * C + lane + WAVE * r];
+      }
+#pragma unroll
+      for (int u0 = 0; u0 < SPW; u0 += 4) {
+        float d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          d[k] = 0.f;
+#pragma unroll
+          for (int r = 0; r < R4; ++r) d[k] += dot4(x[u0 + k][r], wv[r]);
+        }
+        float s[4];
+        wave_sum4(d[0], d[1], d[2], d[3], s[0], s[1], s[2], s[3]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int r = 0; r < R4; ++r) x[u0 + k][r] = (x[u0 + k][r] + x[u0 + k][r] * s[k]) + bv[r];
+      }
+    }
+    if (out.cross) {
+#pragma unroll
+      for (int u = 0; u < SPW; ++u) {
+        const int64_t b = b0 + u;
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+          const int e = 4 * (lane + WAVE * r);
+          if (b < B && e < out.ld_cross)
+            __builtin_nontemporal_store(x[u][r], reinterpret_cast<v4f*>(out.cross + b * out.ld_cross + e));
+        }
+      }
+    }
+    if (out.zc) {
+      v4f fv[R4];
+#pragma unroll
+      for (int r = 0; r < R4; ++r) fv[r] = swf[lane + WAVE * r];
+#pragma unroll
+      for (int u0 = 0; u0 < SPW; u0 += 4) {
+        float z[4], zs[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          z[k] = 0.f;
+#pragma unroll
+          for (int r = 0; r < R4; ++r) z[k] += dot4(x[u0 + k][r], fv[r]);
+        }
+        wave_sum4(z[0], z[1], z[2], z[3], zs[0], zs[1], zs[2], zs[3]);
+        if (lane < 4) {
+          const int64_t b = b0 + u0 + lane;
+          const float zv = lane == 0 ? zs[0] : lane == 1 ? zs[1] : lane == 2 ? zs[2] : zs[3];
+          if (b < B) out.zc[b] = zv;
+        }
+      }
     }
   }
 }
@@ -483,15 +696,57 @@ constexpr int BWD_SPW = 1;   // (backward: 2 waves/SIMD need the registers)
 template <typename T, int RM>
 dcnr_status launch_fwd(const GatherDesc& g, const CrossParams& cp, const int64_t* user,
                        const int64_t* item, const int64_t* cat, const float* num, int64_t B,
-                       void* x0, int ldx, float* zc, int* err, int check, hipStream_t s) {
+                       void* x0, int ldx, float* zc, int* err, int check, hipStream_t s,
+                       float* cross = nullptr, int ldc = 0) {
   constexpr int S = FWD_SPW * WPB;
   size_t lds = (size_t)(((2 * cp.L + 1) * g.D + S * g.n_tab + 3) & ~3) * sizeof(float) +
                (size_t)WPB * RM * WAVE * sizeof(bf16);
   int64_t blocks = std::min<int64_t>(cdiv(B, S), 256 * 8);
   hipLaunchKernelGGL((gather_cross_fwd_kernel<T, RM, FWD_SPW>), dim3((unsigned)blocks), dim3(NT),
-                     lds, s, g, cp, user, item, cat, num, B, (T*)x0, ldx, zc, err, check);
+                     lds, s, g, cp, user, item, cat, num, B, (T*)x0, ldx, zc, err, check, cross, ldc);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
+}
+
+#ifndef GC_V4_SPW
+#define GC_V4_SPW 4
+#endif
+#ifndef GC_V4_WAVES
+#define GC_V4_WAVES 3072
+#endif
+
+template <int R4, int X0BF16>
+dcnr_status launch_v4(const GatherDesc& g, const CrossParams& cp, const int64_t* user,
+                      const int64_t* item, const int64_t* cat, const float* num, int64_t B,
+                      const GcOut& o, int* err, int check, hipStream_t s) {
+  constexpr int SPW = GC_V4_SPW;
+  const size_t lds = (size_t)(2 * cp.L + 1) * R4 * WAVE * 16;
+  // about GC_V4_WAVES waves (measured best: ~3 per SIMD resident at once),
+  // every wave taking the same number of tiles
+  const int64_t ntiles = cdiv(B, SPW);
+  const int64_t waves = cdiv(ntiles, cdiv(ntiles, GC_V4_WAVES));
+  const unsigned blocks = (unsigned)cdiv(waves, WPB);
+  if (SPW * g.n_tab <= 64)
+    hipLaunchKernelGGL((gather_cross_v4_kernel<R4, SPW, 1, X0BF16>), dim3(blocks), dim3(NT), lds, s,
+                       g, cp, user, item, cat, num, B, o, err, check);
+  else
+    hipLaunchKernelGGL((gather_cross_v4_kernel<R4, SPW, 2, X0BF16>), dim3(blocks), dim3(NT), lds, s,
+                       g, cp, user, item, cat, num, B, o, err, check);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+// The 16-byte-lane kernel applies: widths, n_num, offsets 4-aligned, every
+// pointer 16-B aligned, D <= 512, and the id map fits two registers.
+bool v4_ok(const GatherDesc& g, const float* num, const GcOut& o) {
+  auto al = [](const void* p) { return ((uintptr_t)p & 15) == 0; };
+  if (g.D > 2 * 4 * WAVE || g.n_num % 4 || g.n_tab * GC_V4_SPW > 128) return false;
+  if (g.n_num && !al(num)) return false;
+  for (int t = 0; t < g.n_tab; ++t)
+    if (g.width[t] % 4 || g.off[t] % 4 || !al(g.tab[t])) return false;
+  if (o.cross && (o.ld_cross % 4 || !al(o.cross))) return false;
+  if (o.x0 && (o.ld_x0 % 4 || !al(o.x0))) return false;
+  return true;
 }
 
 template <int RM, int L>
@@ -553,6 +808,40 @@ dcnr_status gather_cross_fwd(int precision, const GatherDesc& g, const CrossPara
                  : launch_fwd<bf16, 16>(g, cp, user, item, cat, num, B, x0, ldx, zc, err, check, s);
   return small ? launch_fwd<float, 8>(g, cp, user, item, cat, num, B, x0, ldx, zc, err, check, s)
                : launch_fwd<float, 16>(g, cp, user, item, cat, num, B, x0, ldx, zc, err, check, s);
+}
+
+dcnr_status gather_cross_out(const GatherDesc& g, const CrossParams& cp, const int64_t* user,
+                             const int64_t* item, const int64_t* cat, const float* num, int64_t B,
+                             const GcOut& o, int x0_bf16, int* err, int check, hipStream_t s) {
+  if (B <= 0) return DCNR_OK;
+  if (cp.L > 8 || g.n_tab > MAX_TABLES) {
+    set_error("gather: unsupported n_cross=%d / tables=%d", cp.L, g.n_tab);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  if (!v4_ok(g, num, o)) {   // the general (4-byte lane) kernel
+    if (g.D > 16 * WAVE || (o.x0 && o.ld_x0 > 16 * WAVE) || (o.cross && o.ld_cross > 16 * WAVE)) {
+      set_error("gather: unsupported D=%d", g.D);
+      return DCNR_UNSUPPORTED_SHAPE;
+    }
+    const bool small = g.D <= 8 * WAVE && (!o.x0 || o.ld_x0 <= 8 * WAVE) &&
+                       (!o.cross || o.ld_cross <= 8 * WAVE);
+    if (x0_bf16)
+      return small ? launch_fwd<bf16, 8>(g, cp, user, item, cat, num, B, o.x0, o.ld_x0, o.zc, err,
+                                         check, s, o.cross, o.ld_cross)
+                   : launch_fwd<bf16, 16>(g, cp, user, item, cat, num, B, o.x0, o.ld_x0, o.zc,
+                                          err, check, s, o.cross, o.ld_cross);
+    return small ? launch_fwd<float, 8>(g, cp, user, item, cat, num, B, o.x0, o.ld_x0, o.zc, err,
+                                        check, s, o.cross, o.ld_cross)
+                 : launch_fwd<float, 16>(g, cp, user, item, cat, num, B, o.x0, o.ld_x0, o.zc, err,
+                                         check, s, o.cross, o.ld_cross);
+  }
+  const bool r1 = g.D <= 4 * WAVE && (!o.x0 || o.ld_x0 <= 4 * WAVE) &&
+                  (!o.cross || o.ld_cross <= 4 * WAVE);
+  if (x0_bf16)
+    return r1 ? launch_v4<1, 1>(g, cp, user, item, cat, num, B, o, err, check, s)
+              : launch_v4<2, 1>(g, cp, user, item, cat, num, B, o, err, check, s);
+  return r1 ? launch_v4<1, 0>(g, cp, user, item, cat, num, B, o, err, check, s)
+            : launch_v4<2, 0>(g, cp, user, item, cat, num, B, o, err, check, s);
 }
 
 dcnr_status cross_bwd_scatter(const GatherDesc& g, const CrossBwdParams& p, const int64_t* user,

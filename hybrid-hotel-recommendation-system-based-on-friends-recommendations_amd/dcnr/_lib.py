@@ -56,6 +56,8 @@ _SIGS = {
                                            ctypes.POINTER(ctypes.c_size_t)]),
     "dcnr_forward": (ctypes.c_int, [ctypes.POINTER(ModelDesc), _P, _P, _P, _P, _P, _I64,
                                     ctypes.c_int, ctypes.c_uint64, _P, _P, ctypes.c_size_t, _P]),
+    "dcnr_gather_cross": (ctypes.c_int, [ctypes.POINTER(ModelDesc), _P, _P, _P, _P, _P, _I64, _P,
+                                         _I64, _P, _I64, _P, _P]),
     "dcnr_backward": (ctypes.c_int, [ctypes.POINTER(ModelDesc), _P, _P, _P, _P, _P, _P, _I64, _P,
                                      ctypes.c_uint64, ctypes.c_int, _P, ctypes.c_size_t, _P]),
     "dcnr_bce_workspace_size": (ctypes.c_size_t, []),

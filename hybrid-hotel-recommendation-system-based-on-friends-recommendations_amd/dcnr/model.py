@@ -175,6 +175,44 @@ class DCN_RecSys(nn.Module):
                                     num_features)
         return logits.squeeze()
 
+    @torch.no_grad()
+    def gather_cross(self, user_ids, item_ids, cat_features, num_features, return_x0=False,
+                     out=None):
+        """The front of ``forward`` on its own (train.py:156-159, 166-168):
+        ``x0 = torch.cat([user_emb, item_emb, *cat_embs, num_features], 1)``
+        and ``cross_out`` after the cross network, both fp32 [B, D] (BASELINE
+        configs[1]; dcnr_gather_cross).  Returns ``cross_out`` or
+        ``(x0, cross_out)``.  ``out``: optional preallocated cross_out.
+        With ``check_indices`` an out-of-range id raises IndexError."""
+        dev = self._check_device(user_ids, item_ids, cat_features, num_features)
+        user_ids = user_ids.reshape(-1).to(torch.int64).contiguous()
+        item_ids = item_ids.reshape(-1).to(torch.int64).contiguous()
+        B = user_ids.shape[0]
+        K, F, D = len(self._dims['cat_dims']), self._dims['n_num'], self._dims['input_dim']
+        if cat_features.numel() != B * K or num_features.numel() != B * F or \
+                item_ids.shape[0] != B:
+            raise RuntimeError("input shapes do not match the model")
+        cat_features = cat_features.to(torch.int64).reshape(B, K).contiguous()
+        num_features = num_features.to(torch.float32).reshape(B, F).contiguous()
+        cross = out if out is not None else torch.empty((B, D), dtype=torch.float32, device=dev)
+        if cross.shape != (B, D) or cross.dtype != torch.float32 or not cross.is_contiguous():
+            raise ValueError("out must be a contiguous fp32 [B, D] tensor")
+        x0 = torch.empty((B, D), dtype=torch.float32, device=dev) if return_x0 else None
+        flag = torch.zeros(1, dtype=torch.int32, device=dev) if self.check_indices else None
+        lib = _lib.load()
+        desc = self.desc()
+        _lib.check(lib.dcnr_gather_cross(ctypes.byref(desc), _lib.ptr_array(self.state_tensors()),
+                                         user_ids.data_ptr(), item_ids.data_ptr(),
+                                         cat_features.data_ptr() if cat_features.numel() else None,
+                                         num_features.data_ptr() if num_features.numel() else None,
+                                         B, x0.data_ptr() if x0 is not None else None, D,
+                                         cross.data_ptr(), D,
+                                         flag.data_ptr() if flag is not None else None,
+                                         _lib.stream_ptr(dev)), "dcnr_gather_cross")
+        if flag is not None and int(flag.item()) != 0:
+            raise IndexError("index out of range in self")
+        return (x0, cross) if return_x0 else cross
+
     # ----------------------------------------------------------- flat storage
     def flatten_(self):
         """Move every parameter into one contiguous fp32 buffer (views keep the

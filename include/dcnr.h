@@ -10,6 +10,9 @@
  *   dcnr_forward          DCN_RecSys.forward            train.py:155-170 (dup main.py:114-127)
  *                         incl. ResBlock.forward          train.py:112-122
  *                         and CrossLayer.forward          train.py:96-99
+ *   dcnr_gather_cross     the front of DCN_RecSys.forward: embedding gathers,
+ *                         x0 concat and the cross network   train.py:156-159,166-168
+ *                         (BASELINE configs[1])
  *   dcnr_backward         loss.backward() through the model   train.py:225
  *   dcnr_bce_with_logits  nn.BCEWithLogitsLoss()(preds, y)    train.py:206,224,233,376
  *   dcnr_adam_step        torch.optim.AdamW/Adam(...).step()  train.py:201-204,226
@@ -120,6 +123,21 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
                          const float* num_features /* [B,n_num] */, int64_t B, int mode,
                          uint64_t dropout_seed, float* logits, void* ws, size_t ws_bytes,
                          dcnr_stream_t stream);
+
+/* The embedding gathers, x0 concat and cross network of DCN_RecSys.forward
+ * on their own (train.py:156-159 and 166-168), fp32:
+ *   x0[b]        = [U[u_b] | I[i_b] | C_0[c_b0] .. C_{K-1}[c_b,K-1] | num_b]   (bit-exact copy)
+ *   cross_out[b] = x_L,  x_{l+1} = x_l + x_l * (x_l . w_l) + b_l     (CrossLayer, train.py:96-99)
+ * x0 [B][ld_x0] and cross_out [B][ld_cross] are fp32 device buffers (either
+ * may be NULL; ld >= D).  params as for dcnr_forward (only the embedding
+ * tables and cross_network.* are read).  oob_flag: optional device int32 that
+ * is set nonzero when an id is out of range (ids are clamped in-kernel).
+ * Stateless and re-entrant. */
+dcnr_status dcnr_gather_cross(const dcnr_model_desc* desc, void* const* params,
+                              const int64_t* user_ids, const int64_t* item_ids,
+                              const int64_t* cat_features, const float* num_features, int64_t B,
+                              float* x0, int64_t ld_x0, float* cross_out, int64_t ld_cross,
+                              int32_t* oob_flag, dcnr_stream_t stream);
 
 /* Backward of the last train-mode dcnr_forward on `ws`: given dL/dlogits
  * [B], writes dL/dparam for every parameter into `grads`.  accumulate = 0

@@ -1,0 +1,145 @@
+// Kernel lab for the 16-byte-lane gather/cross forward (gather_cross_v4_kernel):
+//   1. BASELINE configs[1]: B=65536, fp32 cross_out [B][456] (+ optional fp32 x0)
+//   2. configs[2] forward gather: B=131072, bf16 x0 + zc, against the 4-byte-lane
+//      kernel (timing and bit-equality of x0 / zc)
+// Build variants with -DGC_V4_SPW=.. -DGC_V4_WAVES=.. (tools/gather4_lab.sh).
+#include "../hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd/csrc/gather_cross.hip"
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+
+namespace dcnr {
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfprintf(stderr, fmt, ap);
+  va_end(ap);
+  fprintf(stderr, "\n");
+}
+}  // namespace dcnr
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+template <typename F>
+static double time_us(F f, int iters) {
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+  for (int i = 0; i < 3; ++i) f();
+  (void)hipEventRecord(e0, 0);
+  for (int i = 0; i < iters; ++i) f();
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  return ms * 1e3 / iters;
+}
+
+int main() {
+  const int E = 32, K = 12, F = 8, L = 3;
+  const int64_t rows[14] = {1000000, 100000, 1000, 1000, 1000, 1000, 1000, 1000, 1000, 1000, 1000, 1000, 1000, 1000};
+  std::mt19937_64 rng(0);
+  std::uniform_real_distribution<float> U(-1.f, 1.f);
+  dcnr::GatherDesc g;
+  std::memset(&g, 0, sizeof(g));
+  g.n_tab = 2 + K; g.n_num = F;
+  int off = 0;
+  std::vector<std::vector<float>> htab(14);
+  for (int t = 0; t < g.n_tab; ++t) {
+    htab[t].resize(rows[t] * E);
+    for (auto& v : htab[t]) v = U(rng);
+    float* p; CK(hipMalloc(&p, rows[t] * E * 4));
+    CK(hipMemcpy(p, htab[t].data(), rows[t] * E * 4, hipMemcpyHostToDevice));
+    g.tab[t] = p; g.rows[t] = rows[t]; g.width[t] = E; g.off[t] = off; off += E;
+  }
+  g.D = off + F;
+  const int D = g.D, ldx = (D + 7) / 8 * 8;
+  std::vector<float> hw((2 * L + 1) * D);
+  for (auto& v : hw) v = 0.05f * U(rng);
+  float* wts; CK(hipMalloc(&wts, hw.size() * 4));
+  CK(hipMemcpy(wts, hw.data(), hw.size() * 4, hipMemcpyHostToDevice));
+  dcnr::CrossParams cp;
+  std::memset(&cp, 0, sizeof(cp));
+  cp.L = L;
+  for (int l = 0; l < L; ++l) { cp.w[l] = wts + l * D; cp.b[l] = wts + (L + l) * D; }
+  cp.wf_cross = wts + 2 * L * D;
+
+  const int64_t BMAX = 131072;
+  std::vector<int64_t> hu(BMAX), hi(BMAX), hc(BMAX * K);
+  for (int64_t b = 0; b < BMAX; ++b) { hu[b] = rng() % rows[0]; hi[b] = rng() % rows[1]; }
+  for (auto& c : hc) c = rng() % 1000;
+  std::vector<float> hn(BMAX * F);
+  for (auto& v : hn) v = (U(rng) + 1.f) * 0.5f;
+  int64_t *u, *it, *c; float *num, *zc, *zc2, *cross, *x0f; dcnr::bf16 *x0, *x0b; int* err;
+  CK(hipMalloc(&u, BMAX * 8)); CK(hipMalloc(&it, BMAX * 8)); CK(hipMalloc(&c, BMAX * K * 8));
+  CK(hipMalloc(&num, BMAX * F * 4)); CK(hipMalloc(&zc, BMAX * 4)); CK(hipMalloc(&zc2, BMAX * 4));
+  CK(hipMalloc(&x0, BMAX * ldx * 2)); CK(hipMalloc(&x0b, BMAX * ldx * 2));
+  CK(hipMalloc(&cross, BMAX * D * 4)); CK(hipMalloc(&x0f, BMAX * D * 4));
+  CK(hipMalloc(&err, 4)); CK(hipMemset(err, 0, 4));
+  CK(hipMemcpy(u, hu.data(), BMAX * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(it, hi.data(), BMAX * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(c, hc.data(), BMAX * K * 8, hipMemcpyHostToDevice));
+  CK(hipMemcpy(num, hn.data(), BMAX * F * 4, hipMemcpyHostToDevice));
+
+  // ---- 1. configs[1]: cross_out fp32 at B=65536
+  {
+    const int64_t B = 65536;
+    dcnr::GcOut o{cross, nullptr, nullptr, D, 0};
+    double us = time_us([&] { dcnr::gather_cross_out(g, cp, u, it, c, num, B, o, 0, err, 0, 0); }, 50);
+    const double alg = 3760.0 * B;   // 1936 B read + 1824 B write per sample
+    printf("cfg2 cross_out     B=%ld  %7.1f us  %6.0f GB/s algorithmic (%.1f%% of 8 TB/s)\n",
+           (long)B, us, alg / us / 1e3, alg / us / 1e3 / 80.0);
+    dcnr::GcOut o2{cross, x0f, nullptr, D, D};
+    us = time_us([&] { dcnr::gather_cross_out(g, cp, u, it, c, num, B, o2, 0, err, 0, 0); }, 50);
+    printf("cfg2 cross_out+x0  B=%ld  %7.1f us\n", (long)B, us);
+    // host check of 64 sampled rows (x0 bit-exact, cross to 1e-5 rel)
+    std::vector<float> hx(B * D), hxc(B * D);
+    CK(hipMemcpy(hx.data(), x0f, B * D * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hxc.data(), cross, B * D * 4, hipMemcpyDeviceToHost));
+    double worst = 0; long bad_x0 = 0;
+    for (int s = 0; s < 64; ++s) {
+      const int64_t b = (s * 1031) % B;
+      std::vector<double> x(D);
+      for (int t = 0; t < 14; ++t) {
+        const int64_t id = t == 0 ? hu[b] : t == 1 ? hi[b] : hc[b * K + t - 2];
+        for (int k = 0; k < E; ++k) x[t * E + k] = htab[t][id * E + k];
+      }
+      for (int k = 0; k < F; ++k) x[14 * E + k] = hn[b * F + k];
+      for (int e = 0; e < D; ++e) bad_x0 += (float)x[e] != hx[b * D + e];
+      for (int l = 0; l < L; ++l) {
+        double sdot = 0;
+        for (int e = 0; e < D; ++e) sdot += x[e] * hw[l * D + e];
+        for (int e = 0; e < D; ++e) x[e] = x[e] + x[e] * sdot + hw[(L + l) * D + e];
+      }
+      for (int e = 0; e < D; ++e)
+        worst = std::max(worst, std::fabs(x[e] - hxc[b * D + e]) / std::max(1.0, std::fabs(x[e])));
+    }
+    printf("cfg2 check: x0 mismatches %ld, cross max rel err %.2e\n", bad_x0, worst);
+  }
+  // ---- 2. configs[2] forward gather: bf16 x0 + zc, new vs old
+  {
+    const int64_t B = 131072;
+    dcnr::GcOut o{nullptr, x0, zc, 0, ldx};
+    double us_new = time_us([&] { dcnr::gather_cross_out(g, cp, u, it, c, num, B, o, 1, err, 0, 0); }, 30);
+    double us_old = time_us([&] {
+      dcnr::gather_cross_fwd(DCNR_PREC_BF16, g, cp, u, it, c, num, B, x0b, ldx, zc2, err, 0, 0);
+    }, 30);
+    printf("cfg3 x0 bf16 + zc  B=%ld  v4 %7.1f us   old %7.1f us\n", (long)B, us_new, us_old);
+    std::vector<uint16_t> a(B * ldx), bb(B * ldx);
+    std::vector<float> za(B), zb(B);
+    CK(hipMemcpy(a.data(), x0, B * ldx * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(bb.data(), x0b, B * ldx * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(za.data(), zc, B * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(zb.data(), zc2, B * 4, hipMemcpyDeviceToHost));
+    long nx = 0; double zw = 0;
+    for (int64_t i = 0; i < B * ldx; ++i) nx += a[i] != bb[i];
+    for (int64_t i = 0; i < B; ++i) zw = std::max(zw, (double)std::fabs(za[i] - zb[i]) / std::max(1.f, std::fabs(zb[i])));
+    printf("cfg3 check: x0 bf16 mismatches %ld, zc max rel diff %.2e\n", nx, zw);
+  }
+  CK(hipDeviceSynchronize());
+  printf("status %s\n", hipGetErrorString(hipGetLastError()));
+  return 0;
+}

@@ -22,7 +22,8 @@ CLASSES = [
     ("gemm_resid", r"gemm_ws_kernel<16, 2>"),
     ("gemm_f32", r"gemm_ws_kernel<16, 1>"),
     ("gemm_dw", r"gemm_dw_kernel"),
-    ("gather_cross", r"gather_cross_fwd_kernel"),
+    ("gather_cross", r"gather_cross_fwd_kernel|gather_cross_v4_kernel<\d, \d, \d, 1>"),
+    ("gather_cross_cfg2", r"gather_cross_v4_kernel<\d, \d, \d, 0>"),
     ("cross_bwd", r"cross_bwd_kernel"),
     ("adam", r"adam_kernel"),
 ]
