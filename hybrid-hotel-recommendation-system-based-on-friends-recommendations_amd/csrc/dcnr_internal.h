@@ -413,6 +413,7 @@ dcnr_status cross_bwd_scatter(const GatherDesc& g, const CrossBwdParams& p,
                               const float* num, const float* dz, int64_t B,
                               const float* dx0_deep, int ld_dx, const CrossBwdScratch& ws,
                               int accumulate, hipStream_t s);
+
 size_t cross_bwd_part_elems(int D, int L);
 size_t cross_red2_elems(int D, int L);
 int cross_red_groups(int D, int L);

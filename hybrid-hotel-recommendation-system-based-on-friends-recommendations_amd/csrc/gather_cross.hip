@@ -27,6 +27,8 @@
 // pass) cost 285 us against +30 us for the inline atomics at cfg3.
 #include "dcnr_internal.h"
 
+#include <cstring>
+
 // tools/gather_lab.hip rebuilds this file with GC_LAB_MODE bits set to time
 // parts of the kernels in isolation (forward 1: no x0 stores, 2: no cross
 // compute, 4: no row loads; backward 8: no gradient scatter, 16: no cross
@@ -637,6 +639,202 @@ __global__ __launch_bounds__(NT, 2) void cross_bwd_kernel(GatherDesc g, CrossBwd
   for (int i = threadIdx.x; i < stride; i += NT) mp[i] = red[i];
 }
 
+// ----------------------------------------------- backward, 16-byte lanes
+// Same chunk map and wave-owned id pipeline as gather_cross_v4_kernel.  Per
+// tile a wave issues the x0 gathers and dx0_deep row loads of its SPW samples
+// together, then per sample recomputes the cross stack (x_0..x_{L-1} kept in
+// registers), runs its backward, accumulates dw_l / db_l / dw_f / db_f in
+// registers, and scatter-adds dx0 = dx0_cross + dx0_deep into the dense
+// embedding grads (fp32 no-return atomics, 4 per chunk).  Block partials are
+// combined in fixed wave order (deterministic) for cross_reduce_kernel.
+template <int R4, int L, int SPW>
+__global__ __launch_bounds__(NT, 2) void cross_bwd_v4_kernel(GatherDesc g, CrossBwdParams p,
+                                                           const int64_t* user,
+                                                           const int64_t* item,
+                                                           const int64_t* cat, const float* num,
+                                                           const float* dz, int64_t B,
+                                                           const float* dx0_deep, int ld_dx,
+                                                           float* part) {
+  constexpr int C = R4 * WAVE, LL = L > 0 ? L : 1;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ TabLds tl;
+  const int D = g.D, nt = g.n_tab;
+  v4f* sw = reinterpret_cast<v4f*>(smem);   // [L][C]
+  v4f* sb = sw + L * C;                     // [L][C]
+  v4f* swf = sb + L * C;                    // [C]
+  float* red = reinterpret_cast<float*>(swf + C);   // [(2L+1)D+1] block partial
+  // element maps of the dword layout used by the gradient scatter (e < 4C):
+  // egrad[e] = grad row-0 address of element e, estride[e] = its row stride,
+  // etab[e] = table index (-1: not a table element)
+  float** egrad = reinterpret_cast<float**>(red + ((((2 * L + 1) * D + 1) + 3) & ~3));
+  int* estride = reinterpret_cast<int*>(egrad + 4 * C);
+  int* etab = estride + 4 * C;
+  // per-wave dword image of the dx0 row being scattered
+  v4f* wrow = reinterpret_cast<v4f*>(etab + 4 * C) + (threadIdx.x >> 6) * C;
+  for (int i = threadIdx.x; i < (2 * L + 1) * C * 4; i += NT) {
+    const int l = i / (C * 4), e = i % (C * 4);
+    float v = 0.f;
+    if (e < D) v = l < L ? p.cp.w[l][e] : l < 2 * L ? p.cp.b[l - L][e] : p.cp.wf_cross[e];
+    smem[i] = v;
+  }
+  fill_tab_lds(g, tl, p.emb_grad);
+  __syncthreads();
+  for (int e = threadIdx.x; e < 4 * C; e += NT) {
+    int t = -1;
+    for (int q = 0; q < nt; ++q)
+      if (e < D && e >= tl.off[q] && e < tl.off[q] + tl.width[q]) t = q;
+    etab[e] = t;
+    egrad[e] = t >= 0 ? tl.grad[t] + (e - tl.off[t]) : nullptr;
+    estride[e] = t >= 0 ? tl.width[t] : 0;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float* base[R4];
+  int stride[R4], tab[R4];
+#pragma unroll
+  for (int r = 0; r < R4; ++r) {
+    const int e = 4 * (lane + WAVE * r);
+    int t = NO_ELEM, col = 0;
+    if (e < D) {
+      t = NUM_TAB;
+      col = e - (D - g.n_num);
+      for (int q = 0; q < nt; ++q)
+        if (e >= tl.off[q] && e < tl.off[q] + tl.width[q]) { t = q; col = e - tl.off[q]; }
+    }
+    tab[r] = t;
+    base[r] = t >= 0 ? tl.tab[t] + col : (t == NUM_TAB ? num + col : tl.tab[0]);
+    stride[r] = t >= 0 ? tl.width[t] : (t == NUM_TAB ? g.n_num : 0);
+  }
+  const int ju = lane / nt, jt = lane % nt;
+  const int64_t jrows = tl.rows[jt];
+  auto load_ids = [&](int64_t b0) {
+    const int64_t b = b0 + ju;
+    const bool ok = ju < SPW && b < B;
+    const int64_t bc = ok ? b : 0;
+    const int64_t* src = jt == 0 ? user + bc : jt == 1 ? item + bc : cat + bc * (nt - 2) + (jt - 2);
+    int64_t raw = ok ? *src : 0;
+    raw = raw < 0 ? 0 : (raw >= jrows ? jrows - 1 : raw);
+    return (int)raw;
+  };
+
+  v4f dwa[LL][R4], dba[LL][R4], dwfa[R4];
+  float dbf = 0.f;
+#pragma unroll
+  for (int r = 0; r < R4; ++r) {
+    dwfa[r] = v4f{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int l = 0; l < LL; ++l) dwa[l][r] = dba[l][r] = v4f{0.f, 0.f, 0.f, 0.f};
+  }
+  const int64_t ntiles = (B + SPW - 1) / SPW;
+  const int64_t wave_id = (int64_t)blockIdx.x * WPB + w;
+  const int64_t n_waves = (int64_t)gridDim.x * WPB;
+  int idc = wave_id < ntiles ? load_ids(wave_id * SPW) : 0;
+  for (int64_t tile = wave_id; tile < ntiles; tile += n_waves) {
+    const int64_t b0 = tile * SPW;
+    v4f x[SPW][R4], dd[SPW][R4];
+    float dzv[SPW];
+    const int idc_u = idc;   // this tile's ids (idc is refilled with the next tile's below)
+#pragma unroll
+    for (int u = 0; u < SPW; ++u) {
+      const int64_t bc = b0 + u < B ? b0 + u : B - 1;
+#pragma unroll
+      for (int r = 0; r < R4; ++r) {
+        const int t = tab[r];
+        const int id = __builtin_amdgcn_ds_bpermute((u * nt + (t >= 0 ? t : 0)) << 2, idc_u);
+        const int64_t row = t >= 0 ? (int64_t)id : (t == NUM_TAB ? bc : 0);
+        x[u][r] = *reinterpret_cast<const v4f*>(base[r] + row * stride[r]);
+        const int e = 4 * (lane + WAVE * r);
+        dd[u][r] = *reinterpret_cast<const v4f*>(dx0_deep + bc * ld_dx + (e < ld_dx ? e : 0));
+      }
+      dzv[u] = dz[bc];
+    }
+    if (tile + n_waves < ntiles) idc = load_ids((tile + n_waves) * SPW);
+#pragma unroll
+    for (int u = 0; u < SPW; ++u) {
+      if (b0 + u >= B) break;
+      v4f xs[LL][R4], xc[R4];
+      float sl[LL];
+#pragma unroll
+      for (int r = 0; r < R4; ++r)
+        xc[r] = tab[r] == NO_ELEM ? v4f{0.f, 0.f, 0.f, 0.f} : x[u][r];
+#pragma unroll
+      for (int l = 0; l < L; ++l) {
+        float d = 0.f;
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+          xs[l][r] = xc[r];
+          d += dot4(xc[r], sw[l * C + lane + WAVE * r]);
+        }
+        sl[l] = wave_sum_dpp(d);
+#pragma unroll
+        for (int r = 0; r < R4; ++r) xc[r] = (xc[r] + xc[r] * sl[l]) + sb[l * C + lane + WAVE * r];
+      }
+      const float dzb = dzv[u];
+      dbf += dzb;
+      v4f gr[R4];
+#pragma unroll
+      for (int r = 0; r < R4; ++r) {
+        gr[r] = dzb * swf[lane + WAVE * r];
+        dwfa[r] += dzb * xc[r];
+      }
+#pragma unroll
+      for (int l = L - 1; l >= 0; --l) {
+        float d = 0.f;
+#pragma unroll
+        for (int r = 0; r < R4; ++r) d += dot4(gr[r], xs[l][r]);
+        const float gx = wave_sum_dpp(d), s1 = 1.f + sl[l];
+#pragma unroll
+        for (int r = 0; r < R4; ++r) {
+          dba[l][r] += gr[r];
+          dwa[l][r] += gx * xs[l][r];
+          gr[r] = gr[r] * s1 + gx * sw[l * C + lane + WAVE * r];
+        }
+      }
+      // dx0 = cross part + deep part -> dense embedding grads.  The row is
+      // re-laid out through this wave's LDS image into one dword per lane
+      // (element e = lane + 64 q), so each atomic wave-instruction adds two
+      // contiguous 128-B row segments (the full-rate shape for memory-side
+      // float atomics, MI355X_MICROARCH.md "Global float atomics").
+#pragma unroll
+      for (int r = 0; r < R4; ++r) wrow[lane + WAVE * r] = gr[r] + dd[u][r];
+      const float* wf1 = reinterpret_cast<const float*>(wrow);
+#pragma unroll
+      for (int q = 0; q < 4 * R4; ++q) {
+        const int e = lane + WAVE * q;
+        const int t = etab[e];
+        const int id = __builtin_amdgcn_ds_bpermute((u * nt + (t >= 0 ? t : 0)) << 2, idc_u);
+        if (t < 0 || (GC_LAB_MODE & 8)) continue;
+        atomicAdd(egrad[e] + (int64_t)id * estride[e], wf1[e]);
+      }
+    }
+  }
+  // block partial, waves added in fixed order
+  const int stride_p = (2 * L + 1) * D + 1;
+  for (int ww = 0; ww < WPB; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int r = 0; r < R4; ++r) {
+        const int e = 4 * (lane + WAVE * r);
+        if (e >= D) continue;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+#pragma unroll
+          for (int l = 0; l < L; ++l) {
+            red[l * D + e + k] = (ww ? red[l * D + e + k] : 0.f) + dwa[l][r][k];
+            red[(L + l) * D + e + k] = (ww ? red[(L + l) * D + e + k] : 0.f) + dba[l][r][k];
+          }
+          red[2 * L * D + e + k] = (ww ? red[2 * L * D + e + k] : 0.f) + dwfa[r][k];
+        }
+      }
+      if (lane == 0) red[(2 * L + 1) * D] = (ww ? red[(2 * L + 1) * D] : 0.f) + dbf;
+    }
+    __syncthreads();
+  }
+  float* mp = part + (int64_t)blockIdx.x * stride_p;
+  for (int i = threadIdx.x; i < stride_p; i += NT) mp[i] = red[i];
+}
+
 // Reduce per-block partials -> grads.  Block = 64 columns x 4 partial lanes
 // over a range of partial rows (RED_G ranges in blockIdx.y), fp32 block sums
 // to cred2 [RED_G][stride], and the last arriver of each column group adds the
@@ -770,6 +968,52 @@ dcnr_status launch_bwd(const GatherDesc& g, const CrossBwdParams& p, const int64
   return DCNR_OK;
 }
 
+#ifndef GC_V4B_SPW
+#define GC_V4B_SPW 2
+#endif
+#ifndef GC_V4B_WAVES
+#define GC_V4B_WAVES 3072
+#endif
+
+template <int R4, int L>
+dcnr_status launch_bwd_v4(const GatherDesc& g, const CrossBwdParams& p, const int64_t* user,
+                          const int64_t* item, const int64_t* cat, const float* num,
+                          const float* dz, int64_t B, const float* dx0, int ld_dx, float* part,
+                          int64_t* nb_out, hipStream_t s) {
+  constexpr int SPW = GC_V4B_SPW;
+  const size_t lds = (size_t)(2 * L + 1) * R4 * WAVE * 16 +
+                     (size_t)((((2 * L + 1) * g.D + 1) + 3) & ~3) * sizeof(float) +
+                     (size_t)R4 * WAVE * 4 * (8 + 4 + 4) + (size_t)WPB * R4 * WAVE * 16;
+  const int64_t ntiles = cdiv(B, SPW);
+  const int64_t waves = cdiv(ntiles, cdiv(ntiles, GC_V4B_WAVES));
+  const int64_t nb = std::min<int64_t>(cdiv(waves, WPB), BWD_BLOCKS);
+  static size_t attr_lds = 0;
+  if (lds > 64 * 1024 && lds > attr_lds) {
+    DCNR_HIP(hipFuncSetAttribute((const void*)cross_bwd_v4_kernel<R4, L, SPW>,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr_lds = lds;
+  }
+  hipLaunchKernelGGL((cross_bwd_v4_kernel<R4, L, SPW>), dim3((unsigned)nb), dim3(NT), lds, s, g, p,
+                     user, item, cat, num, dz, B, dx0, ld_dx, part);
+  DCNR_LAUNCH_CHECK();
+  *nb_out = nb;
+  return DCNR_OK;
+}
+
+template <int R4>
+dcnr_status dispatch_bwd_v4(int L, const GatherDesc& g, const CrossBwdParams& p,
+                            const int64_t* user, const int64_t* item, const int64_t* cat,
+                            const float* num, const float* dz, int64_t B, const float* dx0,
+                            int ld_dx, float* part, int64_t* nb, hipStream_t s) {
+  switch (L) {
+#define CASE(n) \
+  case n: return launch_bwd_v4<R4, n>(g, p, user, item, cat, num, dz, B, dx0, ld_dx, part, nb, s);
+    CASE(0) CASE(1) CASE(2) CASE(3) CASE(4)
+#undef CASE
+  }
+  return DCNR_UNSUPPORTED_SHAPE;
+}
+
 template <int RM>
 dcnr_status dispatch_bwd_L(int L, const GatherDesc& g, const CrossBwdParams& p,
                            const int64_t* user, const int64_t* item, const int64_t* cat,
@@ -858,8 +1102,18 @@ dcnr_status cross_bwd_scatter(const GatherDesc& g, const CrossBwdParams& p, cons
     set_error("cross_bwd: D=%d unsupported", D);
     return DCNR_UNSUPPORTED_SHAPE;
   }
-  const int64_t nb = bwd_blocks(B);
-  dcnr_status st = D <= 8 * WAVE
+  int64_t nb = bwd_blocks(B);
+  dcnr_status st;
+  const GcOut chk{nullptr, const_cast<float*>(dx0_deep), nullptr, 0, ld_dx};
+  const bool v4 = L <= 4 && g.n_tab * GC_V4B_SPW <= 64 && v4_ok(g, num, chk);
+  if (v4)
+    st = D <= 4 * WAVE && ld_dx <= 4 * WAVE
+             ? dispatch_bwd_v4<1>(L, g, p, user, item, cat, num, dz, B, dx0_deep, ld_dx, ws.part,
+                                  &nb, s)
+             : dispatch_bwd_v4<2>(L, g, p, user, item, cat, num, dz, B, dx0_deep, ld_dx, ws.part,
+                                  &nb, s);
+  else
+    st = D <= 8 * WAVE
                        ? dispatch_bwd_L<8>(L, g, p, user, item, cat, num, dz, B, dx0_deep, ld_dx,
                                            ws.part, nb, s)
                        : dispatch_bwd_L<16>(L, g, p, user, item, cat, num, dz, B, dx0_deep, ld_dx,
@@ -870,5 +1124,6 @@ dcnr_status cross_bwd_scatter(const GatherDesc& g, const CrossBwdParams& p, cons
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
+
 
 }  // namespace dcnr
