@@ -875,6 +875,62 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   return DCNR_OK;
 }
 
+dcnr_status dcnr_candidate_union(const int64_t* positives, int64_t Q, const int64_t* knn_idx,
+                                 int32_t k, int64_t* out_rows, int32_t* out_count,
+                                 dcnr_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (Q < 0 || (Q > 0 && (!positives || !knn_idx || !out_rows || !out_count))) {
+    set_error("dcnr_candidate_union: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  if (Q == 0) return DCNR_OK;
+  TRYP(DCNR_K_SERVE, candidate_union(positives, Q, knn_idx, k, out_rows, out_count, s));
+  return DCNR_OK;
+}
+
+dcnr_status dcnr_ranking_batch(const int64_t* item_rows, int64_t n, int64_t user_row,
+                               const int64_t* item_cat, int32_t n_cat, const float* item_num,
+                               int32_t n_num, int64_t n_items, int64_t* user_ids,
+                               int64_t* item_ids, int64_t* cat_features, float* num_features,
+                               dcnr_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n < 0 || n_items < 1 || n_cat < 0 || n_num < 0 ||
+      (n > 0 && (!item_rows || !user_ids || !item_ids || (n_cat && (!item_cat || !cat_features)) ||
+                 (n_num && (!item_num || !num_features))))) {
+    set_error("dcnr_ranking_batch: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  TRYP(DCNR_K_SERVE, ranking_batch(item_rows, n, user_row, item_cat, n_cat, item_num, n_num,
+                                   n_items, user_ids, item_ids, cat_features, num_features, s));
+  return DCNR_OK;
+}
+
+dcnr_status dcnr_rank_by_score(const float* scores, int64_t n, int64_t* order,
+                               dcnr_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n < 0 || (n > 0 && (!scores || !order))) {
+    set_error("dcnr_rank_by_score: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  TRYP(DCNR_K_SERVE, rank_desc(scores, n, order, s));
+  return DCNR_OK;
+}
+
+dcnr_status dcnr_mmr_rerank(const float* table, const float* inv_norms, int32_t d,
+                            const int64_t* rows, const float* scores, int64_t n,
+                            float lambda_param, int32_t top_k, int64_t* out_pos,
+                            int32_t* out_count, dcnr_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (n < 0 || top_k < 1 || (n > 0 && (!table || !inv_norms || !rows || !scores || !out_pos ||
+                                       !out_count))) {
+    set_error("dcnr_mmr_rerank: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  TRYP(DCNR_K_SERVE, mmr_rerank(table, inv_norms, d, rows, scores, n, lambda_param, top_k,
+                                out_pos, out_count, s));
+  return DCNR_OK;
+}
+
 size_t dcnr_bce_workspace_size(void) { return bce_ws_bytes() + 256; }
 
 dcnr_status dcnr_bce_with_logits(const float* logits, const float* labels, int64_t B, float* loss,

@@ -495,6 +495,17 @@ dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, cons
                         int64_t Q, int k, int64_t* idx, float* dist, void* ws, size_t ws_bytes,
                         hipStream_t s);
 
+// serving (serving.hip)
+dcnr_status candidate_union(const int64_t* pos, int64_t Q, const int64_t* idx, int k,
+                            int64_t* out, int32_t* out_count, hipStream_t s);
+dcnr_status ranking_batch(const int64_t* rows, int64_t n, int64_t user_row, const int64_t* item_cat,
+                          int K, const float* item_num, int F, int64_t n_items, int64_t* user_out,
+                          int64_t* item_out, int64_t* cat_out, float* num_out, hipStream_t s);
+dcnr_status rank_desc(const float* scores, int64_t n, int64_t* order, hipStream_t s);
+dcnr_status mmr_rerank(const float* table, const float* inv, int d, const int64_t* rows,
+                       const float* scores, int64_t n, float lambda, int top_k, int64_t* out_pos,
+                       int32_t* out_count, hipStream_t s);
+
 dcnr_status fill_zero(void* p, size_t bytes, hipStream_t s);
 dcnr_status fill_zero_multi(int n, void* const* ptrs, const int64_t* bytes, hipStream_t s);
 

@@ -8,6 +8,9 @@ System-Based-on-Friends-Recommendations):
   AdamW, Adam                        train.py:201-204
   NearestNeighbors (cosine, brute)   main.py:268-270
   FusedTrainer                       the train.py:219-226 inner-loop step
+  serving.rerank_with_mmr            main.py:133-169
+  serving.RankingPipeline            the /recommendations + /similar_items core
+                                     (main.py:196-230, 294-332)
 
 All compute runs in libdcnr.so (C ABI: include/dcnr.h) on the HIP device.
 """
@@ -15,5 +18,7 @@ from .model import CrossLayer, DCN_RecSys, ResBlock  # noqa: F401
 from .ops import Adam, AdamW, BCEWithLogitsLoss, bce_with_logits  # noqa: F401
 from .knn import NearestNeighbors  # noqa: F401
 from .train import FusedTrainer  # noqa: F401
+from . import serving  # noqa: F401
+from .serving import RankingPipeline, rerank_with_mmr  # noqa: F401
 
 __version__ = "0.1.0"

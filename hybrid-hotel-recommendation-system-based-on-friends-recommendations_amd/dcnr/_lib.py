@@ -70,6 +70,12 @@ _SIGS = {
     "dcnr_cosine_topk_workspace_size": (ctypes.c_size_t, [_I64, _I64, ctypes.c_int32]),
     "dcnr_cosine_topk": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, _P, _I64, ctypes.c_int32,
                                         _P, _P, _P, ctypes.c_size_t, _P]),
+    "dcnr_candidate_union": (ctypes.c_int, [_P, _I64, _P, ctypes.c_int32, _P, _P, _P]),
+    "dcnr_ranking_batch": (ctypes.c_int, [_P, _I64, _I64, _P, ctypes.c_int32, _P, ctypes.c_int32,
+                                          _I64, _P, _P, _P, _P, _P]),
+    "dcnr_rank_by_score": (ctypes.c_int, [_P, _I64, _P, _P]),
+    "dcnr_mmr_rerank": (ctypes.c_int, [_P, _P, ctypes.c_int32, _P, _P, _I64, ctypes.c_float,
+                                       ctypes.c_int32, _P, _P, _P]),
     "dcnr_check_errors": (ctypes.c_int, [_P, ctypes.c_size_t, _P]),
     "dcnr_linear_bf16": (ctypes.c_int, [_P, _I64, _I64, ctypes.c_int32, _P, _I64, ctypes.c_int32,
                                         _P, _P, _I64, ctypes.c_int, _P]),
@@ -82,7 +88,7 @@ _SIGS = {
 }
 
 KERNEL_CLASSES = ["gather_cross", "gemm_fwd", "gemm_dx", "gemm_dw", "rowwise", "reduce",
-                  "cross_bwd", "head", "adam", "knn", "pack"]
+                  "cross_bwd", "head", "adam", "knn", "pack", "serve"]
 
 
 def profile_enable(on: bool):

@@ -19,6 +19,11 @@
  *   dcnr_cosine_topk      NearestNeighbors(metric='cosine', algorithm='brute')
  *                         .kneighbors(vec, n_neighbors=k)      main.py:196-203,268-270,300
  *   dcnr_row_inv_norms    the row normalisation inside sklearn's cosine metric
+ *   dcnr_candidate_union  _generate_candidates' union of positives and their
+ *                         neighbours[1:]                      main.py:196-203
+ *   dcnr_ranking_batch    preprocess_for_ranking              main.py:215-230
+ *   dcnr_rank_by_score    sorted(zip(scores, ids), reverse=True) main.py:325
+ *   dcnr_mmr_rerank       rerank_with_mmr                     main.py:133-169
  *
  * Conventions
  *  - All tensor pointers are DEVICE pointers owned by the caller; the
@@ -179,6 +184,44 @@ dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t
                              const float* queries, int64_t Q, int32_t k, int64_t* idx,
                              float* dist, void* ws, size_t ws_bytes, dcnr_stream_t stream);
 
+/* ---- serving: the steps either side of scoring in /recommendations ----
+ * All operate on at most 4096 items per call (DCNR_UNSUPPORTED_SHAPE above). */
+
+/* Candidate set of _generate_candidates (main.py:196-203): the union of
+ * positives[Q] (embedding rows of the positive hotels) and, for each, the
+ * neighbour rows knn_idx[q][1..k-1] (the dcnr_cosine_topk output for
+ * n_neighbors = k, position 0 dropped as main.py:201 does); negative rows are
+ * skipped.  out_rows: the distinct rows ascending; out_count[0] (device
+ * int32) = their number.  Q*k <= 4096. */
+dcnr_status dcnr_candidate_union(const int64_t* positives, int64_t Q, const int64_t* knn_idx,
+                                 int32_t k, int64_t* out_rows, int32_t* out_count,
+                                 dcnr_stream_t stream);
+
+/* Ranking batch of preprocess_for_ranking (main.py:215-230) for one user:
+ * user_ids[i] = user_row, item_ids[i] = item_rows[i], and the item's
+ * categorical codes / scaled numeric features gathered from per-item tables
+ * item_cat [n_items][n_cat] (int64) and item_num [n_items][n_num] (fp32). */
+dcnr_status dcnr_ranking_batch(const int64_t* item_rows, int64_t n, int64_t user_row,
+                               const int64_t* item_cat, int32_t n_cat, const float* item_num,
+                               int32_t n_num, int64_t n_items, int64_t* user_ids,
+                               int64_t* item_ids, int64_t* cat_features, float* num_features,
+                               dcnr_stream_t stream);
+
+/* order[i] = index of the i-th highest score; equal scores keep input order
+ * (Python's stable sorted(..., reverse=True), main.py:325).  n <= 4096. */
+dcnr_status dcnr_rank_by_score(const float* scores, int64_t n, int64_t* order,
+                               dcnr_stream_t stream);
+
+/* rerank_with_mmr (main.py:133-169) over n candidates given in ranked order:
+ * rows[i] = embedding row of candidate i in `table` [., d] (-1: no embedding),
+ * scores[i] its score.  Writes out_pos[0 .. top_k) = positions (into the ranked
+ * list) of the re-ranked items, -1 padded; out_count[0] (device int32) = their
+ * number.  Cosine similarity via inv_norms (dcnr_row_inv_norms). */
+dcnr_status dcnr_mmr_rerank(const float* table, const float* inv_norms, int32_t d,
+                            const int64_t* rows, const float* scores, int64_t n,
+                            float lambda_param, int32_t top_k, int64_t* out_pos,
+                            int32_t* out_count, dcnr_stream_t stream);
+
 /* The deep tower's Linear layer as a standalone bf16 call (nn.Linear forward,
  * train.py:143,105,109): C[M,N] = X[M,K] . W[N,K]^T + bias, X/W bf16
  * row-major (K, ldx, ldw multiples of 8), C bf16 (out_f32 = 0) or fp32.
@@ -213,7 +256,8 @@ typedef enum {
   DCNR_K_ADAM = 8,         /* fused Adam/AdamW                              */
   DCNR_K_KNN = 9,          /* cosine top-k                                  */
   DCNR_K_PACK = 10,        /* weight packing / zero fills                  */
-  DCNR_K_COUNT = 11
+  DCNR_K_SERVE = 11,       /* candidate union, ranking batch, sort, MMR     */
+  DCNR_K_COUNT = 12
 } dcnr_kernel_class;
 
 void dcnr_profile_enable(int on);

@@ -28,6 +28,10 @@ reference repository root):
   ``sklearn/metrics/pairwise.py`` cosine_distances and
   ``sklearn/neighbors/_base.py`` ``_kneighbors_reduce_func``: argpartition
   then argsort)
+* ``main.py:196-203``   candidate union of _generate_candidates
+* ``main.py:325``       stable descending sort of the scored candidates
+* ``main.py:133-169``   ``rerank_with_mmr`` (pinned by tests/golden/f8_mmr.npz,
+  made by running the reference: tests/golden/make_serving_golden.py)
 """
 from __future__ import annotations
 
@@ -299,3 +303,57 @@ def cosine_kneighbors(table: np.ndarray, queries: np.ndarray, k: int):
     d = np.clip(1.0 - s, 0.0, 2.0).astype(np.float32)
     idx = np.argsort(d, axis=1, kind='stable')[:, :k]
     return np.take_along_axis(d, idx, axis=1), idx
+
+
+# --------------------------------------------------------------------------
+# serving: candidate union, ranking order, MMR (main.py:196-203, 325, 133-169)
+# --------------------------------------------------------------------------
+def candidate_union(positive_rows, knn_idx):
+    """_generate_candidates' set (main.py:196-203): the positives plus each
+    one's neighbours with position 0 dropped (main.py:201), as ascending rows."""
+    s = set(int(r) for r in positive_rows)
+    for row in np.asarray(knn_idx):
+        s.update(int(r) for r in row[1:] if r >= 0)
+    return np.asarray(sorted(s), dtype=np.int64)
+
+
+def rank_by_score(scores):
+    """sorted(zip(scores, ids), key=score, reverse=True) (main.py:325): a
+    stable descending order (equal scores keep their input order)."""
+    return np.argsort(-np.asarray(scores, dtype=np.float32), kind='stable')
+
+
+def mmr_rerank(emb, rows, scores, lam, top_k=20):
+    """rerank_with_mmr (main.py:133-169) on embedding rows (-1 = id absent from
+    item_id_mapping) in ranked order; returns positions into the ranked list.
+    cosine_similarity as sklearn: normalize (zero rows stay zero), then dot."""
+    emb = np.asarray(emb, dtype=np.float32)
+    n = len(rows)
+    if n == 0:
+        return []
+
+    def unit(v):
+        nv = np.sqrt(np.dot(v, v))
+        return v / nv if nv > 0 else v
+
+    final = [0]
+    remaining = list(range(1, n))
+    while len(final) < min(top_k, n):
+        best, best_score = -1, -np.inf
+        sel = [rows[p] for p in final if rows[p] >= 0]
+        for p in remaining:
+            if rows[p] < 0:
+                continue
+            if not sel:
+                ms = np.float32(0.0)
+            else:
+                c = unit(emb[rows[p]])
+                ms = max(np.float32(np.dot(c, unit(emb[s]))) for s in sel)
+            m = np.float32(lam) * np.float32(scores[p]) - np.float32(1 - lam) * ms
+            if m > best_score:
+                best, best_score = p, m
+        if best == -1:
+            break
+        final.append(best)
+        remaining.remove(best)
+    return final

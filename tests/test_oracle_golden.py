@@ -94,3 +94,27 @@ def test_f6_cosine_knn_vs_sklearn():
             # the k-set can differ only inside the tie group at the boundary
             inner = ref_d < ref_d[-1] - 2e-6
             assert set(ref_i[inner]) <= set(i[r].tolist())
+
+
+def mmr_scenarios():
+    fx = golden("f8_mmr.npz")
+    mapping = {int(i): r for r, i in enumerate(fx["ids_all"])}
+    for s, name in enumerate(fx["names"]):
+        ids = fx[f"s{s}_ids"]
+        rows = np.array([mapping.get(int(i), -1) for i in ids], dtype=np.int64)
+        yield (str(name), fx["emb"], ids, rows, fx[f"s{s}_scores"], float(fx[f"s{s}_lam"]),
+               int(fx[f"s{s}_topk"]), fx[f"s{s}_out"])
+
+
+def test_f8_mmr_oracle_vs_reference():
+    """oracle.mmr_rerank restates main.py:133-169; f8 was made by running it."""
+    for name, emb, ids, rows, scores, lam, top_k, expect in mmr_scenarios():
+        pos = orc.mmr_rerank(emb, rows, scores, lam, top_k)
+        assert [int(ids[p]) for p in pos] == expect.tolist(), name
+
+
+def test_rank_and_union_oracle():
+    s = np.array([0.5, 2.0, 0.5, -1.0, 2.0], np.float32)
+    assert orc.rank_by_score(s).tolist() == [1, 4, 0, 2, 3]   # stable on ties
+    u = orc.candidate_union([5, 9], np.array([[5, 3, 9, -1], [9, 5, 7, 7]]))
+    assert u.tolist() == [3, 5, 7, 9]

@@ -1,0 +1,110 @@
+"""GPU parity of the serving core (dcnr.serving; serving.hip + knn.hip + the
+eval forward) against the reference's MMR golden fixture (f8, made by running
+main.py:133-169) and the CPU oracle.
+
+Criteria: candidate sets, ranking batches, sort orders and MMR selections are
+integer/index results and must be identical; logits follow the fp32 bar of
+test_parity_gpu (1e-4 * max(|ref|, 1)).  Inputs are drawn so that no two
+scores or similarities that decide an order lie within fp32 rounding.
+"""
+import numpy as np
+import pytest
+import torch
+
+import dcnr_oracle as orc
+import golden_common as gc
+from conftest import golden
+from helpers import np_state, our_model, spec_of
+
+pytestmark = pytest.mark.gpu
+
+
+def test_mmr_vs_reference_golden(dev):
+    from dcnr import serving
+    fx = golden("f8_mmr.npz")
+    ids_all = fx["ids_all"]
+    serving.ml_artifacts.clear()
+    serving.ml_artifacts['item_embeddings'] = fx["emb"]
+    serving.ml_artifacts['artifacts'] = {'item_id_mapping': {int(i): r for r, i in enumerate(ids_all)}}
+    serving.ml_artifacts['device'] = dev
+    for s, name in enumerate(fx["names"]):
+        ranked = list(zip(fx[f"s{s}_scores"].tolist(), fx[f"s{s}_ids"].tolist()))
+        got = serving.rerank_with_mmr(ranked, float(fx[f"s{s}_lam"]), int(fx[f"s{s}_topk"]))
+        assert got == fx[f"s{s}_out"].tolist(), str(name)
+    assert serving.rerank_with_mmr([], 0.5) == []
+
+
+@pytest.mark.parametrize("n", [1, 7, 300, 4096])
+def test_rank_by_score_stable(dev, n):
+    from dcnr.serving import RankingPipeline
+    rng = np.random.default_rng(n)
+    s = rng.integers(-20, 20, n).astype(np.float32) / 4   # many exact ties
+    pipe = RankingPipeline.__new__(RankingPipeline)
+    pipe.device = dev
+    order = pipe.rank(torch.from_numpy(s).to(dev)).cpu().numpy()
+    assert order.tolist() == orc.rank_by_score(s).tolist()
+
+
+def make_pipeline(dev, n_items=3000, d=16, seed=0):
+    import dcnr
+    cfg = dict(n_users=400, n_items=n_items, cat_dims={"a": 30, "b": 250, "c": 1000}, n_num=4,
+               params=dict(emb_dim=d, hidden_dim=64, n_cross_layers=2, n_res_blocks=2,
+                           dropout=0.0))
+    m = our_model(cfg, seed=seed).to(dev)
+    rng = np.random.default_rng(seed)
+    item_cat = np.stack([rng.integers(0, c, n_items) for c in cfg["cat_dims"].values()], 1)
+    item_num = rng.random((n_items, 4), dtype=np.float32)
+    pipe = dcnr.serving.RankingPipeline(m, item_cat, item_num)
+    return cfg, m, pipe, item_cat, item_num
+
+
+def test_candidate_union_and_batch(dev):
+    from dcnr import _lib  # noqa: F401
+    cfg, m, pipe, item_cat, item_num = make_pipeline(dev)
+    emb = m.item_embedding.weight.detach().cpu().numpy()
+    rng = np.random.default_rng(3)
+    pos = rng.choice(cfg["n_items"], 40, replace=False)
+    cand = pipe.candidates(pos).cpu().numpy()
+    _, idx = orc.cosine_kneighbors(emb, emb[pos], 11)
+    assert cand.tolist() == orc.candidate_union(pos, idx).tolist()
+    u, i, c, x = pipe.ranking_batch(17, torch.from_numpy(cand).to(dev))
+    assert (u.cpu().numpy() == 17).all()
+    assert np.array_equal(i.cpu().numpy(), cand)
+    assert np.array_equal(c.cpu().numpy(), item_cat[cand])
+    assert np.array_equal(x.cpu().numpy(), item_num[cand])
+    # /similar_items: kneighbors(n+1)[1:]
+    sim = pipe.similar_items(int(pos[0]), 10).cpu().numpy()
+    assert sim.tolist() == idx[0, 1:].tolist()
+
+
+@pytest.mark.parametrize("lam", [1.0, 0.7, 0.3])
+def test_recommend_matches_oracle(dev, lam):
+    cfg, m, pipe, item_cat, item_num = make_pipeline(dev, seed=5)
+    sd = np_state(m)
+    spec = spec_of(cfg)
+    emb = sd['item_embedding.weight'].astype(np.float32)
+    rng = np.random.default_rng(11)
+    pos = rng.choice(cfg["n_items"], 12, replace=False)
+    user = 123
+    rows, logits = pipe.recommend(user, pos, lambda_param=lam, top_k=20)
+    # oracle composition of main.py:196-203, 215-230, 319-332
+    _, idx = orc.cosine_kneighbors(emb, emb[pos], 11)
+    cand = orc.candidate_union(pos, idx)
+    n = len(cand)
+    z, _ = orc.forward(sd, spec, np.full(n, user), cand, item_cat[cand], item_num[cand],
+                       train=False)
+    order = orc.rank_by_score(z.astype(np.float32))
+    ranked, rz = cand[order], z[order]
+    zs = np.sort(z)
+    assert np.min(np.diff(zs)) > 1e-5, "inputs must not have near-tied scores"
+    if lam < 1.0:
+        p = orc.mmr_rerank(emb, ranked, rz.astype(np.float32), lam, 20)
+        ranked, rz = ranked[p], rz[p]
+    assert rows.cpu().numpy().tolist() == ranked.tolist()
+    got = logits.cpu().double().numpy()
+    assert np.max(np.abs(got - rz) / np.maximum(np.abs(rz), 1.0)) <= 1e-4
+    # host filters (city / negative reviews, main.py:210-212)
+    allowed = set(cand[::2].tolist())
+    excluded = {int(cand[0])}
+    rows2, _ = pipe.recommend(user, pos, 1.0, allowed=allowed, excluded=excluded)
+    assert set(rows2.cpu().tolist()) == (allowed - excluded)
