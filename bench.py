@@ -143,6 +143,84 @@ def bench_cfg2(model, gen, dev, iters, world):
                          "bytes_per_sample": CFG2_BYTES, "avg_launch_ms": ms / cnt}}
 
 
+def bench_cfg5(dev, iters, cpu):
+    """BASELINE configs[4]: cosine top-k over 1M hotel vectors (d=64) feeding
+    the DCN-R ranking batch (dcnr.serving.RankingPipeline; the item table of a
+    DCN-R with n_items = 1M, emb_dim = 64).  Top-k per-launch time from HIP
+    events (class knn); end-to-end request latency = candidates of Q=32
+    positive hotels (one batched top-11) -> union -> ranking batch -> eval
+    forward -> sort -> MMR (lambda 0.7, top 20), host syncs included."""
+    import dcnr
+    from dcnr import _lib
+    torch.manual_seed(5)
+    n_items = 1_000_000
+    m = dcnr.DCN_RecSys(1_000_000, n_items, CFG["cat_dims"], CFG["n_num"],
+                        dict(CFG["params"], emb_dim=64), precision="bf16").to(dev).eval()
+    g = torch.Generator(device=dev).manual_seed(7)
+    item_cat = torch.randint(0, 1000, (n_items, 12), generator=g, device=dev)
+    item_num = torch.rand((n_items, 8), generator=g, device=dev)
+    pipe = dcnr.RankingPipeline(m, item_cat, item_num)
+    table_bytes = n_items * (64 * 4 + 4)
+    out = {"workload": "BASELINE configs[4]: cosine top-11 over 1M x 64 hotel vectors fused into "
+                       "a DCN-R ranking batch (emb_dim 64, 12 x 1000 cat, 8 dense, 3 cross, "
+                       "4 x 512, bf16 eval)", "k": 11}
+    for Q in (1, 32, 256):
+        q = pipe.index._table[torch.randint(0, n_items, (Q,), generator=g, device=dev)]
+        for _ in range(2):
+            pipe.index.kneighbors_device(q, 11)
+        _lib.profile_enable(True)
+        _lib.profile_collect()
+        for _ in range(iters):
+            pipe.index.kneighbors_device(q, 11)
+        _lib.profile_enable(False)
+        ms, cnt = _lib.profile_collect()["knn"]
+        t = ms / cnt / 1e3
+        out[f"topk_q{Q}_us"] = t * 1e6
+        out[f"topk_q{Q}_queries_per_sec"] = Q / t
+        if Q == 1:
+            out["roofline"] = {"bound": "hbm", "kernel": "scan2_kernel + merge (dcnr_cosine_topk, Q=1)",
+                               "achieved": table_bytes / t / 1e9, "peak": PEAK_HBM / 1e9,
+                               "unit": "GB/s", "frac": table_bytes / t / PEAK_HBM,
+                               "bytes_per_call": table_bytes}
+    users = torch.randint(0, 1_000_000, (iters,), generator=g, device=dev).tolist()
+    pos = [torch.randint(0, n_items, (32,), generator=g, device=dev) for _ in range(iters)]
+    for k in range(2):
+        pipe.recommend(users[k], pos[k], lambda_param=0.7)
+    torch.cuda.synchronize()
+    n_scored = sum(pipe.candidates(p).numel() for p in pos)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(iters):
+        pipe.recommend(users[k], pos[k], lambda_param=0.7)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out["request_ms"] = el / iters * 1e3
+    out["requests_per_sec"] = iters / el
+    out["candidates_per_request"] = n_scored / iters
+    out["scored_pairs_per_sec"] = n_scored / el
+    if cpu:
+        try:
+            from sklearn.neighbors import NearestNeighbors as SkNN
+            tab = pipe.index._table.cpu().numpy()
+            nn = SkNN(n_neighbors=11, metric="cosine", algorithm="brute").fit(tab)
+            t0 = time.perf_counter()
+            for j in range(3):
+                nn.kneighbors(tab[j:j + 1], n_neighbors=11)
+            cpu_t = (time.perf_counter() - t0) / 3
+            out["cpu_baseline_topk"] = {"value": 1.0 / cpu_t, "unit": "queries/s",
+                                        "cores": int(os.environ.get("OMP_NUM_THREADS",
+                                                                    os.cpu_count() or 1)),
+                                        "kind": "reference",
+                                        "sample": "sklearn NearestNeighbors(cosine, brute)"
+                                                  ".kneighbors, 3 single queries on the same "
+                                                  "1M x 64 table (main.py:268-270, 200)"}
+        except Exception as e:   # sklearn absent: report nothing rather than a fake number
+            out["cpu_baseline_topk"] = {"error": repr(e)}
+    del pipe, m
+    torch.cuda.empty_cache()
+    return out
+
+
 def pmc_traffic(kernel_class):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -164,6 +242,7 @@ def main():
     ap.add_argument("--pool", type=int, default=8)
     ap.add_argument("--eval-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-serving", action="store_true", help="skip the configs[4] top-k leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -241,6 +320,8 @@ def main():
         dist.all_reduce(ev, op=dist.ReduceOp.MAX)
     pairs_per_s = world * B * args.eval_steps / float(ev.item())
     cfg2 = bench_cfg2(model, gen, dev, max(args.steps, 10), world)
+    cfg5 = bench_cfg5(dev, 10, world == 1 and rank == 0 and not args.no_cpu_baseline) \
+        if not args.no_serving else None
 
     if rank == 0:
         samples = world * B * args.steps
@@ -297,6 +378,7 @@ def main():
                                 "frac": gather_gbs / (PEAK_HBM / 1e9),
                                 "bytes_per_sample": GATHER_BYTES, "avg_launch_ms": g_ms / g_cnt},
             "configs1": cfg2,
+            "configs4": cfg5,
             "kernel_ms_per_step": per_step_ms,
             "kernel_launches_per_step": launches,
         }
