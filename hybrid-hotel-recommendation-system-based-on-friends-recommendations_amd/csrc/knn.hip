@@ -32,16 +32,16 @@ __device__ __forceinline__ bool cless(float da, int ia, float db, int ib) {
 }
 
 // bitonic sort of CAP entries in LDS, ascending; all NT threads participate
-__device__ void bitonic(float* cd, int* ci) {
-  for (int k2 = 2; k2 <= CAP; k2 <<= 1) {
+__device__ void bitonic(float* cd, int* ci, int n2 = CAP) {
+  for (int k2 = 2; k2 <= n2; k2 <<= 1) {
     for (int j = k2 >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < CAP / 2; t += NT) {
-        int i = (t / j) * 2 * j + (t % j);
-        int p = i + j;
-        bool asc = (i & k2) == 0;
-        float a = cd[i], b = cd[p];
-        int ia = ci[i], ib = ci[p];
-        bool sw = asc ? cless(b, ib, a, ia) : cless(a, ia, b, ib);
+      for (int t = threadIdx.x; t < n2 / 2; t += NT) {
+        const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+        const int p = i + j;
+        const bool asc = (i & k2) == 0;
+        const float a = cd[i], b = cd[p];
+        const int ia = ci[i], ib = ci[p];
+        const bool sw = asc ? cless(b, ib, a, ia) : cless(a, ia, b, ib);
         if (sw) { cd[i] = b; cd[p] = a; ci[i] = ib; ci[p] = ia; }
       }
       __syncthreads();
@@ -152,6 +152,9 @@ __global__ __launch_bounds__(NT) void scan_kernel(const float* __restrict__ tab,
 // is XCD-grouped: the blocks that share a row slice run on one XCD, whose L2
 // serves the repeated reads of the slice.
 constexpr int K2_NT = 256, K2_WPB = K2_NT / 64, K2_QT = 32, K2_CAP = 64, K2_KMAX = 32;
+#ifndef MFMA_MIN_Q
+#define MFMA_MIN_Q 4   // queries from which the fp32-MFMA scan (v3) is used
+#endif
 
 __device__ __forceinline__ void wave_sort64(float& d, int& i, int lane) {
 #pragma unroll
@@ -190,7 +193,8 @@ __global__ __launch_bounds__(K2_NT) void scan2_kernel(const float* __restrict__ 
                                                       const float* __restrict__ inv, int64_t N,
                                                       const float* __restrict__ qn, int64_t Q,
                                                       int k, int64_t rows_per_block, int nslices,
-                                                      int qtiles, Cand* out) {
+                                                      int qtiles, Cand* out,
+                                                      const float* __restrict__ thr0) {
   __shared__ float cd[K2_WPB][K2_QT][K2_CAP];
   __shared__ int ci[K2_WPB][K2_QT][K2_CAP];
   __shared__ int cntl[K2_WPB][K2_QT];
@@ -204,9 +208,11 @@ __global__ __launch_bounds__(K2_NT) void scan2_kernel(const float* __restrict__ 
   // the normalised queries are read with wave-uniform addresses: scalar
   // loads into SGPRs, one FMA operand each (no LDS broadcast traffic)
   const float4* qv = reinterpret_cast<const float4*>(qn + q0 * DV * 4);
-  // per-query list count and threshold of this wave: lane qq holds query qq's
+  // per-query list count and threshold of this wave: lane qq holds query qq's;
+  // bound0: the admission bound (kth_bound_kernel), lane qq holding query qq's
   int cntv = 0;
   float thrv = FLT_MAX;
+  const float bound0 = lane < nq ? thr0[q0 + lane] : FLT_MAX;
   const int64_t r0 = (int64_t)slice * rows_per_block;
   const int64_t r1 = min(N, r0 + rows_per_block);
   for (int64_t base = r0 + 64 * w; base < r1; base += 64 * K2_WPB) {
@@ -227,7 +233,8 @@ __global__ __launch_bounds__(K2_NT) void scan2_kernel(const float* __restrict__ 
       }
       const float dist = fminf(fmaxf(1.f - s * ir, 0.f), 2.f);
       float th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thrv), qq));
-      bool pass = ok && dist < th;
+      const float b0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bound0), qq));
+      bool pass = ok && dist < th && dist <= b0;
       uint64_t m = __ballot(pass);
       if (!m) continue;
       int c = __builtin_amdgcn_readlane(cntv, qq);
@@ -283,6 +290,200 @@ __global__ __launch_bounds__(K2_NT) void scan2_kernel(const float* __restrict__ 
   }
 }
 
+// ---------------------------------------------------------------- scan v3
+// fp32 MFMA scoring (v_mfma_f32_16x16x4_f32, exact f32 products and sums):
+// per wave, 16-row tiles of the table (A operand) against K3_QT queries
+// (B operand, resident in registers, 16 per column block).  The dot product
+// is order-free in k, so lane (r, g) feeds k = 16 s + 4 g + j from the float4
+// chunk 4 s + g of its row: every A/B fragment comes from one 16-B load, no
+// shuffles.  Output lane (q, g) holds rows 4 g .. 4 g + 3 for query q.  The
+// candidate lists are the per-(wave, query) LDS lists of scan v2; appends use
+// ballot over the four lanes of a query; a list above K2_CAP - 16 entries is
+// compacted before the next tile (at most 16 appends per tile).
+constexpr int K3_QT = 32, K3_CB = K3_QT / 16;
+
+template <int DV>
+__global__ __launch_bounds__(K2_NT) void scan3_kernel(const float* __restrict__ tab,
+                                                      const float* __restrict__ inv, int64_t N,
+                                                      const float* __restrict__ qn, int64_t Q,
+                                                      int k, int64_t rows_per_block, int nslices,
+                                                      int qtiles, Cand* out,
+                                                      const float* __restrict__ thr0) {
+  constexpr int S4 = DV / 4;
+  __shared__ float cd[K2_WPB][K3_QT][K2_CAP];
+  __shared__ int ci[K2_WPB][K3_QT][K2_CAP];
+  __shared__ int cntl[K2_WPB][K3_QT];
+  const int bid = blockIdx.x;
+  const int tile = (bid / 8) % qtiles;
+  const int slice = (bid % 8) + 8 * (bid / (8 * qtiles));
+  if (slice >= nslices) return;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int64_t q0 = (int64_t)tile * K3_QT;
+  const int nq = (int)min<int64_t>(K3_QT, Q - q0);
+  float4 bq[K3_CB][S4];
+#pragma unroll
+  for (int cb = 0; cb < K3_CB; ++cb) {
+    const int64_t qi = q0 + 16 * cb + r16;
+#pragma unroll
+    for (int s = 0; s < S4; ++s)
+      bq[cb][s] = qi < Q ? reinterpret_cast<const float4*>(qn + qi * DV * 4)[4 * s + g]
+                         : float4{0.f, 0.f, 0.f, 0.f};
+  }
+  float thr[K3_CB], bnd[K3_CB];
+  int cnt[K3_CB];
+#pragma unroll
+  for (int cb = 0; cb < K3_CB; ++cb) {
+    thr[cb] = FLT_MAX;
+    cnt[cb] = 0;
+    const int64_t qi = q0 + 16 * cb + r16;
+    bnd[cb] = qi < Q ? thr0[qi] : FLT_MAX;
+  }
+  const uint64_t qmask = 0x0001000100010001ull << r16;
+  const uint64_t below = (1ull << lane) - 1;
+  const int64_t r0 = (int64_t)slice * rows_per_block;
+  const int64_t r1 = min(N, r0 + rows_per_block);
+  // one-tile software pipeline: the next tile's rows are in flight while this
+  // tile's MFMAs and appends run
+  auto load_tile = [&](int64_t b, float4 (&x)[S4], float (&v)[4]) {
+    const int64_t ra = b + r16;
+    const int64_t rac = ra < r1 ? ra : r0;
+#pragma unroll
+    for (int s = 0; s < S4; ++s) x[s] = reinterpret_cast<const float4*>(tab + rac * DV * 4)[4 * s + g];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = inv[b + 4 * g + i < r1 ? b + 4 * g + i : r0];
+  };
+  float4 xa[S4];
+  float iv[4];
+  if (r0 + 16 * w < r1) load_tile(r0 + 16 * w, xa, iv);
+  for (int64_t base = r0 + 16 * w; base < r1; base += 16 * K2_WPB) {
+    float4 xn[S4];
+    float ivn[4];
+    if (base + 16 * K2_WPB < r1) load_tile(base + 16 * K2_WPB, xn, ivn);
+    const int64_t rb = base + 4 * g;
+#pragma unroll
+    for (int cb = 0; cb < K3_CB; ++cb) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s = 0; s < S4; ++s) {
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s].x, bq[cb][s].x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s].y, bq[cb][s].y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s].z, bq[cb][s].z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s].w, bq[cb][s].w, acc, 0, 0, 0);
+      }
+      float* lcd = cd[w][16 * cb + r16];
+      int* lci = ci[w][16 * cb + r16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float dist = fminf(fmaxf(1.f - acc[i] * iv[i], 0.f), 2.f);
+        const bool pass = rb + i < r1 && dist < thr[cb] && dist <= bnd[cb] && 16 * cb + r16 < nq;
+        const uint64_t m = __ballot(pass);
+        if (!m) continue;
+        const uint64_t mq = m & qmask;
+        if (pass) {
+          const int slot = cnt[cb] + __popcll(mq & below);
+          lcd[slot] = dist;
+          lci[slot] = (int)(rb + i);
+        }
+        cnt[cb] += __popcll(mq);
+      }
+      // keep room for the next tile's (at most 16) appends per query
+      uint64_t need = __ballot(lane < 16 && cnt[cb] > K2_CAP - 16);
+      while (need) {
+        const int q = __builtin_ctzll(need);
+        need &= need - 1;
+        float th;
+        const int c2 = wave_compact(cd[w][16 * cb + q], ci[w][16 * cb + q],
+                                    __builtin_amdgcn_readlane(cnt[cb], q), k, lane, &th);
+        if (r16 == q) { cnt[cb] = c2; thr[cb] = th; }
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < S4; ++s) xa[s] = xn[s];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) iv[i] = ivn[i];
+  }
+#pragma unroll
+  for (int cb = 0; cb < K3_CB; ++cb)
+    for (int q = 0; q < 16 && 16 * cb + q < nq; ++q) {
+      float th;
+      const int c = wave_compact(cd[w][16 * cb + q], ci[w][16 * cb + q],
+                                 __builtin_amdgcn_readlane(cnt[cb], q), k, lane, &th);
+      if (lane == 0) cntl[w][16 * cb + q] = c;
+    }
+  __syncthreads();
+  for (int qq = w; qq < nq; qq += K2_WPB) {
+    float d = FLT_MAX;
+    int i = INT_MAX;
+    for (int ww = 0; ww < K2_WPB; ++ww) {
+      const int c = cntl[ww][qq];
+      const int sl = ww == 0 ? lane : lane - k;
+      if (ww == 0 || lane >= k) {
+        const bool has = sl >= 0 && sl < k && sl < c;
+        d = has ? cd[ww][qq][sl] : FLT_MAX;
+        i = has ? ci[ww][qq][sl] : INT_MAX;
+      }
+      if (ww > 0) wave_sort64(d, i, lane);
+    }
+    Cand* o = out + ((q0 + qq) * nslices + slice) * (int64_t)k;
+    if (lane < k) o[lane] = Cand{d, i};
+  }
+}
+
+// Per-query admission bound for the scans: the k-th smallest distance over
+// the first TH_S rows of the table (+ TH_MARGIN, covering rounding differences
+// between this pass and the scan kernels).  Every row of the true top-k has a
+// distance <= the k-th best of any subset, so rows above the bound are never
+// appended: the wave lists then see a handful of rows instead of refilling
+// and re-sorting while their own thresholds converge.
+constexpr int TH_S = 512;
+constexpr float TH_MARGIN = 1e-5f;
+
+template <int DV>
+__global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict__ tab,
+                                                        const float* __restrict__ inv, int64_t N,
+                                                        const float* __restrict__ qn, int k,
+                                                        float* thr0) {
+  __shared__ float key[TH_S];
+  const int64_t qq = blockIdx.x;
+  const float4* qv = reinterpret_cast<const float4*>(qn + qq * DV * 4);
+  const int S = (int)min<int64_t>(N, TH_S);
+  for (int t = threadIdx.x; t < TH_S; t += 256) {
+    float dist = FLT_MAX;
+    if (t < S) {
+      const float4* rp = reinterpret_cast<const float4*>(tab + (int64_t)t * DV * 4);
+      float4 x[DV];
+#pragma unroll
+      for (int v = 0; v < DV; ++v) x[v] = rp[v];
+      float s = 0.f;
+#pragma unroll
+      for (int v = 0; v < DV; ++v) {
+        const float4 q = qv[v];
+        s += x[v].x * q.x + x[v].y * q.y + x[v].z * q.z + x[v].w * q.w;
+      }
+      dist = fminf(fmaxf(1.f - s * inv[t], 0.f), 2.f);
+    }
+    key[t] = dist;
+  }
+  __syncthreads();
+  for (int k2 = 2; k2 <= TH_S; k2 <<= 1)
+    for (int j = k2 >> 1; j > 0; j >>= 1) {
+      {
+        const int t = threadIdx.x;
+        const int lo = ((t & ~(j - 1)) << 1) | (t & (j - 1)), hi = lo + j;
+        const float a = key[lo], b = key[hi];
+        if (((lo & k2) == 0) == (b < a)) { key[lo] = b; key[hi] = a; }
+      }
+      __syncthreads();
+    }
+  if (threadIdx.x == 0) thr0[qq] = S >= k ? key[k - 1] + TH_MARGIN : FLT_MAX;
+}
+
+__global__ void fill_kernel(float* p, int64_t n, float v) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
 // normalised queries (sklearn normalize(): zero norm -> unchanged), one wave per query
 __global__ void qnorm_kernel(const float* q, int64_t Q, int d, float* qn) {
   const int lane = threadIdx.x & 63;
@@ -299,6 +500,7 @@ __global__ void qnorm_kernel(const float* q, int64_t Q, int d, float* qn) {
 // loaded up front (MT per thread, one round trip), then filtered against the
 // running k-th best and compacted in LDS.
 constexpr int MT = 16;
+constexpr int FT = 24;   // fast path: candidates loaded per thread per round
 // groups > 1: block (query, group) merges lists [g*lpg, (g+1)*lpg) of its
 // query into gout[query][group] (a first stage); groups == 1: the final
 // stage writes idx / dist.
@@ -315,6 +517,44 @@ __global__ __launch_bounds__(NT) void merge_kernel(const Cand* in, int nslices, 
   const int l0 = grp * lpg, nl = max(0, min(lpg, nslices - l0));
   const Cand* c = in + (qq * (int64_t)nslices + l0) * k;
   const int total = nl * k;
+  // fast path: the valid candidates (with admission bounds, a few per query)
+  // fit the buffer -> one gather and one sort
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  for (int base = 0; base < total; base += NT * FT) {
+    Cand e[FT];   // all loads of a round in flight together
+#pragma unroll
+    for (int j = 0; j < FT; ++j) {
+      const int t = base + j * NT + threadIdx.x;
+      e[j] = t < total ? c[t] : Cand{FLT_MAX, INT_MAX};
+    }
+#pragma unroll
+    for (int j = 0; j < FT; ++j)
+      if (e[j].i != INT_MAX) {
+        const int pos = atomicAdd(&cnt, 1);
+        if (pos < CAP) { cd[pos] = e[j].d; ci[pos] = e[j].i; }
+      }
+  }
+  __syncthreads();
+  const int nv = cnt;
+  if (nv <= CAP) {
+    int n2 = 2;
+    while (n2 < nv) n2 <<= 1;
+    for (int t = nv + threadIdx.x; t < n2; t += NT) { cd[t] = FLT_MAX; ci[t] = INT_MAX; }
+    __syncthreads();
+    bitonic(cd, ci, n2);
+    for (int t = threadIdx.x; t < k; t += NT) {
+      const bool ok = t < nv;
+      if (groups > 1) {
+        gout[(qq * groups + grp) * k + t] = Cand{ok ? cd[t] : FLT_MAX, ok ? ci[t] : INT_MAX};
+      } else {
+        idx[qq * k + t] = ok ? (int64_t)ci[t] : -1;
+        dist[qq * k + t] = ok ? cd[t] : FLT_MAX;
+      }
+    }
+    return;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) { cnt = 0; thr = FLT_MAX; }
   __syncthreads();
   for (int base = 0; base < total; base += NT * MT) {
@@ -390,10 +630,23 @@ size_t topk_ws_d(int64_t N, int64_t Q, int k, int d) {
   int ns; int64_t rps;
   if (use_v2(d, k)) {
     plan2(N, &ns, &rps);
-    return rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * d * 4;
+    return rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4;
   }
   plan(N, Q, k, &ns, &rps);
   return (size_t)Q * ns * k * sizeof(Cand);
+}
+
+// Final merge of the per-block k-lists, one block per query.  Measured at
+// 1M rows (512 lists, 5632 candidates per query): this filter-and-compact
+// block 32 us; a two-stage (16 groups, then the group lists) 32 + 16 us; a
+// one-shot 8192-entry bitonic sort by 1024 threads 107 us; a per-wave register
+// merge 50 us -- the block barriers of a one-block kernel dominate all of them.
+dcnr_status merge_lists(const Cand* cands, int64_t Q, int ns, int k, int64_t* idx, float* dist,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(merge_kernel, dim3((unsigned)Q), dim3(NT), 0, s, cands, ns, k, idx, dist, 1,
+                     nullptr);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
 }
 
 // enough for every d (the v2 path keeps Q x d <= Q x 64 normalised queries)
@@ -423,26 +676,53 @@ dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, cons
     float* qn = (float*)((char*)ws + rup((size_t)Q * ns * k * sizeof(Cand), 256));
     hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)cdiv(Q, 4)), dim3(256), 0, s, q, Q, d, qn);
     DCNR_LAUNCH_CHECK();
+    // admission bounds: worth their launch once several queries share a scan
+    float* thr0 = qn + Q * d;
+    if (Q >= 1) {
+      switch (d / 4) {
+#define CASEK(n)                                                                           \
+  case n:                                                                                  \
+    hipLaunchKernelGGL(kth_bound_kernel<n>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, \
+                       qn, k, thr0);                                                       \
+    break;
+        CASEK(1) CASEK(2) CASEK(3) CASEK(4) CASEK(5) CASEK(6) CASEK(7) CASEK(8)
+        CASEK(9) CASEK(10) CASEK(11) CASEK(12) CASEK(13) CASEK(14) CASEK(15) CASEK(16)
+#undef CASEK
+      }
+    } else {
+      hipLaunchKernelGGL(fill_kernel, dim3((unsigned)cdiv(Q, 256)), dim3(256), 0, s, thr0, Q,
+                         FLT_MAX);
+    }
+    DCNR_LAUNCH_CHECK();
+    if (Q >= MFMA_MIN_Q && d % 16 == 0) {
+      const int qtiles = (int)cdiv(Q, K3_QT);
+      const int64_t blocks = rup(ns, 8) * qtiles;
+      switch (d / 16) {
+#define CASE3(n)                                                                                   \
+  case n:                                                                                          \
+    hipLaunchKernelGGL(scan3_kernel<4 * n>, dim3((unsigned)blocks), dim3(K2_NT), 0, s, t, inv, N,  \
+                       qn, Q, k, rps, ns, qtiles, cands, thr0);                                    \
+    break;
+        CASE3(1) CASE3(2) CASE3(3) CASE3(4)
+#undef CASE3
+      }
+      DCNR_LAUNCH_CHECK();
+      return merge_lists(cands, Q, ns, k, idx, dist, s);
+    }
     const int qtiles = (int)cdiv(Q, K2_QT);
     const int64_t blocks = rup(ns, 8) * qtiles;
     switch (d / 4) {
 #define CASE(n)                                                                                  \
   case n:                                                                                        \
     hipLaunchKernelGGL(scan2_kernel<n>, dim3((unsigned)blocks), dim3(K2_NT), 0, s, t, inv, N, qn, \
-                       Q, k, rps, ns, qtiles, cands);                                            \
+                       Q, k, rps, ns, qtiles, cands, thr0);                                      \
     break;
       CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
       CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
 #undef CASE
     }
     DCNR_LAUNCH_CHECK();
-    // (a two-stage merge, 16 list groups per query then the group lists, measured
-    // 32 + 16 us against 33 us for this single stage: the per-block fixed cost
-    // dominates at these candidate counts)
-    hipLaunchKernelGGL(merge_kernel, dim3((unsigned)Q), dim3(NT), 0, s, cands, ns, k, idx, dist, 1,
-                       nullptr);
-    DCNR_LAUNCH_CHECK();
-    return DCNR_OK;
+    return merge_lists(cands, Q, ns, k, idx, dist, s);
   }
   plan(N, Q, k, &ns, &rps);
   dim3 grid(ns, (unsigned)cdiv(Q, QT));

@@ -6,7 +6,7 @@ dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 tab = torch.randn((1_000_000, 64), generator=g, device=dev)
 nn = dcnr.NearestNeighbors(metric="cosine").fit(tab)
-for Q in (1, 8, 32, 256):
+for Q in (1, 4, 8, 32, 256):
     q = tab[torch.randint(0, 1_000_000, (Q,), generator=g, device=dev)]
     for _ in range(3): nn.kneighbors_device(q, 11)
     torch.cuda.synchronize()
@@ -24,3 +24,11 @@ ref = (1 - qn @ tn.T).clamp(0, 2)
 rd, ri = torch.topk(ref, 11, dim=1, largest=False)
 print("max |dist diff|", float((rd - d).abs().max()), "same sets",
       sum(set(a.tolist()) == set(b.tolist()) for a, b in zip(i, ri)), "/ 8")
+for Q in (4, 40, 300):
+    q = tab[torch.randint(0, 1_000_000, (Q,), generator=g, device=dev)]
+    d, i = nn.kneighbors_device(q, 11)
+    qn = q / q.norm(dim=1, keepdim=True)
+    ref = (1 - qn @ tn.T).clamp(0, 2)
+    rd, ri = torch.topk(ref, 11, dim=1, largest=False)
+    print(f"Q={Q}: max |dist diff|", float((rd - d).abs().max()), "same sets",
+          sum(set(a.tolist()) == set(b.tolist()) for a, b in zip(i, ri)), f"/ {Q}")
