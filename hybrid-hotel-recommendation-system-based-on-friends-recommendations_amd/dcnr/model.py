@@ -214,15 +214,16 @@ class DCN_RecSys(nn.Module):
         return (x0, cross) if return_x0 else cross
 
     # ----------------------------------------------------------- flat storage
-    def flatten_(self):
+    def flatten_(self, pad_to: int = 64):
         """Move every parameter into one contiguous fp32 buffer (views keep the
         state_dict API) and give each a ``.grad`` view into one flat gradient
-        buffer: lets the fused optimizer and the DP all-reduce run as single
-        launches.  Returns (flat_params, flat_grads)."""
+        buffer: lets the fused optimizer and the DP exchange run as single
+        launches.  The total length is padded to a multiple of ``pad_to``
+        (the optimizer shards split it evenly).  Returns (flat_params, flat_grads)."""
         params = self.param_tensors()
         dev = params[0].device
         sizes = [((p.numel() + 63) // 64) * 64 for p in params]
-        total = sum(sizes)
+        total = ((sum(sizes) + pad_to - 1) // pad_to) * pad_to
         flat = torch.zeros(total, dtype=torch.float32, device=dev)
         gflat = torch.zeros(total, dtype=torch.float32, device=dev)
         off = 0

@@ -3,8 +3,15 @@
 optimizer.step) as native calls over flat parameter/gradient/moment buffers:
 
     dcnr_forward(train) -> dcnr_bce_with_logits -> dcnr_backward
-      -> [RCCL all-reduce of the flat gradient when data-parallel]
-      -> dcnr_adam_step (one launch over every parameter, dense semantics)
+      -> data-parallel exchange + dcnr_adam_step (dense semantics):
+         world == 1: one launch over every parameter
+         world > 1, shard_optimizer (default): reduce-scatter of the flat
+           gradient (RCCL), AdamW on this rank's 1/world shard of the flat
+           parameters with its 1/world of the moments, all-gather of the
+           updated parameters -- the all-reduce's bytes, 1/world of the
+           optimizer's HBM traffic and moment memory (ZeRO-1 style)
+         world > 1, shard_optimizer=False: all-reduce, then every rank
+           updates everything
 
 Numerically the same update as ``torch.optim.AdamW``/``Adam`` on the
 reference's dense gradients (every embedding row's moments decay every step).
@@ -24,19 +31,24 @@ from .ops import bce_with_logits
 
 class FusedTrainer:
     def __init__(self, model: DCN_RecSys, lr=1e-3, weight_decay=1e-2, optimizer_name='AdamW',
-                 betas=(0.9, 0.999), eps=1e-8, process_group=None, sync_bn=False):
+                 betas=(0.9, 0.999), eps=1e-8, process_group=None, sync_bn=False,
+                 shard_optimizer=None):
         if optimizer_name not in ('AdamW', 'Adam'):
             raise ValueError("optimizer_name must be 'AdamW' or 'Adam' (train.py:201-204)")
         self.model = model
-        self.flat, self.gflat = model.flatten_()
-        self.m = torch.zeros_like(self.flat)
-        self.v = torch.zeros_like(self.flat)
+        self.pg = process_group
+        dist_on = dist.is_available() and dist.is_initialized()
+        self.world = dist.get_world_size(process_group) if dist_on else 1
+        self.rank = dist.get_rank(process_group) if dist_on else 0
+        self.shard = (self.world > 1) if shard_optimizer is None else bool(shard_optimizer)
+        self.flat, self.gflat = model.flatten_(pad_to=64 * self.world)
+        n = self.flat.numel() // (self.world if self.shard else 1)
+        self.m = torch.zeros(n, dtype=torch.float32, device=self.flat.device)
+        self.v = torch.zeros_like(self.m)
+        self.gshard = torch.empty_like(self.m) if self.shard else None
         self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
         self.decoupled = optimizer_name == 'AdamW'
         self.step_count = 0
-        self.pg = process_group
-        self.world = dist.get_world_size(process_group) if (dist.is_available() and
-                                                             dist.is_initialized()) else 1
         self._ws = None
         self._grads = [p.grad for p in model.param_tensors()]   # views into gflat
         if sync_bn and self.world > 1:
@@ -54,18 +66,38 @@ class FusedTrainer:
         loss, dz = bce_with_logits(logits, y, True, 1.0 / self.world)
         run_backward(model, user, item, cat, num, dz, self._ws, self._grads, seed,
                      accumulate=False)
-        if self.world > 1:
-            dist.all_reduce(self.gflat, op=dist.ReduceOp.SUM, group=self.pg)
-        self.optimizer_step()
+        self.exchange_and_update()
         return (loss, logits) if return_logits else loss
 
-    def optimizer_step(self):
-        lib = _lib.load()
+    def exchange_and_update(self, adam=None):
+        """The data-parallel gradient exchange and the optimizer step on the
+        flat buffers.  ``adam(p, g, m, v, step)`` defaults to dcnr_adam_step
+        (the CPU tests pass a host restatement to check the exchange)."""
+        adam = adam or self._adam
         self.step_count += 1
-        n = (ctypes.c_int64 * 1)(self.flat.numel())
-        _lib.check(lib.dcnr_adam_step(1, _lib.ptr_array([self.flat]), _lib.ptr_array([self.gflat]),
-                                      _lib.ptr_array([self.m]), _lib.ptr_array([self.v]), n,
+        if self.world > 1 and self.shard:
+            n = self.m.numel()
+            dist.reduce_scatter_tensor(self.gshard, self.gflat, op=dist.ReduceOp.SUM,
+                                       group=self.pg)
+            pshard = self.flat[self.rank * n:(self.rank + 1) * n]
+            adam(pshard, self.gshard, self.m, self.v, self.step_count)
+            dist.all_gather_into_tensor(self.flat, pshard, group=self.pg)
+            return
+        if self.world > 1:
+            dist.all_reduce(self.gflat, op=dist.ReduceOp.SUM, group=self.pg)
+        adam(self.flat, self.gflat, self.m, self.v, self.step_count)
+
+    def optimizer_step(self):
+        """Adam/AdamW over the local flat gradient (no exchange)."""
+        self.step_count += 1
+        self._adam(self.flat, self.gflat, self.m, self.v, self.step_count)
+
+    def _adam(self, p, g, m, v, step):
+        lib = _lib.load()
+        n = (ctypes.c_int64 * 1)(p.numel())
+        _lib.check(lib.dcnr_adam_step(1, _lib.ptr_array([p]), _lib.ptr_array([g]),
+                                      _lib.ptr_array([m]), _lib.ptr_array([v]), n,
                                       float(self.lr), float(self.betas[0]), float(self.betas[1]),
-                                      float(self.eps), float(self.wd), self.step_count,
+                                      float(self.eps), float(self.wd), int(step),
                                       1 if self.decoupled else 0,
-                                      _lib.stream_ptr(self.flat.device)), "dcnr_adam_step")
+                                      _lib.stream_ptr(p.device)), "dcnr_adam_step")

@@ -176,3 +176,52 @@ def _grad_worker(rank, world, port):
 
 def test_dp_gradient_exchange_gloo_world2():
     _run(_grad_worker)
+
+
+def _host_adam(p, g, m, v, step, lr=1e-2, b1=0.9, b2=0.999, eps=1e-8, wd=1e-2):
+    """torch.optim.AdamW's update (train.py:201-204) on host tensors, in place."""
+    p.mul_(1 - lr * wd)
+    m.lerp_(g, 1 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1 - b2)
+    denom = (v.sqrt() / (1 - b2 ** step) ** 0.5).add_(eps)
+    p.addcdiv_(m, denom, value=-lr / (1 - b1 ** step))
+
+
+def _exchange_worker(rank, world, port):
+    _init(rank, world, port)
+    try:
+        import dcnr
+        for shard in (True, False):
+            torch.manual_seed(0)
+            m = dcnr.DCN_RecSys(50, 40, {"a": 10, "b": 3}, 3,
+                                dict(emb_dim=8, hidden_dim=16, n_cross_layers=1, n_res_blocks=1,
+                                     dropout=0.0))
+            tr = dcnr.FusedTrainer(m, lr=1e-2, weight_decay=1e-2, shard_optimizer=shard)
+            assert tr.flat.numel() % (64 * world) == 0
+            assert tr.m.numel() == tr.flat.numel() // (world if shard else 1)
+            ref_p = tr.flat.clone()
+            ref_m = torch.zeros_like(ref_p)
+            ref_v = torch.zeros_like(ref_p)
+            for step in range(1, 4):
+                gs = [torch.Generator().manual_seed(100 * step + r) for r in range(world)]
+                grads = [torch.randn(tr.flat.numel(), generator=gg) for gg in gs]
+                tr.gflat.copy_(grads[rank])
+                tr.exchange_and_update(adam=_host_adam)
+                _host_adam(ref_p, sum(grads), ref_m, ref_v, step)
+                np.testing.assert_allclose(tr.flat.numpy(), ref_p.numpy(), rtol=2e-6, atol=1e-7)
+                # every rank holds the same parameters, bit for bit
+                allp = [torch.empty_like(tr.flat) for _ in range(world)]
+                dist.all_gather(allp, tr.flat)
+                assert all(torch.equal(allp[0], a) for a in allp[1:])
+            # the module's parameters are views of the exchanged flat buffer
+            assert m.final_linear.weight.data_ptr() >= tr.flat.data_ptr()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_optimizer_exchange_matches_allreduce_adam(world):
+    """FusedTrainer's data-parallel exchange (reduce-scatter -> AdamW on the
+    rank's shard -> all-gather, and the all-reduce variant) gives every rank
+    the single-process AdamW update of the summed gradient."""
+    _run(_exchange_worker, world)
