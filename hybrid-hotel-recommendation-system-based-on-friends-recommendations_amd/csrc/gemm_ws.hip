@@ -45,15 +45,24 @@ template <int EPI> constexpr int ws_tm() {
   return EPI == NT_EPI_RESID ? 32 : EPI == NT_EPI_RESID_BN ? 32 : EPI == NT_EPI_DROP_BN ? 64 : WS_TM_PLAIN;
 }
 template <int EPI> constexpr bool ws_ops_early() { return EPI == NT_EPI_RESID_BN; }
+// X-tile buffers in the LDS ring: the next NB-1 tiles are in flight while one
+// is consumed.  Only the epilogues without operand loads can use NB > 2 (an
+// operand load's wait would also wait for every older tile DMA).
+#ifndef WS_NB_PLAIN
+#define WS_NB_PLAIN 2
+#endif
+template <int EPI> constexpr int ws_nb() {
+  return (EPI == NT_EPI_BIAS || EPI == NT_EPI_BIAS_STATS || EPI == NT_EPI_F32) ? WS_NB_PLAIN : 2;
+}
 
-template <int KTP, int TM> struct WsCfg {
+template <int KTP, int TM, int NB = 2> struct WsCfg {
   static constexpr int P = KTP * 64;                      // LDS bytes per X row
   static constexpr int CPR = KTP * 4;                     // 16-B chunks per row
   static constexpr int TILE = TM * P;                     // bytes per X buffer
   static constexpr int RPD = 1024 / P;                    // rows per DMA wave-instruction
   static constexpr int DPW = TM / RPD / WS_WAVES;         // DMAs per wave per tile
   static constexpr int RB = TM / 16;                      // 16-row blocks per tile
-  static constexpr size_t LDS_BYTES = 2 * (size_t)TILE + 3 * WS_TN * 4 + 16;   // + hand-off flag
+  static constexpr size_t LDS_BYTES = NB * (size_t)TILE + 3 * WS_TN * 4 + 16;  // + hand-off flag
 };
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -102,7 +111,8 @@ __device__ __forceinline__ void issue_tile(u32x4 xr, int64_t ldx, int K, uint32_
 template <int KTP, int EPI>
 __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   constexpr int WS_TM = ws_tm<EPI>();
-  using C = WsCfg<KTP, WS_TM>;
+  constexpr int NB = ws_nb<EPI>();
+  using C = WsCfg<KTP, WS_TM, NB>;
   constexpr int WS_RB = C::RB;
   constexpr bool STATS = EPI >= NT_EPI_BIAS_STATS;
   constexpr bool HAS_R = EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN;
@@ -125,7 +135,11 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     return rsrc_words(a.X + m0 * a.ldx, rows > 0 ? rows * a.ldx * 2 : 0);
   };
   const uint32_t lbase = lds_addr(lds);
-  if (group < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(group), a.ldx, a.K, lbase, wave, lane);
+#pragma unroll
+  for (int j = 0; j < NB - 1; ++j)
+    if (group + (int64_t)j * groups < a.mtiles)
+      issue_tile<KTP, WS_TM>(tile_rsrc(group + (int64_t)j * groups), a.ldx, a.K, lbase + j * C::TILE,
+                             wave, lane);
 
   // resident W: fragments (column block cb, k-step kt) of columns nw + 16cb + l15
   bf16x8 wf[2][KTP];
@@ -145,7 +159,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     }
   }
   // per-column constants of the slice: bias, -mean*invstd, invstd
-  float* bias_s = reinterpret_cast<float*>(lds + 2 * C::TILE);
+  float* bias_s = reinterpret_cast<float*>(lds + NB * C::TILE);
   float* nmi_s = bias_s + WS_TN;
   float* istd_s = bias_s + 2 * WS_TN;
   for (int c = tid; c < WS_TN; c += WS_NT) {
@@ -181,9 +195,10 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   // fragment read offsets: row rb*16 + l15, chunk (4kt + q) ^ l15
   const uint32_t rowoff = (uint32_t)l15 * C::P;
   int buf = 0;
-  for (int64_t mt = group; mt < a.mtiles; mt += groups, buf ^= 1) {
-    const int64_t mn = mt + groups;
-    if (mn < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + (buf ^ 1) * C::TILE, wave, lane);
+  for (int64_t mt = group; mt < a.mtiles; mt += groups, buf = buf + 1 == NB ? 0 : buf + 1) {
+    const int64_t mn = mt + (int64_t)(NB - 1) * groups;
+    const int nbuf = buf + NB - 1 >= NB ? buf - 1 : buf + NB - 1;   // (buf + NB - 1) % NB
+    if (mn < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + nbuf * C::TILE, wave, lane);
     const int64_t m0 = mt * WS_TM;
     const int nst = nw + (q & 1) * 16 + (q >> 1) * 8;   // store-layout column
     // epilogue operands (WS_OPS_EARLY: all issued before the MFMAs, else one
@@ -333,10 +348,16 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
           __builtin_amdgcn_raw_buffer_store_b128(sv, cr, off, 0, 0);
       }
     }
-    // next tile's X landed (this wave's DMAs are older than its epilogue's
-    // stores) and every wave is done reading this buffer
+    // next tile's X landed and every wave is done reading this buffer.  Younger
+    // than the next tile's DMAs: the stores of the last NB-1 tiles and the
+    // DMAs of the NB-2 tiles after it -- when all of those were issued (near
+    // the end some prefetches are not) the count below is exact, else wait all
     constexpr int NSTORE = (EPI == NT_EPI_F32 ? 2 : 1) * WS_RB;
-    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NSTORE) : "memory");
+    constexpr int NWAIT = (NB - 1) * NSTORE + (NB - 2) * C::DPW;
+    if (NB == 2 || mn < a.mtiles)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NWAIT) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
   if constexpr (STATS) {
     // 16-lane butterfly: lane (q, m) ends with k = bit2(m), cb = bit3(m),
@@ -358,7 +379,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     if (a.fin) {
       // the last workgroup of this column slice to finish sums the slice's
       // partial rows in fixed group order (fp64) and finalises the columns
-      int* flag = reinterpret_cast<int*>(lds + 2 * C::TILE + 3 * WS_TN * 4);
+      int* flag = reinterpret_cast<int*>(lds + NB * C::TILE + 3 * WS_TN * 4);
       if (last_arriver(a.rf.counter + slice, groups, flag) && tid < WS_TN) {
         const int nc = n0 + tid;
         if (nc < a.N) {
@@ -390,7 +411,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
 template <int KTP, int EPI>
 dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   constexpr int WS_TM = ws_tm<EPI>();
-  using C = WsCfg<KTP, WS_TM>;
+  using C = WsCfg<KTP, WS_TM, ws_nb<EPI>()>;
   static bool attr_set = false;
   if (!attr_set) {
     DCNR_HIP(hipFuncSetAttribute((const void*)gemm_ws_kernel<KTP, EPI>,

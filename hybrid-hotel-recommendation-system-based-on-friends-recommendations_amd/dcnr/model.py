@@ -121,12 +121,56 @@ class DCN_RecSys(nn.Module):
             desc.bn_allreduce = self.bn_allreduce
         return desc
 
+    # Host-side dispatch cost matters for small serving batches: building
+    # state_dict() per call costs ~150 us, so the (dict, key) slot of every
+    # state tensor is resolved once (state_dict order) and the device-pointer
+    # table is rebuilt only when a pointer changed (.to(), .data = ...).
+    def __setattr__(self, name, value):
+        if isinstance(value, nn.Module) and '_slots' in self.__dict__:
+            self.__dict__['_slots'] = None
+        super().__setattr__(name, value)
+
+    def __getstate__(self):   # pickle / deepcopy: the caches are rebuilt on use
+        st = self.__dict__.copy()
+        st.pop('_slots', None)
+        st.pop('_ptr_cache', None)
+        return st
+
+    def _state_slots(self):
+        slots = self.__dict__.get('_slots')
+        if slots is None:
+            slots = []
+            for name in self.state_dict(keep_vars=True).keys():
+                path, attr = name.rsplit('.', 1)
+                mod = self.get_submodule(path)
+                is_p = attr in mod._parameters
+                slots.append(((mod._parameters if is_p else mod._buffers), attr, is_p))
+            self.__dict__['_slots'] = slots
+            self.__dict__['_ptr_cache'] = None
+        return slots
+
     def state_tensors(self) -> List[torch.Tensor]:
         """All state_dict tensors in state_dict order (params + BN buffers)."""
-        return [t for t in self.state_dict(keep_vars=True).values()]
+        return [d[k] for d, k, _ in self._state_slots()]
 
     def param_tensors(self) -> List[torch.Tensor]:
-        return [p for _, p in self.named_parameters()]
+        """named_parameters() order (state_dict order without the buffers)."""
+        return [d[k] for d, k, is_p in self._state_slots() if is_p]
+
+    def state_ptr_array(self):
+        """ctypes array of the state tensors' device pointers (state_dict order),
+        validated (fp32/int64, contiguous) whenever a pointer changed."""
+        ts = self.state_tensors()
+        key = tuple(t.data_ptr() for t in ts)
+        cache = self.__dict__.get('_ptr_cache')
+        if cache is not None and cache[0] == key:
+            return cache[1]
+        for t in ts:
+            if t.dtype not in (torch.float32, torch.int64) or not t.is_contiguous():
+                raise RuntimeError("dcnr requires fp32 contiguous parameters")
+        arr = _lib.ptr_array(ts)
+        self.__dict__['_ptr_cache'] = (key, arr)
+        return arr
 
     def workspace_bytes(self, B: int, mode: int) -> int:
         lib = _lib.load()
@@ -144,9 +188,6 @@ class DCN_RecSys(nn.Module):
         for t in tensors:
             if t.device != dev:
                 raise RuntimeError(f"input on {t.device} but model on {dev}")
-        for t in self.state_tensors():
-            if t.dtype not in (torch.float32, torch.int64) or not t.is_contiguous():
-                raise RuntimeError("dcnr requires fp32 contiguous parameters")
         return dev
 
     def forward(self, user_ids, item_ids, cat_features, num_features):
@@ -201,7 +242,7 @@ class DCN_RecSys(nn.Module):
         flag = torch.zeros(1, dtype=torch.int32, device=dev) if self.check_indices else None
         lib = _lib.load()
         desc = self.desc()
-        _lib.check(lib.dcnr_gather_cross(ctypes.byref(desc), _lib.ptr_array(self.state_tensors()),
+        _lib.check(lib.dcnr_gather_cross(ctypes.byref(desc), self.state_ptr_array(),
                                          user_ids.data_ptr(), item_ids.data_ptr(),
                                          cat_features.data_ptr() if cat_features.numel() else None,
                                          num_features.data_ptr() if num_features.numel() else None,
@@ -254,7 +295,7 @@ def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     logits = torch.empty(B, dtype=torch.float32, device=dev)
-    state = _lib.ptr_array(model.state_tensors())
+    state = model.state_ptr_array()
     desc = model.desc()
     model._active_ws = ws          # the SyncBN hook (dcnr.parallel) maps pointers into it
     st = lib.dcnr_forward(ctypes.byref(desc), state, user.data_ptr(), item.data_ptr(),
@@ -277,7 +318,7 @@ def run_backward(model: DCN_RecSys, user, item, cat, num, dlogits, ws, grads: Li
     B = user.shape[0]
     desc = model.desc()
     model._active_ws = ws
-    st = lib.dcnr_backward(ctypes.byref(desc), _lib.ptr_array(model.state_tensors()),
+    st = lib.dcnr_backward(ctypes.byref(desc), model.state_ptr_array(),
                            _lib.ptr_array(grads), user.data_ptr(), item.data_ptr(),
                            cat.data_ptr() if cat.numel() else None,
                            num.data_ptr() if num.numel() else None, B,

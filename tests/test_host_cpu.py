@@ -79,3 +79,31 @@ def test_bad_precision_rejected():
     with pytest.raises(ValueError):
         dcnr.DCN_RecSys(3, 3, {}, 1, dict(emb_dim=4, hidden_dim=8, n_cross_layers=1, dropout=0.0),
                         precision="fp8")
+
+
+def test_state_dict_file_roundtrip_and_flat_views(tmp_path):
+    """On-disk compatibility: the reference saves
+    ``model.state_dict()`` with torch.save (train.py:391) and main.py loads it
+    with load_state_dict (main.py:264); item_embeddings.npy is the item table
+    (train.py:393-394).  Our module round-trips the same file format, also
+    after FusedTrainer moved the parameters into its flat buffer."""
+    import numpy as np
+    import torch
+    import dcnr
+    cfg = gc.CFG1
+    a = our_model(cfg)
+    path = tmp_path / "final_dcn_model.pth"
+    torch.save(a.state_dict(), path)
+    b = dcnr.DCN_RecSys(cfg["n_users"], cfg["n_items"], cfg["cat_dims"], cfg["n_num"],
+                        dict(cfg["params"]))
+    tr = dcnr.FusedTrainer(b, lr=1e-3)          # parameters now views of tr.flat
+    b.load_state_dict(torch.load(path, weights_only=True))
+    for (k, x), (k2, y) in zip(a.state_dict().items(), b.state_dict().items()):
+        assert k == k2 and torch.equal(x, y), k
+    # the loaded values live in the trainer's flat buffer
+    w = b.final_linear.weight
+    off = (w.data_ptr() - tr.flat.data_ptr()) // 4
+    assert torch.equal(tr.flat[off:off + w.numel()], w.reshape(-1))
+    np.save(tmp_path / "item_embeddings.npy", b.item_embedding.weight.detach().numpy())
+    emb = np.load(tmp_path / "item_embeddings.npy")
+    assert emb.shape == (cfg["n_items"], cfg["params"]["emb_dim"]) and emb.dtype == np.float32
