@@ -25,7 +25,7 @@
 #include "dcnr_internal.h"
 
 #ifndef WS_LAB_MODE
-#define WS_LAB_MODE 0   // tools/ws_lab.hip: 1 no C stores, 2 no X DMAs, 4 no MFMAs
+#define WS_LAB_MODE 0   // tools/ws_lab.hip: 1 no C stores, 2 no X DMAs, 4 no MFMAs, 8 no epilogue
 #endif
 
 namespace dcnr {
@@ -253,6 +253,12 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     }
 
     // ---- epilogue: lane holds C[m][nw + 16cb + 4q .. +3], m = m0 + 16rb + l15
+    if constexpr (WS_LAB_MODE & 8) {   // lab: no epilogue (keep acc alive)
+      float t = 0.f;
+#pragma unroll
+      for (int rb = 0; rb < WS_RB; ++rb) t += acc[rb][0][0] + acc[rb][1][3];
+      if (t == 12345.f) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), cr, 0, 0, 0);
+    } else
 #pragma unroll
     for (int rb = 0; rb < WS_RB; ++rb) {
       const int64_t m = m0 + rb * 16 + l15;
