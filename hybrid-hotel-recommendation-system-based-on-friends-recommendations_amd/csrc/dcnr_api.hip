@@ -875,6 +875,18 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   return DCNR_OK;
 }
 
+dcnr_status dcnr_gather_rows(const int64_t* idx, int64_t n, int64_t n_src, int32_t n_arrays,
+                             const void* const* src, void* const* dst, const int64_t* row_bytes,
+                             dcnr_stream_t stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (!src || !dst || !row_bytes || (n > 0 && !idx)) {
+    set_error("dcnr_gather_rows: null argument");
+    return DCNR_BAD_ARG;
+  }
+  TRYP(DCNR_K_SERVE, gather_rows(idx, n, n_src, n_arrays, src, dst, row_bytes, s));
+  return DCNR_OK;
+}
+
 dcnr_status dcnr_candidate_union(const int64_t* positives, int64_t Q, const int64_t* knn_idx,
                                  int32_t k, int64_t* out_rows, int32_t* out_count,
                                  dcnr_stream_t stream) {

@@ -496,6 +496,9 @@ dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, cons
                         hipStream_t s);
 
 // serving (serving.hip)
+dcnr_status gather_rows(const int64_t* idx, int64_t n, int64_t n_src, int n_arrays,
+                        const void* const* src, void* const* dst, const int64_t* row_bytes,
+                        hipStream_t s);
 dcnr_status candidate_union(const int64_t* pos, int64_t Q, const int64_t* idx, int k,
                             int64_t* out, int32_t* out_count, hipStream_t s);
 dcnr_status ranking_batch(const int64_t* rows, int64_t n, int64_t user_row, const int64_t* item_cat,

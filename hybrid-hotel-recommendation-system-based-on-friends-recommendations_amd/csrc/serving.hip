@@ -205,7 +205,58 @@ __global__ __launch_bounds__(SV_NT) void mmr_kernel(const float* table, const fl
   if (threadIdx.x == 0) *out_count = cnt;
 }
 
+// Batch assembly of a device-resident dataset (the DataLoader of
+// train.py:195-196): dst_a[i] = src_a[idx[i]] for each array a, whole rows of
+// row_bytes (a multiple of 4) copied as dwords, one wave per (row, array).
+struct RowGather {
+  const char* src[8];
+  char* dst[8];
+  int64_t row_bytes[8];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void gather_rows_kernel(const int64_t* idx, int64_t n,
+                                                          int64_t n_src, RowGather g) {
+  const int64_t w = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (w >= n * g.n) return;
+  const int a = (int)(w % g.n);
+  const int64_t i = w / g.n;
+  int64_t r = idx[i];
+  r = r < 0 ? 0 : (r >= n_src ? n_src - 1 : r);
+  const int64_t words = g.row_bytes[a] >> 2;
+  const uint32_t* s = reinterpret_cast<const uint32_t*>(g.src[a] + r * g.row_bytes[a]);
+  uint32_t* d = reinterpret_cast<uint32_t*>(g.dst[a] + i * g.row_bytes[a]);
+  for (int64_t k = lane; k < words; k += 64) d[k] = s[k];
+}
+
 }  // namespace
+
+dcnr_status gather_rows(const int64_t* idx, int64_t n, int64_t n_src, int n_arrays,
+                        const void* const* src, void* const* dst, const int64_t* row_bytes,
+                        hipStream_t s) {
+  if (n_arrays < 1 || n_arrays > 8 || n < 0 || n_src < 1) {
+    set_error("gather_rows: 1..8 arrays, n_src >= 1");
+    return DCNR_BAD_ARG;
+  }
+  RowGather g;
+  g.n = n_arrays;
+  for (int a = 0; a < n_arrays; ++a) {
+    if (!src[a] || !dst[a] || row_bytes[a] <= 0 || row_bytes[a] % 4) {
+      set_error("gather_rows: array %d: null pointer or row bytes %lld not a multiple of 4", a,
+                (long long)row_bytes[a]);
+      return DCNR_BAD_ARG;
+    }
+    g.src[a] = (const char*)src[a];
+    g.dst[a] = (char*)dst[a];
+    g.row_bytes[a] = row_bytes[a];
+  }
+  if (n == 0) return DCNR_OK;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3((unsigned)cdiv(n * n_arrays, 4)), dim3(256), 0, s,
+                     idx, n, n_src, g);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
 
 dcnr_status candidate_union(const int64_t* pos, int64_t Q, const int64_t* idx, int k,
                             int64_t* out, int32_t* out_count, hipStream_t s) {

@@ -8,6 +8,7 @@ System-Based-on-Friends-Recommendations):
   AdamW, Adam                        train.py:201-204
   NearestNeighbors (cosine, brute)   main.py:268-270
   FusedTrainer                       the train.py:219-226 inner-loop step
+  DeviceLoader                       TensorDataset + DataLoader (train.py:195-196)
   serving.rerank_with_mmr            main.py:133-169
   serving.RankingPipeline            the /recommendations + /similar_items core
                                      (main.py:196-230, 294-332)
@@ -19,6 +20,7 @@ from .ops import Adam, AdamW, BCEWithLogitsLoss, bce_with_logits  # noqa: F401
 from .knn import NearestNeighbors  # noqa: F401
 from .train import FusedTrainer  # noqa: F401
 from . import serving  # noqa: F401
+from .data import DeviceLoader  # noqa: F401
 from .serving import RankingPipeline, rerank_with_mmr  # noqa: F401
 
 __version__ = "0.1.0"

@@ -19,6 +19,8 @@
  *   dcnr_cosine_topk      NearestNeighbors(metric='cosine', algorithm='brute')
  *                         .kneighbors(vec, n_neighbors=k)      main.py:196-203,268-270,300
  *   dcnr_row_inv_norms    the row normalisation inside sklearn's cosine metric
+ *   dcnr_gather_rows      the batch assembly of TensorDataset + DataLoader
+ *                         (train.py:195-196) on a device-resident dataset
  *   dcnr_candidate_union  _generate_candidates' union of positives and their
  *                         neighbours[1:]                      main.py:196-203
  *   dcnr_ranking_batch    preprocess_for_ranking              main.py:215-230
@@ -183,6 +185,14 @@ size_t dcnr_cosine_topk_workspace_size(int64_t N, int64_t Q, int32_t k);
 dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t N, int32_t d,
                              const float* queries, int64_t Q, int32_t k, int64_t* idx,
                              float* dist, void* ws, size_t ws_bytes, dcnr_stream_t stream);
+
+/* Batch assembly of a device-resident dataset (TensorDataset + DataLoader,
+ * train.py:195-196): for each of n_arrays (<= 8) arrays of n_src rows of
+ * row_bytes[a] bytes (a multiple of 4), dst[a] row i = src[a] row idx[i]
+ * (idx clamped to [0, n_src)).  Host arrays of device pointers. */
+dcnr_status dcnr_gather_rows(const int64_t* idx, int64_t n, int64_t n_src, int32_t n_arrays,
+                             const void* const* src, void* const* dst, const int64_t* row_bytes,
+                             dcnr_stream_t stream);
 
 /* ---- serving: the steps either side of scoring in /recommendations ----
  * All operate on at most 4096 items per call (DCNR_UNSUPPORTED_SHAPE above). */

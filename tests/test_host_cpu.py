@@ -107,3 +107,18 @@ def test_state_dict_file_roundtrip_and_flat_views(tmp_path):
     np.save(tmp_path / "item_embeddings.npy", b.item_embedding.weight.detach().numpy())
     emb = np.load(tmp_path / "item_embeddings.npy")
     assert emb.shape == (cfg["n_items"], cfg["params"]["emb_dim"]) and emb.dtype == np.float32
+
+
+def test_device_loader_permutation_is_dataloaders():
+    """DeviceLoader's epoch order is the reference DataLoader(shuffle=True)'s
+    (train.py:195-196) for the same global seed state."""
+    import torch
+    from torch.utils.data import DataLoader, TensorDataset
+    from dcnr.data import randomsampler_permutation
+    n = 1000
+    for seed in (0, 7):
+        torch.manual_seed(seed)
+        ref = torch.cat([b[0] for b in DataLoader(TensorDataset(torch.arange(n)), batch_size=64,
+                                                  shuffle=True)])
+        torch.manual_seed(seed)
+        assert torch.equal(randomsampler_permutation(n), ref)

@@ -108,3 +108,25 @@ def test_recommend_matches_oracle(dev, lam):
     excluded = {int(cand[0])}
     rows2, _ = pipe.recommend(user, pos, 1.0, allowed=allowed, excluded=excluded)
     assert set(rows2.cpu().tolist()) == (allowed - excluded)
+
+
+def test_device_loader_matches_dataloader(dev):
+    """Batches of dcnr.DeviceLoader == TensorDataset + DataLoader(shuffle=True)
+    batches (train.py:195-196), bit for bit, including the partial last one."""
+    from torch.utils.data import DataLoader, TensorDataset
+    import dcnr
+    rng = np.random.default_rng(0)
+    n, K, F = 1003, 5, 3
+    collab = torch.from_numpy(rng.integers(0, 1000, (n, 2)))
+    cat = torch.from_numpy(rng.integers(0, 50, (n, K)))
+    num = torch.from_numpy(rng.random((n, F), dtype=np.float32))
+    y = torch.from_numpy((rng.random(n) < 0.5).astype(np.float32))
+    for shuffle in (True, False):
+        torch.manual_seed(3)
+        ref = list(DataLoader(TensorDataset(collab, cat, num, y), batch_size=128, shuffle=shuffle))
+        torch.manual_seed(3)
+        got = list(dcnr.DeviceLoader(collab, cat, num, y, batch_size=128, shuffle=shuffle))
+        assert len(got) == len(ref) == 8
+        for g, r in zip(got, ref):
+            for a, b in zip(g, r):
+                assert torch.equal(a.cpu(), b)
