@@ -176,10 +176,17 @@ struct Layout {
   // backward
   void* G; void* dt2; void* du; void* da;
   float* dx0; float* slab; int64_t slab_elems; float* cpart; size_t cpart_elems;
+  // 1-bit keep masks for the backward GEMM epilogues (bf16, Hp % 32 == 0):
+  // mask_a1[j] = [a1_j != 0], mask_h[j] = [h_j > 0] (j >= 1)
+  uint8_t* mask_a1[MAX_RES]; uint8_t* mask_h[MAX_RES + 1];
   float* cred2; size_t cred2_elems;             // cross partial second stage
   double* bce_part;
   size_t total;
 };
+
+// the backward GEMM epilogues read 1-bit keep masks (bf16 path, mask rows of
+// whole 32-bit words) instead of the bf16 activations
+bool masks_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && d.Hp % 32 == 0; }
 
 Layout make_layout(const Dims& d, int64_t B, int mode, void* ws) {
   Layout L;
@@ -214,6 +221,11 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws) {
   L.a1 = b.take(act);
   if (train)
     for (int j = 0; j < d.R; ++j) L.a1s[j] = b.take(act);
+  if (train && masks_ok(d)) {
+    const size_t mb = (size_t)B * d.Hp / 8;
+    for (int j = 0; j < d.R; ++j) L.mask_a1[j] = (uint8_t*)b.take(mb);
+    for (int j = 1; j < d.R; ++j) L.mask_h[j] = (uint8_t*)b.take(mb);
+  }
   L.zc = (float*)b.take(B * 4);
   L.zdeep = (float*)b.take(B * 4);
   for (int i = 0; i < 2 * d.R; ++i) {
@@ -444,8 +456,8 @@ dcnr_status linear_fwd_stats(const dcnr_model_desc* desc, const Dims& d, const L
 // C = mask(H) * (X W^T [+ R]) and part = [sum C, sum C*xhat(T)] (BN backward)
 dcnr_status linear_dx_bn(const dcnr_model_desc* desc, const Dims& d, const Layout& L, int epi,
                          const void* X, const void* Wt, const void* R, void* C, const void* H,
-                         float hscale, const void* T, const BnBufs& bn, int64_t B,
-                         const RedFinal& rf, int* nc, int* fin_done, hipStream_t s) {
+                         const uint8_t* Hbits, float hscale, const void* T, const BnBufs& bn,
+                         int64_t B, const RedFinal& rf, int* nc, int* fin_done, hipStream_t s) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
   a.X = (const bf16*)X; a.ldx = d.Hp; a.M = B; a.K = d.Hp;
@@ -453,6 +465,7 @@ dcnr_status linear_dx_bn(const dcnr_model_desc* desc, const Dims& d, const Layou
   a.C = C; a.ldc = d.Hp;
   a.R = R; a.ldr = d.Hp;
   a.H = (const bf16*)H; a.ldh = d.Hp; a.hscale = hscale;
+  a.Hb = (const uint32_t*)Hbits; a.ldhb = d.Hp / 32;
   a.T = (const bf16*)T; a.ldt = d.Hp;
   a.mean = bn.mean; a.invstd = bn.invstd;
   a.part = L.part;
@@ -713,7 +726,7 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
                        L.bn[2 * j], s, nc, fuse ? L.b1p[j] : nullptr));
     void* a1 = train ? L.a1s[j] : L.a1;
     TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
-                     dropout_seed, j, s));
+                     dropout_seed, j, s, train ? L.mask_a1[j] : nullptr));
     if (fuse)
       TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(desc, d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j],
                                              L.t2[j], B,
@@ -732,7 +745,8 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
                                             d.H, L.zc, P.bf, logits, s));
     else
       TRYP(DCNR_K_ROWWISE, bn_add_relu2(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
-                                        L.bn[2 * j + 1].scale, L.bn[2 * j + 1].shift, s));
+                                        L.bn[2 * j + 1].scale, L.bn[2 * j + 1].shift, s,
+                                        train && j + 1 < d.R ? L.mask_h[j + 1] : nullptr));
   }
   if (!bn_add_relu_head_supported(d.prec, d.Hp)) {
     TRYP(DCNR_K_HEAD, row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
@@ -803,7 +817,8 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       // saved activation, BN1 partials (and, without SyncBN, its backward
       // coefficients and dgamma/dbeta) in the same pass
       TRYP(DCNR_K_GEMM_DX, linear_dx_bn(desc, d, L, NT_EPI_DROP_BN, L.dt2, L.W2t[j], nullptr, L.da,
-                                        L.a1s[j], p > 0.f ? 1.f / (1.f - p) : 1.f, L.t1[j], bn1,
+                                        L.a1s[j], L.mask_a1[j], p > 0.f ? 1.f / (1.f - p) : 1.f,
+                                        L.t1[j], bn1,
                                         B,
                                         bn_bwd_rf(L, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr,
                                                   Gk.b1, accumulate),
@@ -830,7 +845,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       // (in place over this block's du, the residual operand) and the partials
       const BnBufs& bp = L.bn[2 * (j - 1) + 1];
       TRYP(DCNR_K_GEMM_DX, linear_dx_bn(desc, d, L, NT_EPI_RESID_BN, L.a1, L.W1t[j], L.du, L.du,
-                                        L.h[j], 1.f, L.t2[j - 1], bp, B,
+                                        L.h[j], L.mask_h[j], 1.f, L.t2[j - 1], bp, B,
                                         bn_bwd_rf(L, B, P.blk[j - 1].g2, bp.invstd,
                                                   Gr.blk[j - 1].g2, Gr.blk[j - 1].be2, nullptr,
                                                   Gr.blk[j - 1].b2, accumulate),

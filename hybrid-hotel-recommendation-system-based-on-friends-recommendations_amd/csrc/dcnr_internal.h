@@ -319,6 +319,8 @@ struct NtArgs {
   const float* bias;
   const void* R; int64_t ldr;
   const bf16* H; int64_t ldh; float hscale;         // mask source (RESID_BN, DROP_BN)
+  const uint32_t* Hb; int64_t ldhb;                 // or its 1-bit image (gemm_ws): bit c%32
+                                                    // of word [m][c/32] = keep column c
   const bf16* T; int64_t ldt;                       // BN input for xhat
   const float* mean; const float* invstd;
   float* part;                                      // column partials (stats epilogues)
@@ -433,13 +435,15 @@ dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, 
 dcnr_status bn_bwd_coef(const double* sums, int N, int Nr, const float* gamma, const float* invstd,
                         float* coef, int train, hipStream_t s);
 
-// a = dropout(relu(t*scale+shift))
+// a = dropout(relu(t*scale+shift)); bits (bf16 only, may be null): the 1-bit
+// image [B][ld/8 bytes] of a != 0 (bit c%8 of byte c/8 of the row)
 dcnr_status bn_relu_drop(int precision, const void* t, void* a, int64_t B, int N, int ld,
                          const float* scale, const float* shift, float p, uint64_t seed,
-                         int layer, hipStream_t s);
-// out = relu(t*scale + shift + x)
+                         int layer, hipStream_t s, uint8_t* bits = nullptr);
+// out = relu(t*scale + shift + x); bits: the 1-bit image of out > 0
 dcnr_status bn_add_relu2(int precision, const void* t, const void* x, void* out, int64_t B, int N,
-                         int ld, const float* scale, const float* shift, hipStream_t s);
+                         int ld, const float* scale, const float* shift, hipStream_t s,
+                         uint8_t* bits = nullptr);
 
 // backward helpers -----------------------------------------------------
 // du = g*[out>0], g = G[b,n] (G != null) or dz[b]*wf[n]; NK=3 partials:

@@ -183,9 +183,26 @@ template <typename T> struct ColSumOp {
   }
 };
 
+// 1-bit image of "stored value > 0" for V = 8 bf16 columns c..c+7 of row r
+// (the keep mask the backward GEMM epilogues apply), one byte per thread
+template <typename T>
+__device__ __forceinline__ void store_pos_bits(uint8_t* bits, int64_t r, int ldb, int c,
+                                               const float (&y)[VE<T>]) {
+  if constexpr (sizeof(T) == 2) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const uint16_t h = __builtin_bit_cast(uint16_t, (bf16)y[v]);
+      b |= (uint32_t)((h & 0x7fffu) != 0 && !(h & 0x8000u)) << v;
+    }
+    bits[r * ldb + (c >> 3)] = (uint8_t)b;
+  }
+}
+
 template <typename T> struct BnReluDropOp {  // a = dropout(relu(t*sc+sh))
   const T* t; T* a; int ld; const float* sc; const float* sh;
   float inv_keep; uint32_t thresh; uint64_t seed; int layer; int drop;
+  uint8_t* bits;
   struct Cst { float sc[VE<T>], sh[VE<T>]; };
   struct Reg { float x[VE<T>]; };
   __device__ void prep(int c, Cst& q) const { ldc(sc + c, q.sc); ldc(sh + c, q.sh); }
@@ -195,11 +212,13 @@ template <typename T> struct BnReluDropOp {  // a = dropout(relu(t*sc+sh))
     for (int v = 0; v < VE<T>; ++v) q.x[v] = fmaxf(q.x[v] * k.sc[v] + k.sh[v], 0.f);
     if (drop) apply_dropout<VE<T>>(seed, layer, r, c, thresh, inv_keep, q.x);
     stv<T, true>(a + r * ld + c, q.x);
+    if (bits) store_pos_bits<T>(bits, r, ld >> 3, c, q.x);
   }
 };
 
 template <typename T> struct BnAddReluOp {   // out = relu(t*sc+sh + x)
   const T* t; const T* x; T* out; int ld; const float* sc; const float* sh;
+  uint8_t* bits;
   struct Cst { float sc[VE<T>], sh[VE<T>]; };
   struct Reg { float a[VE<T>], b[VE<T>]; };
   __device__ void prep(int c, Cst& q) const { ldc(sc + c, q.sc); ldc(sh + c, q.sh); }
@@ -211,6 +230,7 @@ template <typename T> struct BnAddReluOp {   // out = relu(t*sc+sh + x)
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) q.a[v] = fmaxf(q.a[v] * k.sc[v] + k.sh[v] + q.b[v], 0.f);
     stv<T, true>(out + r * ld + c, q.a);
+    if (bits) store_pos_bits<T>(bits, r, ld >> 3, c, q.a);
   }
 };
 
@@ -683,30 +703,32 @@ static uint32_t drop_thresh(float p) {   // 16-bit threshold (see dropout_bits)
 template <typename T>
 static dcnr_status bn_relu_drop_impl(const void* t, void* a, int64_t B, int N, int ld,
                                      const float* sc, const float* sh, float p, uint64_t seed,
-                                     int layer, hipStream_t s) {
+                                     int layer, hipStream_t s, uint8_t* bits) {
   BnReluDropOp<T> op{(const T*)t, (T*)a, ld, sc, sh, p > 0.f ? 1.f / (1.f - p) : 1.f,
-                     drop_thresh(p), seed, layer, p > 0.f};
+                     drop_thresh(p), seed, layer, p > 0.f, bits};
   return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
 }
 dcnr_status bn_relu_drop(int precision, const void* t, void* a, int64_t B, int N, int ld,
                          const float* scale, const float* shift, float p, uint64_t seed,
-                         int layer, hipStream_t s) {
+                         int layer, hipStream_t s, uint8_t* bits) {
   return precision == DCNR_PREC_BF16
-             ? bn_relu_drop_impl<bf16>(t, a, B, N, ld, scale, shift, p, seed, layer, s)
-             : bn_relu_drop_impl<float>(t, a, B, N, ld, scale, shift, p, seed, layer, s);
+             ? bn_relu_drop_impl<bf16>(t, a, B, N, ld, scale, shift, p, seed, layer, s, bits)
+             : bn_relu_drop_impl<float>(t, a, B, N, ld, scale, shift, p, seed, layer, s, nullptr);
 }
 
 template <typename T>
 static dcnr_status bn_add_relu_impl(const void* t, const void* x, void* out, int64_t B, int N,
-                                    int ld, const float* sc, const float* sh, hipStream_t s) {
-  BnAddReluOp<T> op{(const T*)t, (const T*)x, (T*)out, ld, sc, sh};
+                                    int ld, const float* sc, const float* sh, hipStream_t s,
+                                    uint8_t* bits) {
+  BnAddReluOp<T> op{(const T*)t, (const T*)x, (T*)out, ld, sc, sh, bits};
   return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
 }
 dcnr_status bn_add_relu2(int precision, const void* t, const void* x, void* out, int64_t B, int N,
-                         int ld, const float* scale, const float* shift, hipStream_t s) {
+                         int ld, const float* scale, const float* shift, hipStream_t s,
+                         uint8_t* bits) {
   return precision == DCNR_PREC_BF16
-             ? bn_add_relu_impl<bf16>(t, x, out, B, N, ld, scale, shift, s)
-             : bn_add_relu_impl<float>(t, x, out, B, N, ld, scale, shift, s);
+             ? bn_add_relu_impl<bf16>(t, x, out, B, N, ld, scale, shift, s, bits)
+             : bn_add_relu_impl<float>(t, x, out, B, N, ld, scale, shift, s, nullptr);
 }
 
 template <typename T>

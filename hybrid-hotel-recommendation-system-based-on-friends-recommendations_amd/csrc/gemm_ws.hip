@@ -108,7 +108,7 @@ __device__ __forceinline__ void issue_tile(u32x4 xr, int64_t ldx, int K, uint32_
   }
 }
 
-template <int KTP, int EPI>
+template <int KTP, int EPI, int HB = 0>
 __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   constexpr int WS_TM = ws_tm<EPI>();
   constexpr int NB = ws_nb<EPI>();
@@ -178,8 +178,10 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
       __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, (int)(a.M * a.ldc * es), 0x00020000);
   const __amdgpu_buffer_rsrc_t rr_ = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.R, (short)0, HAS_R ? (int)(a.M * a.ldr * 2) : 0, 0x00020000);
+  constexpr bool hbits = HAS_HT && HB;   // 1-bit keep mask (a.Hb) instead of bf16 H
   const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.H, (short)0, HAS_HT ? (int)(a.M * a.ldh * 2) : 0, 0x00020000);
+      hbits ? (void*)a.Hb : (void*)a.H, (short)0,
+      HAS_HT ? (int)(hbits ? a.M * a.ldhb * 4 : a.M * a.ldh * 2) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.T, (short)0, HAS_HT ? (int)(a.M * a.ldt * 2) : 0, 0x00020000);
 
@@ -206,13 +208,18 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     constexpr bool WS_OPS_EARLY = ws_ops_early<EPI>();
     constexpr int NSLOT = WS_OPS_EARLY ? WS_RB : 2;
     u32x4 rv[NSLOT], hv[NSLOT], tv[NSLOT];
+    uint32_t hw[NSLOT];   // the mask word of columns nw .. nw+31 (hbits)
     auto load_ops = [&](int rb, int slot) {
       const int64_t m = m0 + rb * 16 + l15;
       const bool ok = m < a.M && nst < a.N;
       if constexpr (HAS_R)
         rv[slot] = __builtin_amdgcn_raw_buffer_load_b128(rr_, ok ? (int)((m * a.ldr + nst) * 2) : OOR, 0, 0);
       if constexpr (HAS_HT) {
-        hv[slot] = __builtin_amdgcn_raw_buffer_load_b128(hr, ok ? (int)((m * a.ldh + nst) * 2) : OOR, 0, 0);
+        if constexpr (hbits)
+          hw[slot] = __builtin_amdgcn_raw_buffer_load_b32(
+              hr, (m < a.M && nw < a.N) ? (int)((m * a.ldhb + (nw >> 5)) * 4) : OOR, 0, 0);
+        else
+          hv[slot] = __builtin_amdgcn_raw_buffer_load_b128(hr, ok ? (int)((m * a.ldh + nst) * 2) : OOR, 0, 0);
         tv[slot] = __builtin_amdgcn_raw_buffer_load_b128(tr, ok ? (int)((m * a.ldt + nst) * 2) : OOR, 0, 0);
       }
     };
@@ -269,7 +276,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
       u32x4 of[2];
       if constexpr (HAS_R) to_acc_layout(rv[slot], rf);
       if constexpr (HAS_HT) {
-        to_acc_layout(hv[slot], hf);
+        if constexpr (!hbits) to_acc_layout(hv[slot], hf);
         to_acc_layout(tv[slot], tf);
       }
 #pragma unroll
@@ -300,10 +307,15 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
           // DROP_BN: keep where h != 0 (the saved dropout activation)
 #pragma unroll
           for (int d = 0; d < 2; ++d) {
-            const uint32_t hw = hf[cb][d];
-            uint32_t keep = ((hw & 0x7fff7fffu) + 0x7fff7fffu) & 0x80008000u;
-            if constexpr (EPI == NT_EPI_RESID_BN) keep &= ~hw;
-            o[cb][d] &= (keep >> 15) * 0xffffu;
+            if constexpr (hbits) {   // bits 16cb + 4q + 2d (+1) of the wave's 32 columns
+              const uint32_t kb = hw[slot] >> (16 * cb + 4 * q + 2 * d);
+              o[cb][d] &= ((kb & 1u) * 0xffffu) | (((kb >> 1) & 1u) * 0xffff0000u);
+            } else {
+              const uint32_t hb = hf[cb][d];
+              uint32_t keep = ((hb & 0x7fff7fffu) + 0x7fff7fffu) & 0x80008000u;
+              if constexpr (EPI == NT_EPI_RESID_BN) keep &= ~hb;
+              o[cb][d] &= (keep >> 15) * 0xffffu;
+            }
           }
         }
         if constexpr (STATS) {
@@ -414,13 +426,13 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   }
 }
 
-template <int KTP, int EPI>
+template <int KTP, int EPI, int HB = 0>
 dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   constexpr int WS_TM = ws_tm<EPI>();
   using C = WsCfg<KTP, WS_TM, ws_nb<EPI>()>;
   static bool attr_set = false;
   if (!attr_set) {
-    DCNR_HIP(hipFuncSetAttribute((const void*)gemm_ws_kernel<KTP, EPI>,
+    DCNR_HIP(hipFuncSetAttribute((const void*)gemm_ws_kernel<KTP, EPI, HB>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES));
     attr_set = true;
   }
@@ -442,10 +454,11 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
       b.C = (char*)a.C + m0 * a.ldc * (EPI == NT_EPI_F32 ? 4 : 2);
       if (a.R) b.R = (const char*)a.R + m0 * a.ldr * 2;
       if (a.H) b.H = a.H + m0 * a.ldh;
+      if (a.Hb) b.Hb = a.Hb + m0 * a.ldhb;
       if (a.T) b.T = a.T + m0 * a.ldt;
       if (a.part) b.part = a.part + (int64_t)total * 2 * a.N;
       int np = 0;
-      dcnr_status st = launch_ws<KTP, EPI>(b, s, &np);
+      dcnr_status st = launch_ws<KTP, EPI, HB>(b, s, &np);
       if (st != DCNR_OK) return st;
       total += np;
     }
@@ -459,16 +472,16 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   if (need < grid) grid = (int)(cdiv(need, unit) * unit);
   a.groups = grid / a.nslices;
   if (nparts) *nparts = a.groups;
-  hipLaunchKernelGGL((gemm_ws_kernel<KTP, EPI>), dim3(grid), dim3(WS_NT), C::LDS_BYTES, s, a);
+  hipLaunchKernelGGL((gemm_ws_kernel<KTP, EPI, HB>), dim3(grid), dim3(WS_NT), C::LDS_BYTES, s, a);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
 
-template <int EPI>
+template <int EPI, int HB = 0>
 dcnr_status dispatch_ws(const NtArgs& a, hipStream_t s, int* nparts) {
-  if (a.K <= 128) return launch_ws<4, EPI>(a, s, nparts);
-  if (a.K <= 256) return launch_ws<8, EPI>(a, s, nparts);
-  return launch_ws<16, EPI>(a, s, nparts);
+  if (a.K <= 128) return launch_ws<4, EPI, HB>(a, s, nparts);
+  if (a.K <= 256) return launch_ws<8, EPI, HB>(a, s, nparts);
+  return launch_ws<16, EPI, HB>(a, s, nparts);
 }
 
 }  // namespace
@@ -497,8 +510,12 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
     case NT_EPI_F32: return dispatch_ws<NT_EPI_F32>(a, s, nparts);
     case NT_EPI_RESID: return dispatch_ws<NT_EPI_RESID>(a, s, nparts);
     case NT_EPI_BIAS_STATS: return dispatch_ws<NT_EPI_BIAS_STATS>(a, s, nparts);
-    case NT_EPI_RESID_BN: return dispatch_ws<NT_EPI_RESID_BN>(a, s, nparts);
-    case NT_EPI_DROP_BN: return dispatch_ws<NT_EPI_DROP_BN>(a, s, nparts);
+    case NT_EPI_RESID_BN:
+      return a.Hb ? dispatch_ws<NT_EPI_RESID_BN, 1>(a, s, nparts)
+                  : dispatch_ws<NT_EPI_RESID_BN, 0>(a, s, nparts);
+    case NT_EPI_DROP_BN:
+      return a.Hb ? dispatch_ws<NT_EPI_DROP_BN, 1>(a, s, nparts)
+                  : dispatch_ws<NT_EPI_DROP_BN, 0>(a, s, nparts);
   }
   set_error("gemm_ws: bad epilogue");
   return DCNR_BAD_ARG;
