@@ -243,6 +243,10 @@ def main():
     ap.add_argument("--eval-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-serving", action="store_true", help="skip the configs[4] top-k leg")
+    ap.add_argument("--exchange", default="dense", choices=["dense", "sparse"],
+                    help="N>1 gradient exchange: dense = reduce-scatter/all-gather of the flat "
+                         "gradient (sharded AdamW); sparse = owner-bucketed user-table rows + "
+                         "all-reduce of the rest")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -260,7 +264,8 @@ def main():
     torch.manual_seed(42)
     model = dcnr.DCN_RecSys(CFG["n_users"], CFG["n_items"], CFG["cat_dims"], CFG["n_num"],
                             dict(CFG["params"]), precision=args.precision).to(dev)
-    trainer = dcnr.FusedTrainer(model, lr=1e-3, weight_decay=1e-4, optimizer_name="AdamW")
+    trainer = dcnr.FusedTrainer(model, lr=1e-3, weight_decay=1e-4, optimizer_name="AdamW",
+                                exchange=args.exchange)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 * rank)
     pool = [make_batch(gen, B, dev) for _ in range(max(1, args.pool))]
@@ -359,7 +364,10 @@ def main():
                                    "AdamW (+grad all-reduce), BASELINE configs[2]/[3]",
                        "batch_per_gpu": B, "global_batch": world * B,
                        "tables": "1M x 32 users, 100k x 32 hotels, 12 x 1000 x 32 cat, 8 dense",
-                       "deep": "3 cross + 4 x 512 residual", "parallelism": f"dp{world}"},
+                       "deep": "3 cross + 4 x 512 residual", "parallelism": f"dp{world}",
+                       "exchange": "none" if world == 1 else (
+                           "sparse user rows + all-reduce" if args.exchange == "sparse"
+                           else "reduce-scatter + sharded AdamW + all-gather")},
             "scored_pairs_per_sec": pairs_per_s,
             "final_loss": final_loss,
             "roofline": {"bound": "hbm",

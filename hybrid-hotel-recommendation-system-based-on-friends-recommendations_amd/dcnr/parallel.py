@@ -17,6 +17,10 @@ plain data-parallel split of each batch across ranks:
 
 Default (sync_bn=False) is local BN: every rank normalises with its own
 batch, like torch DDP without SyncBatchNorm.
+
+``sparse_rows_allreduce`` is the owner-bucketed sparse exchange of one
+embedding table's gradient (SURVEY.md 8e option B), used by
+``FusedTrainer(exchange="sparse")`` for the user table.
 """
 from __future__ import annotations
 
@@ -86,3 +90,61 @@ def install_sync_bn(model, group=None) -> SyncBNHook:
 def remove_sync_bn(model):
     model.bn_allreduce = None
     model._sync_bn_hook = None
+
+
+def sparse_rows_allreduce(grad: torch.Tensor, local_ids: torch.Tensor, group=None) -> dict:
+    """Sum a row-sparse embedding gradient over ranks, in place.
+
+    ``grad`` [n_rows, d] holds this rank's dense gradient, nonzero only in
+    rows listed in ``local_ids`` (the batch's ids for this table).  Rows are
+    owned in contiguous ranges of ceil(n_rows / world).  The exchange:
+      1. every rank sends its touched rows (distinct ids, ascending) to their
+         owners (all_to_all, sizes exchanged first);
+      2. each owner sums what it received in source-rank order (a fixed order:
+         every row is summed 0 + g_0 + g_1 + ..., as a single process would);
+      3. the owners' summed rows are all-gathered (padded to the largest
+         owner list) and written into ``grad``, which is zero elsewhere.
+    Every rank ends with the same ``grad``, bit for bit.  Returns the rows
+    sent / received counts for reporting."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    n, d = grad.shape
+    dev = grad.device
+    per = (n + world - 1) // world
+    uniq = torch.unique(local_ids.reshape(-1))
+    rows = grad.index_select(0, uniq)
+    send = torch.bincount(torch.div(uniq, per, rounding_mode='floor'), minlength=world)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send, group=group)
+    sc, rc = send.tolist(), recv.tolist()
+    rids = torch.empty(sum(rc), dtype=torch.int64, device=dev)
+    dist.all_to_all_single(rids, uniq, rc, sc, group=group)
+    rrows = torch.empty((sum(rc), d), dtype=grad.dtype, device=dev)
+    dist.all_to_all_single(rrows, rows, rc, sc, group=group)
+    lo = rank * per
+    span = max(0, min(per, n - lo))
+    acc = torch.zeros((span, d), dtype=grad.dtype, device=dev)
+    off = 0
+    for r in range(world):            # fixed source order; ids distinct per source
+        if rc[r]:
+            acc.index_add_(0, rids[off:off + rc[r]] - lo, rrows[off:off + rc[r]])
+        off += rc[r]
+    mine = torch.unique(rids)
+    vals = acc.index_select(0, mine - lo)
+    cnt = torch.tensor([mine.numel()], dtype=torch.int64, device=dev)
+    cnts = [torch.empty_like(cnt) for _ in range(world)]
+    dist.all_gather(cnts, cnt, group=group)
+    cnts = [int(c.item()) for c in cnts]
+    cap = max(max(cnts), 1)
+    pid = torch.full((cap,), -1, dtype=torch.int64, device=dev)
+    pval = torch.zeros((cap, d), dtype=grad.dtype, device=dev)
+    pid[:mine.numel()] = mine
+    pval[:mine.numel()] = vals
+    aid = torch.empty((world * cap,), dtype=torch.int64, device=dev)
+    aval = torch.empty((world * cap, d), dtype=grad.dtype, device=dev)
+    dist.all_gather_into_tensor(aid, pid, group=group)
+    dist.all_gather_into_tensor(aval, pval, group=group)
+    keep = aid >= 0
+    grad.zero_()
+    grad.index_copy_(0, aid[keep], aval[keep])
+    return {"rows_sent": int(uniq.numel()), "rows_owned": int(mine.numel()), "rows_total": sum(cnts)}

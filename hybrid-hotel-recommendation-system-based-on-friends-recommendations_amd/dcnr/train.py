@@ -12,6 +12,11 @@ optimizer.step) as native calls over flat parameter/gradient/moment buffers:
            optimizer's HBM traffic and moment memory (ZeRO-1 style)
          world > 1, shard_optimizer=False: all-reduce, then every rank
            updates everything
+         world > 1, exchange="sparse": the user table's gradient goes through
+           the owner-bucketed sparse exchange (dcnr.parallel.
+           sparse_rows_allreduce: only the rows the ranks' batches touched),
+           the rest of the flat gradient through one all-reduce, then every
+           rank updates everything
 
 Numerically the same update as ``torch.optim.AdamW``/``Adam`` on the
 reference's dense gradients (every embedding row's moments decay every step).
@@ -32,7 +37,7 @@ from .ops import bce_with_logits
 class FusedTrainer:
     def __init__(self, model: DCN_RecSys, lr=1e-3, weight_decay=1e-2, optimizer_name='AdamW',
                  betas=(0.9, 0.999), eps=1e-8, process_group=None, sync_bn=False,
-                 shard_optimizer=None):
+                 shard_optimizer=None, exchange="dense"):
         if optimizer_name not in ('AdamW', 'Adam'):
             raise ValueError("optimizer_name must be 'AdamW' or 'Adam' (train.py:201-204)")
         self.model = model
@@ -40,6 +45,11 @@ class FusedTrainer:
         dist_on = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(process_group) if dist_on else 1
         self.rank = dist.get_rank(process_group) if dist_on else 0
+        if exchange not in ("dense", "sparse"):
+            raise ValueError("exchange must be 'dense' or 'sparse'")
+        self.exchange = exchange
+        if exchange == "sparse":
+            shard_optimizer = False
         self.shard = (self.world > 1) if shard_optimizer is None else bool(shard_optimizer)
         self.flat, self.gflat = model.flatten_(pad_to=64 * self.world)
         n = self.flat.numel() // (self.world if self.shard else 1)
@@ -66,15 +76,25 @@ class FusedTrainer:
         loss, dz = bce_with_logits(logits, y, True, 1.0 / self.world)
         run_backward(model, user, item, cat, num, dz, self._ws, self._grads, seed,
                      accumulate=False)
-        self.exchange_and_update()
+        self.exchange_and_update(user_ids=user)
         return (loss, logits) if return_logits else loss
 
-    def exchange_and_update(self, adam=None):
+    def exchange_and_update(self, adam=None, user_ids=None):
         """The data-parallel gradient exchange and the optimizer step on the
         flat buffers.  ``adam(p, g, m, v, step)`` defaults to dcnr_adam_step
-        (the CPU tests pass a host restatement to check the exchange)."""
+        (the CPU tests pass a host restatement to check the exchange).
+        ``user_ids``: this rank's batch user ids (the sparse exchange)."""
         adam = adam or self._adam
         self.step_count += 1
+        if self.world > 1 and self.exchange == "sparse":
+            from .parallel import sparse_rows_allreduce
+            uw = self.model.user_embedding.weight
+            nu = ((uw.numel() + 63) // 64) * 64     # its padded segment at offset 0
+            assert uw.data_ptr() == self.flat.data_ptr()
+            self.last_exchange = sparse_rows_allreduce(uw.grad, user_ids, self.pg)
+            dist.all_reduce(self.gflat[nu:], op=dist.ReduceOp.SUM, group=self.pg)
+            adam(self.flat, self.gflat, self.m, self.v, self.step_count)
+            return
         if self.world > 1 and self.shard:
             n = self.m.numel()
             dist.reduce_scatter_tensor(self.gshard, self.gflat, op=dist.ReduceOp.SUM,

@@ -225,3 +225,63 @@ def test_sharded_optimizer_exchange_matches_allreduce_adam(world):
     rank's shard -> all-gather, and the all-reduce variant) gives every rank
     the single-process AdamW update of the summed gradient."""
     _run(_exchange_worker, world)
+
+
+def _sparse_worker(rank, world, port):
+    """Owner-bucketed sparse exchange of the user table (FusedTrainer
+    exchange="sparse"): each rank's user-table gradient is nonzero only on
+    its batch's ids (what dcnr_backward writes); after the exchange every rank
+    holds the dense SUM, bit for bit (summed in rank order), and the AdamW
+    step matches the single-process update."""
+    _init(rank, world, port)
+    try:
+        import dcnr
+        n_users, d = 257, 8
+        ids = [torch.randint(0, n_users, (40,), generator=torch.Generator().manual_seed(50 + r))
+               for r in range(world)]
+        ids[world - 1][:5] = n_users - 1          # the last owner's tail row
+        grads = []
+        for r in range(world):
+            gr = torch.zeros(n_users, d)
+            u = torch.unique(ids[r])
+            gr[u] = torch.randn(u.numel(), d, generator=torch.Generator().manual_seed(7 + r))
+            grads.append(gr)
+        mine = grads[rank].clone()
+        info = parallel.sparse_rows_allreduce(mine, ids[rank])
+        want = sum(grads)
+        assert torch.equal(mine, want)
+        assert info["rows_sent"] == torch.unique(ids[rank]).numel()
+        assert info["rows_total"] == torch.unique(torch.cat(ids)).numel()
+        # through FusedTrainer
+        torch.manual_seed(0)
+        m = dcnr.DCN_RecSys(n_users, 40, {"a": 10, "b": 3}, 3,
+                            dict(emb_dim=d, hidden_dim=16, n_cross_layers=1, n_res_blocks=1,
+                                 dropout=0.0))
+        tr = dcnr.FusedTrainer(m, lr=1e-2, weight_decay=1e-2, exchange="sparse")
+        assert not tr.shard and tr.m.numel() == tr.flat.numel()
+        ref_p, ref_m, ref_v = tr.flat.clone(), torch.zeros_like(tr.flat), torch.zeros_like(tr.flat)
+        nu = ((n_users * d + 63) // 64) * 64
+        for step in range(1, 3):
+            full = []
+            for r in range(world):
+                gg = torch.randn(tr.flat.numel(), generator=torch.Generator().manual_seed(9 * step + r))
+                gu = torch.zeros(n_users, d)
+                u = torch.unique(ids[r])
+                gu[u] = gg[:n_users * d].view(n_users, d)[u]
+                gg[:nu] = 0
+                gg[:n_users * d] = gu.reshape(-1)
+                full.append(gg)
+            tr.gflat.copy_(full[rank])
+            tr.exchange_and_update(adam=_host_adam, user_ids=ids[rank])
+            _host_adam(ref_p, sum(full), ref_m, ref_v, step)
+            np.testing.assert_allclose(tr.flat.numpy(), ref_p.numpy(), rtol=2e-6, atol=1e-7)
+            allp = [torch.empty_like(tr.flat) for _ in range(world)]
+            dist.all_gather(allp, tr.flat)
+            assert all(torch.equal(allp[0], a) for a in allp[1:])
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sparse_user_table_exchange(world):
+    _run(_sparse_worker, world)
