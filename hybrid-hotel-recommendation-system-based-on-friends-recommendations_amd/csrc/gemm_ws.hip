@@ -36,6 +36,9 @@ namespace {
 // allow; RESID_BN (three operands) needs 32-row tiles to have its operands in
 // flight during the MFMAs ("early"); RESID and DROP_BN load theirs one row
 // block ahead of use ("late").
+#ifndef WS_PREFETCH_PIN
+#define WS_PREFETCH_PIN 1
+#endif
 #ifndef WS_TM_PLAIN
 #define WS_TM_PLAIN 64
 #endif
@@ -196,6 +199,9 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
 
   // fragment read offsets: row rb*16 + l15, chunk (4kt + q) ^ l15
   const uint32_t rowoff = (uint32_t)l15 * C::P;
+  int coff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) coff[j] = ((4 * j + q) ^ l15) * 16;
   int buf = 0;
   for (int64_t mt = group; mt < a.mtiles; mt += groups, buf = buf + 1 == NB ? 0 : buf + 1) {
     const int64_t mn = mt + (int64_t)(NB - 1) * groups;
@@ -236,18 +242,20 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     for (int rb = 0; rb < WS_RB; ++rb)
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // fragment (kt, rb): row rb*16 + l15, physical chunk (4kt + q) ^ l15 =
+    // 16 (kt >> 2) + coff[kt & 3]: 4 offset registers, the rest immediates
+    auto xrd = [&](int kt, int rb) {
+      return *reinterpret_cast<const bf16x8*>(xb + rb * 16 * C::P + (kt >> 2) * 256 + coff[kt & 3]);
+    };
     bf16x8 xf[2][WS_RB];
 #pragma unroll
-    for (int rb = 0; rb < WS_RB; ++rb)
-      xf[0][rb] = *reinterpret_cast<const bf16x8*>(xb + rb * 16 * C::P + ((q ^ l15) & 15) * 16);
+    for (int rb = 0; rb < WS_RB; ++rb) xf[0][rb] = xrd(0, rb);
 #pragma unroll
     for (int kt = 0; kt < KTP; ++kt) {
       const int cur = kt & 1;
       if (kt + 1 < KTP) {
-        const int ch = ((4 * (kt + 1) + q) ^ l15);
 #pragma unroll
-        for (int rb = 0; rb < WS_RB; ++rb)
-          xf[cur ^ 1][rb] = *reinterpret_cast<const bf16x8*>(xb + rb * 16 * C::P + ch * 16);
+        for (int rb = 0; rb < WS_RB; ++rb) xf[cur ^ 1][rb] = xrd(kt + 1, rb);
       }
 #pragma unroll
       for (int rb = 0; rb < WS_RB; ++rb)
@@ -257,6 +265,18 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
             acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][kt], xf[cur][rb], acc[rb][cb], 0, 0, 0);
           else
             acc[rb][cb][0] += (float)xf[cur][rb][cb] + (float)wf[cb][kt][0];
+#if WS_PREFETCH_PIN
+      // keep step kt+1's fragment reads in step kt (a full step of MFMAs
+      // between a read and its use), spread between the MFMAs
+      if (kt + 1 < KTP) {
+#pragma unroll
+        for (int rb = 0; rb < WS_RB; ++rb) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#endif
     }
 
     // ---- epilogue: lane holds C[m][nw + 16cb + 4q .. +3], m = m0 + 16rb + l15
