@@ -433,6 +433,29 @@ bool gemm_final_ok(const dcnr_model_desc* desc, const NtArgs& a, int epi) {
   return !off && !desc->bn_allreduce && gemm_ws_single_launch(a, epi);
 }
 
+// Eval forward with BatchNorm (running statistics) + ReLU (+ residual) in the
+// streaming GEMM's epilogue: no t1/t2 round trip through HBM and no rowwise
+// passes (bf16, gemm_ws shapes).
+bool eval_fuse_ok(const Dims& d) {
+  static const bool off = getenv("DCNR_DISABLE_EVAL_FUSE") != nullptr ||
+                          getenv("DCNR_GEMM_NT") != nullptr ||
+                          getenv("DCNR_DISABLE_GEMM_NT") != nullptr;
+  return d.prec == DCNR_PREC_BF16 && !off && gemm_nt_supported(d.Hp, d.Hp);
+}
+
+// out = relu((A W^T + b) * bn.scale + bn.shift [+ R])
+dcnr_status linear_bn_relu(const Dims& d, const void* A, const void* W, const float* bias,
+                           const BnBufs& bn, const void* R, void* out, int64_t B, hipStream_t s) {
+  NtArgs a;
+  memset(&a, 0, sizeof(a));
+  a.X = (const bf16*)A; a.ldx = d.Hp; a.M = B; a.K = d.Hp;
+  a.W = (const bf16*)W; a.ldw = d.Hp; a.N = d.Hp;
+  a.C = out; a.ldc = d.Hp; a.bias = bias;
+  a.R = R; a.ldr = d.Hp;
+  a.bn_scale = bn.scale; a.bn_shift = bn.shift;
+  return gemm_ws(R ? NT_EPI_BN_RESID_RELU : NT_EPI_BN_RELU, a, s);
+}
+
 // *fin_done = 1 when rf was applied inside the GEMM (else the caller reduces
 // the nc partial rows in L.part)
 dcnr_status linear_fwd_stats(const dcnr_model_desc* desc, const Dims& d, const Layout& L,
@@ -708,6 +731,21 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
                                                B, o, d.prec == DCNR_PREC_BF16, L.err, check, s));
   }
   TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.x0, d.Dp, L.W0p, d.Dp, L.b0p, L.h[0], B, s));
+  if (!train && eval_fuse_ok(d)) {
+    for (int j = 0; j < d.R; ++j) {
+      const auto& Bk = P.blk[j];
+      TRY(bn_layer_fwd(desc, d, L, nullptr, B, false, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
+                       L.bn[2 * j], s));
+      TRYP(DCNR_K_GEMM_FWD, linear_bn_relu(d, L.h[j], L.W1p[j], L.b1p[j], L.bn[2 * j], nullptr, L.a1, B, s));
+      TRY(bn_layer_fwd(desc, d, L, nullptr, B, false, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
+                       L.bn[2 * j + 1], s));
+      TRYP(DCNR_K_GEMM_FWD, linear_bn_relu(d, L.a1, L.W2p[j], L.b2p[j], L.bn[2 * j + 1], L.h[j], L.h[j + 1],
+                                           B, s));
+    }
+    TRYP(DCNR_K_HEAD, row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
+    TRYP(DCNR_K_HEAD, head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
+    return DCNR_OK;
+  }
   const float p = train ? d.dropout : 0.f;
   for (int j = 0; j < d.R; ++j) {
     const auto& Bk = P.blk[j];

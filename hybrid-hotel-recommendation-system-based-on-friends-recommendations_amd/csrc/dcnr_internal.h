@@ -310,6 +310,10 @@ enum NtEpi : int {
   NT_EPI_BIAS_STATS = 3,   // C = acc + bias; part = [sum(c - bias), sum((c - bias)^2)]
   NT_EPI_RESID_BN = 4,     // C = (acc + R) * [H > 0]; part = [sum c, sum c*xhat(T)]
   NT_EPI_DROP_BN = 5,      // C = acc * [H != 0] * hscale; part = [sum c, sum c*xhat(T)]
+  // eval-mode BatchNorm folded into the epilogue (gemm_ws only; bn_scale /
+  // bn_shift = the running-stat affine of bn_finalize2):
+  NT_EPI_BN_RELU = 6,        // C = relu((acc + bias) * sc + sh)
+  NT_EPI_BN_RESID_RELU = 7,  // C = relu((acc + bias) * sc + sh + R)
 };
 // (c is the stored bf16 value; xhat(T) = (T[m][n] - mean[n]) * invstd[n])
 struct NtArgs {
@@ -323,6 +327,7 @@ struct NtArgs {
                                                     // of word [m][c/32] = keep column c
   const bf16* T; int64_t ldt;                       // BN input for xhat
   const float* mean; const float* invstd;
+  const float* bn_scale; const float* bn_shift;     // BN_RELU, BN_RESID_RELU
   float* part;                                      // column partials (stats epilogues)
   // gemm_ws only: fin != 0 -> the last workgroup of each column slice reduces
   // the partials (fp64, fixed order) and runs red_finalize itself (fin_shift:
@@ -337,7 +342,7 @@ dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullp
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
 // whether gemm_ws runs as one launch (a requirement for fin)
 bool gemm_ws_single_launch(const NtArgs& a, int epi);
-inline bool nt_epi_stats(int epi) { return epi >= NT_EPI_BIAS_STATS; }
+inline bool nt_epi_stats(int epi) { return epi >= NT_EPI_BIAS_STATS && epi <= NT_EPI_DROP_BN; }
 
 // bf16 weight-gradient GEMM (gemm_dw.hip): slab[split][n][k] = sum over the
 // split's batch rows of A[b][n] * B[b][k]; A = dY [Btot][lda], B = X [Btot][ldb]

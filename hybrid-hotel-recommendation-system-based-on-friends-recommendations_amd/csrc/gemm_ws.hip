@@ -45,7 +45,8 @@ namespace {
 constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
 
 template <int EPI> constexpr int ws_tm() {
-  return EPI == NT_EPI_RESID ? 32 : EPI == NT_EPI_RESID_BN ? 32 : EPI == NT_EPI_DROP_BN ? 64 : WS_TM_PLAIN;
+  return (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU) ? 32 : EPI == NT_EPI_RESID_BN ? 32
+         : EPI == NT_EPI_DROP_BN ? 64 : WS_TM_PLAIN;
 }
 template <int EPI> constexpr bool ws_ops_early() { return EPI == NT_EPI_RESID_BN; }
 // X-tile buffers in the LDS ring: the next NB-1 tiles are in flight while one
@@ -55,7 +56,8 @@ template <int EPI> constexpr bool ws_ops_early() { return EPI == NT_EPI_RESID_BN
 #define WS_NB_PLAIN 2
 #endif
 template <int EPI> constexpr int ws_nb() {
-  return (EPI == NT_EPI_BIAS || EPI == NT_EPI_BIAS_STATS || EPI == NT_EPI_F32) ? WS_NB_PLAIN : 2;
+  return (EPI == NT_EPI_BIAS || EPI == NT_EPI_BIAS_STATS || EPI == NT_EPI_F32 || EPI == NT_EPI_BN_RELU)
+             ? WS_NB_PLAIN : 2;
 }
 
 template <int KTP, int TM, int NB = 2> struct WsCfg {
@@ -117,10 +119,11 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   constexpr int NB = ws_nb<EPI>();
   using C = WsCfg<KTP, WS_TM, NB>;
   constexpr int WS_RB = C::RB;
-  constexpr bool STATS = EPI >= NT_EPI_BIAS_STATS;
-  constexpr bool HAS_R = EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN;
+  constexpr bool STATS = EPI >= NT_EPI_BIAS_STATS && EPI <= NT_EPI_DROP_BN;
+  constexpr bool HAS_R = EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_BN_RESID_RELU;
   constexpr bool HAS_HT = EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN;
-  constexpr bool HAS_BIAS = EPI <= NT_EPI_BIAS_STATS;
+  constexpr bool HAS_BIAS = EPI <= NT_EPI_BIAS_STATS || EPI >= NT_EPI_BN_RELU;
+  constexpr bool HAS_SS = EPI >= NT_EPI_BN_RELU;   // eval BN affine + ReLU
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, l15 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -161,7 +164,8 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
       }
     }
   }
-  // per-column constants of the slice: bias, -mean*invstd, invstd
+  // per-column constants of the slice: bias, -mean*invstd, invstd (eval BN:
+  // scale, shift)
   float* bias_s = reinterpret_cast<float*>(lds + NB * C::TILE);
   float* nmi_s = bias_s + WS_TN;
   float* istd_s = bias_s + 2 * WS_TN;
@@ -171,6 +175,10 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     if constexpr (HAS_HT) {
       nmi_s[c] = n < a.N ? -a.mean[n] * a.invstd[n] : 0.f;
       istd_s[c] = n < a.N ? a.invstd[n] : 0.f;
+    }
+    if constexpr (HAS_SS) {
+      nmi_s[c] = n < a.N ? a.bn_scale[n] : 0.f;
+      istd_s[c] = n < a.N ? a.bn_shift[n] : 0.f;
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -311,9 +319,19 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
           v[0] += bb[0];
           v[1] += bb[1];
         }
+        if constexpr (HAS_SS) {
+          const float4 sc = *reinterpret_cast<const float4*>(nmi_s + cl);
+          const float4 sh = *reinterpret_cast<const float4*>(istd_s + cl);
+          v[0] = v[0] * f2v{sc.x, sc.y} + f2v{sh.x, sh.y};
+          v[1] = v[1] * f2v{sc.z, sc.w} + f2v{sh.z, sh.w};
+        }
         if constexpr (HAS_R) {
 #pragma unroll
           for (int d = 0; d < 2; ++d) v[d] += unpack2(rf[cb][d]);
+        }
+        if constexpr (HAS_SS) {
+#pragma unroll
+          for (int d = 0; d < 2; ++d) v[d] = f2v{fmaxf(v[d][0], 0.f), fmaxf(v[d][1], 0.f)};
         }
         if constexpr (EPI == NT_EPI_DROP_BN) {
           v[0] *= a.hscale;
@@ -519,7 +537,8 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
   if (a.M <= 0 || a.N <= 0) return DCNR_OK;
   const bool ht = epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN;
   if (!gemm_nt_supported(a.K, a.N) || a.ldx % 8 || a.ldw % 8 || a.ldc % 8 ||
-      ((epi == NT_EPI_RESID || epi == NT_EPI_RESID_BN) && (a.ldr % 8 || !a.R)) ||
+      ((epi == NT_EPI_RESID || epi == NT_EPI_RESID_BN || epi == NT_EPI_BN_RESID_RELU) && (a.ldr % 8 || !a.R)) ||
+      (epi >= NT_EPI_BN_RELU && (!a.bn_scale || !a.bn_shift)) ||
       (ht && (!a.H || !a.T || !a.mean || !a.invstd || a.ldh % 8 || a.ldt % 8)) ||
       (nt_epi_stats(epi) && !a.part)) {
     set_error("gemm_ws: unsupported K=%d N=%d / missing epilogue operand", a.K, a.N);
@@ -533,6 +552,8 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
     case NT_EPI_RESID_BN:
       return a.Hb ? dispatch_ws<NT_EPI_RESID_BN, 1>(a, s, nparts)
                   : dispatch_ws<NT_EPI_RESID_BN, 0>(a, s, nparts);
+    case NT_EPI_BN_RELU: return dispatch_ws<NT_EPI_BN_RELU>(a, s, nparts);
+    case NT_EPI_BN_RESID_RELU: return dispatch_ws<NT_EPI_BN_RESID_RELU>(a, s, nparts);
     case NT_EPI_DROP_BN:
       return a.Hb ? dispatch_ws<NT_EPI_DROP_BN, 1>(a, s, nparts)
                   : dispatch_ws<NT_EPI_DROP_BN, 0>(a, s, nparts);

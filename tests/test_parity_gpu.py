@@ -201,6 +201,22 @@ def test_bf16_mode_close(dev):
     np.testing.assert_allclose(gn[big], fx["gnorm64"][big], rtol=5e-2)
 
 
+def test_bf16_eval_fused_close(dev):
+    """bf16 eval forward: BatchNorm (running stats) + ReLU (+ residual) run in
+    the streaming GEMM epilogue (NT_EPI_BN_RELU / NT_EPI_BN_RESID_RELU);
+    checked against the fp64 oracle after a train step moved the running
+    stats off their init values."""
+    fx = golden("f3_cfg3r_train.npz")
+    m = our_model(gc.CFG3R, precision="bf16").to(dev)
+    run_train(m, dev, fx["user"], fx["item"], fx["cat"], fx["num"], fx["y"])
+    m.eval()
+    with torch.no_grad():
+        ze = m(*to_dev(dev, fx["user"], fx["item"], fx["cat"], fx["num"])).reshape(-1).cpu().numpy()
+    zr, _ = orc.forward(np_state(m), spec_of(gc.CFG3R), fx["user"], fx["item"], fx["cat"], fx["num"],
+                        train=False)
+    assert np.linalg.norm(ze - zr) / np.linalg.norm(zr) <= 1e-2
+
+
 def test_batch_one_semantics(dev):
     cfg = gc.CFG_ODD
     m = our_model(cfg).to(dev)
