@@ -732,13 +732,20 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   }
   TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.x0, d.Dp, L.W0p, d.Dp, L.b0p, L.h[0], B, s));
   if (!train && eval_fuse_ok(d)) {
+    // every layer's running-stat affine in one launch
+    BnEvalBatch eb;
+    memset(&eb, 0, sizeof(eb));
+    eb.n = 2 * d.R; eb.N = d.Hp; eb.Nr = d.H;
     for (int j = 0; j < d.R; ++j) {
       const auto& Bk = P.blk[j];
-      TRY(bn_layer_fwd(desc, d, L, nullptr, B, false, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
-                       L.bn[2 * j], s));
+      const BnBufs& b1 = L.bn[2 * j];
+      const BnBufs& b2 = L.bn[2 * j + 1];
+      eb.f[2 * j] = BnFinal{Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1, b1.scale, b1.shift, b1.mean, b1.invstd};
+      eb.f[2 * j + 1] = BnFinal{Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2, b2.scale, b2.shift, b2.mean, b2.invstd};
+    }
+    TRYP(DCNR_K_REDUCE, bn_eval_finalize(eb, s));
+    for (int j = 0; j < d.R; ++j) {
       TRYP(DCNR_K_GEMM_FWD, linear_bn_relu(d, L.h[j], L.W1p[j], L.b1p[j], L.bn[2 * j], nullptr, L.a1, B, s));
-      TRY(bn_layer_fwd(desc, d, L, nullptr, B, false, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
-                       L.bn[2 * j + 1], s));
       TRYP(DCNR_K_GEMM_FWD, linear_bn_relu(d, L.a1, L.W2p[j], L.b2p[j], L.bn[2 * j + 1], L.h[j], L.h[j + 1],
                                            B, s));
     }

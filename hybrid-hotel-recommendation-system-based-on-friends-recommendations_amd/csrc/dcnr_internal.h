@@ -223,6 +223,9 @@ struct BnFinal {   // per BN layer
 // N = padded width, Nr = real width (parameters have Nr entries; pads -> 0)
 dcnr_status bn_finalize2(const double* sums, int N, int Nr, int train, const BnFinal& f,
                          hipStream_t s);
+// eval (running-stat) finalize of up to 16 BN layers in one launch
+struct BnEvalBatch { BnFinal f[16]; int n, N, Nr; };
+dcnr_status bn_eval_finalize(const BnEvalBatch& b, hipStream_t s);
 // Fused reduce + consumer (used when no SyncBN hook must see the sums)
 enum RedMode : int { RED_BN_FWD = 0, RED_BN_BWD = 1, RED_BIAS = 2, RED_SUMS = 3 };
 constexpr int RED_G = 32;          // chunk groups per column group

@@ -680,6 +680,32 @@ dcnr_status col_sum(int precision, const void* x, int64_t B, int N, int ld, floa
                                      : col_sum_impl<float>(x, B, N, ld, part, nchunks, s);
 }
 
+// eval-mode finalize of several BN layers in one launch (blockIdx.y = layer):
+// the same per-column arithmetic as bn_finalize_kernel's running-stat branch
+__global__ void bn_eval_multi_kernel(BnEvalBatch b) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const BnFinal& f = b.f[blockIdx.y];
+  if (n >= b.N) return;
+  if (n >= b.Nr) {
+    f.scale[n] = 0.f; f.shift[n] = 0.f; f.mean[n] = 0.f; f.invstd[n] = 0.f;
+    return;
+  }
+  const double mean = f.rmean[n], var = f.rvar[n];
+  float inv = (float)(1.0 / sqrt(var + (double)BN_EPS));
+  float sc = f.gamma[n] * inv;
+  f.scale[n] = sc;
+  f.shift[n] = f.beta[n] - (float)mean * sc;
+  f.mean[n] = (float)mean;
+  f.invstd[n] = inv;
+}
+
+dcnr_status bn_eval_finalize(const BnEvalBatch& b, hipStream_t s) {
+  if (b.n <= 0) return DCNR_OK;
+  hipLaunchKernelGGL(bn_eval_multi_kernel, dim3((unsigned)cdiv(b.N, NT), (unsigned)b.n), dim3(NT), 0, s, b);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
 dcnr_status bn_finalize2(const double* sums, int N, int Nr, int train, const BnFinal& f,
                          hipStream_t s) {
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((unsigned)cdiv(N, NT)), dim3(NT), 0, s, sums, N, Nr,

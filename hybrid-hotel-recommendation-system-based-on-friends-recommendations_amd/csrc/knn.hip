@@ -517,6 +517,102 @@ __global__ __launch_bounds__(NT) void merge_kernel(const Cand* in, int nslices, 
   const int l0 = grp * lpg, nl = max(0, min(lpg, nslices - l0));
   const Cand* c = in + (qq * (int64_t)nslices + l0) * k;
   const int total = nl * k;
+  // fast path 0 (final stage, one load round, up to 4 lists per thread): the
+  // k-th smallest of the lists' minima bounds the k-th best overall (k lists
+  // each hold a candidate at or under it), so only the candidates at or under
+  // that bound -- found by a 2-pass radix select over the minima -- are sorted.
+  // Same result as sorting them all: every candidate of the k best passes.
+  if (groups == 1 && total <= NT * FT && nl <= 4 * NT) {
+    __shared__ unsigned hist[256];
+    __shared__ unsigned sel_prefix, sel_need;
+    __shared__ int sel_fail;
+    Cand e[FT];
+#pragma unroll
+    for (int j = 0; j < FT; ++j) {
+      const int t = j * NT + threadIdx.x;
+      e[j] = t < total ? c[t] : Cand{FLT_MAX, INT_MAX};
+    }
+    // distances are >= 0: their bits order like the values
+    auto key = [](float x) { return __float_as_uint(fmaxf(x, 0.f)); };
+    unsigned mk[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int l = threadIdx.x + r * NT;
+      float m = FLT_MAX;
+      if (l < nl)
+        for (int j = 0; j < k; ++j) m = fminf(m, c[(int64_t)l * k + j].d);
+      mk[r] = l < nl ? key(m) : 0xffffffffu;
+    }
+    if (threadIdx.x == 0) { sel_prefix = 0; sel_need = (unsigned)k; sel_fail = 0; }
+    unsigned mask = 0;
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int sh = 24 - 8 * pass;
+      for (int b = threadIdx.x; b < 256; b += NT) hist[b] = 0;
+      __syncthreads();
+      const unsigned prefix = sel_prefix;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (mk[r] != 0xffffffffu && (mk[r] & mask) == prefix) atomicAdd(&hist[(mk[r] >> sh) & 255u], 1u);
+      __syncthreads();
+      if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        const unsigned need = sel_need;
+        unsigned h[4], sum = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) { h[b] = hist[4 * lane + b]; sum += h[b]; }
+        unsigned incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+          const unsigned v = __shfl_up(incl, off, 64);
+          if (lane >= off) incl += v;
+        }
+        unsigned cum = incl - sum;
+        if (cum < need && need <= incl) {
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            if (cum + h[b] >= need) {
+              sel_prefix = prefix | ((unsigned)(4 * lane + b) << sh);
+              sel_need = need - cum;
+              break;
+            }
+            cum += h[b];
+          }
+        }
+        if (lane == 63 && incl < need) sel_fail = 1;   // fewer than k lists hold candidates
+      }
+      mask |= 255u << sh;
+      __syncthreads();
+    }
+    if (!sel_fail) {
+      const unsigned tk = sel_prefix | 0xffffu;
+      if (threadIdx.x == 0) cnt = 0;
+      __syncthreads();
+      constexpr int SCAP = 128;
+#pragma unroll
+      for (int j = 0; j < FT; ++j)
+        if (e[j].i != INT_MAX && key(e[j].d) <= tk) {
+          const int pos = atomicAdd(&cnt, 1);
+          if (pos < SCAP) { cd[pos] = e[j].d; ci[pos] = e[j].i; }
+        }
+      __syncthreads();
+      const int nv = cnt;
+      if (nv <= SCAP) {
+        int n2 = 2;
+        while (n2 < nv) n2 <<= 1;
+        for (int t = nv + threadIdx.x; t < n2; t += NT) { cd[t] = FLT_MAX; ci[t] = INT_MAX; }
+        __syncthreads();
+        bitonic(cd, ci, n2);
+        for (int t = threadIdx.x; t < k; t += NT) {
+          const bool ok = t < nv;
+          idx[qq * k + t] = ok ? (int64_t)ci[t] : -1;
+          dist[qq * k + t] = ok ? cd[t] : FLT_MAX;
+        }
+        return;
+      }
+    }
+    __syncthreads();
+  }
   // fast path: the valid candidates (with admission bounds, a few per query)
   // fit the buffer -> one gather and one sort
   if (threadIdx.x == 0) cnt = 0;
