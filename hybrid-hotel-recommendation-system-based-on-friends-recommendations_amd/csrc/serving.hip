@@ -26,6 +26,7 @@ namespace {
 
 constexpr int SV_NT = 1024;
 constexpr int SV_MAX = 4096;   // max candidates per call (LDS sort capacity)
+constexpr size_t MMR_LDS_MAX = 128 * 1024;   // dynamic LDS of mmr_lds_kernel
 
 // ascending bitonic sort of n2 (power of two) (key, val) pairs in LDS;
 // less(a, b) on (key, val)
@@ -205,6 +206,72 @@ __global__ __launch_bounds__(SV_NT) void mmr_kernel(const float* table, const fl
   if (threadIdx.x == 0) *out_count = cnt;
 }
 
+__global__ __launch_bounds__(SV_NT) void mmr_lds_kernel(const float* table, const float* inv, int d,
+                                                    const int64_t* rows, const float* scores,
+                                                    int n, float lambda, int top_k,
+                                                    int64_t* out_pos, int32_t* out_count) {
+  __shared__ float maxsim[SV_MAX];
+  __shared__ unsigned char taken[SV_MAX];
+  __shared__ float sv[SV_NT / 64];
+  __shared__ int sp[SV_NT / 64];
+  __shared__ float selv[256];
+  __shared__ int any_sel;
+  // the candidates' raw rows (stride d+1: one row per thread, conflict-free)
+  // and inverse norms, loaded once instead of re-read every selection round
+  extern __shared__ float lds_rows[];
+  float* invs = lds_rows + (size_t)n * (d + 1);
+  for (int e = threadIdx.x; e < n * d; e += SV_NT) {
+    const int t = e / d, c = e - t * d;
+    const int64_t r = rows[t];
+    lds_rows[t * (d + 1) + c] = r >= 0 ? table[r * d + c] : 0.f;
+  }
+  for (int t = threadIdx.x; t < n; t += SV_NT) invs[t] = rows[t] >= 0 ? inv[rows[t]] : 0.f;
+  for (int t = threadIdx.x; t < n; t += SV_NT) { maxsim[t] = -FLT_MAX; taken[t] = 0; }
+  if (threadIdx.x == 0) { any_sel = 0; taken[0] = 1; out_pos[0] = 0; }
+  __syncthreads();
+  const int want = min(top_k, n);
+  int cnt = 1, last = 0;
+  for (;;) {
+    // fold the last selected item into every candidate's max similarity
+    const int64_t sr = rows[last];
+    if (sr >= 0) {
+      const float is = invs[last];
+      for (int t = threadIdx.x; t < d; t += SV_NT) selv[t] = lds_rows[last * (d + 1) + t] * is;
+      __syncthreads();
+      for (int t = threadIdx.x; t < n; t += SV_NT) {
+        const int64_t r = rows[t];
+        if (r < 0 || taken[t]) continue;
+        const float* rw = lds_rows + t * (d + 1);
+        float s = 0.f;
+        for (int c = 0; c < d; ++c) s += rw[c] * selv[c];
+        s *= invs[t];
+        maxsim[t] = fmaxf(maxsim[t], s);
+      }
+      if (threadIdx.x == 0) any_sel = 1;
+      __syncthreads();
+    }
+    if (cnt >= want) break;
+    float v = -FLT_MAX;
+    int p = INT_MAX;
+    const bool sel = any_sel != 0;
+    for (int t = threadIdx.x; t < n; t += SV_NT) {
+      if (taken[t] || rows[t] < 0) continue;
+      const float m = lambda * scores[t] - (1.f - lambda) * (sel ? maxsim[t] : 0.f);
+      if (p == INT_MAX || m > v || (m == v && t < p)) { v = m; p = t; }
+    }
+    float bv;
+    int bp;
+    block_argmax(v, p, sv, sp, bv, bp);
+    if (bp == INT_MAX) break;
+    if (threadIdx.x == 0) { taken[bp] = 1; out_pos[cnt] = bp; }
+    __syncthreads();
+    ++cnt;
+    last = bp;
+  }
+  for (int t = threadIdx.x + cnt; t < top_k; t += SV_NT) out_pos[t] = -1;
+  if (threadIdx.x == 0) *out_count = cnt;
+}
+
 // Batch assembly of a device-resident dataset (the DataLoader of
 // train.py:195-196): dst_a[i] = src_a[idx[i]] for each array a, whole rows of
 // row_bytes (a multiple of 4) copied as dwords, one wave per (row, array).
@@ -300,8 +367,22 @@ dcnr_status mmr_rerank(const float* table, const float* inv, int d, const int64_
     return DCNR_UNSUPPORTED_SHAPE;
   }
   if (n <= 0) return DCNR_OK;
-  hipLaunchKernelGGL(mmr_kernel, dim3(1), dim3(SV_NT), 0, s, table, inv, d, rows, scores, (int)n,
-                     lambda, top_k, out_pos, out_count);
+  // candidate rows staged in LDS when they fit (the same arithmetic, in the
+  // same order, as the kernel that re-reads them from the table)
+  const size_t lds = ((size_t)n * (d + 1) + (size_t)n) * sizeof(float);
+  if (lds <= MMR_LDS_MAX) {
+    static bool attr = false;
+    if (!attr) {
+      DCNR_HIP(hipFuncSetAttribute((const void*)mmr_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (int)MMR_LDS_MAX));
+      attr = true;
+    }
+    hipLaunchKernelGGL(mmr_lds_kernel, dim3(1), dim3(SV_NT), lds, s, table, inv, d, rows, scores, (int)n,
+                       lambda, top_k, out_pos, out_count);
+  } else {
+    hipLaunchKernelGGL(mmr_kernel, dim3(1), dim3(SV_NT), 0, s, table, inv, d, rows, scores, (int)n,
+                       lambda, top_k, out_pos, out_count);
+  }
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }

@@ -427,6 +427,32 @@ def test_cosine_knn_vs_sklearn_golden(dev):
             np.testing.assert_array_equal(i[r][isolated], ref_i[isolated])
 
 
+@pytest.mark.parametrize("Q", [1, 3, 8])
+def test_cosine_knn_full_size(dev, Q):
+    """configs[4] size: cosine top-11 over 1M x 64 (VALU scan for Q < 4, MFMA
+    scan for Q >= 4; final merge through the list-minima bound) against a
+    brute-force torch fp32 reference on the device (random table: no ties)."""
+    import dcnr
+    g = torch.Generator(device=dev).manual_seed(11 + Q)
+    table = torch.randn(1_000_000, 64, device=dev, generator=g)
+    q = torch.randn(Q, 64, device=dev, generator=g)
+    nn_ = dcnr.NearestNeighbors(metric="cosine", algorithm="brute").fit(table)
+    d, i = nn_.kneighbors(q, n_neighbors=11)
+    d = np.asarray(d.cpu() if torch.is_tensor(d) else d)
+    i = np.asarray(i.cpu() if torch.is_tensor(i) else i)
+    tn = table / table.norm(dim=1, keepdim=True)
+    qn = q / q.norm(dim=1, keepdim=True)
+    ref_d, ref_i = torch.topk(1.0 - qn @ tn.T, 11, dim=1, largest=False)
+    ref_d, ref_i = ref_d.cpu().numpy(), ref_i.cpu().numpy()
+    np.testing.assert_allclose(d, ref_d, rtol=0, atol=2e-6)
+    for r in range(Q):
+        near = np.diff(ref_d[r]) <= 2e-6
+        isolated = np.ones(11, bool)
+        isolated[1:] &= ~near
+        isolated[:-1] &= ~near
+        np.testing.assert_array_equal(i[r][isolated], ref_i[r][isolated])
+
+
 @pytest.mark.parametrize("M,K,N,out_f32", [(4096, 512, 512, 0), (1000, 456, 512, 1),
                                            (333, 64, 96, 0), (70000, 128, 256, 1)])
 def test_linear_bf16_vs_torch(dev, M, K, N, out_f32):
