@@ -44,11 +44,20 @@ namespace {
 #endif
 constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
 
+#ifndef WS_TM_RESID
+#define WS_TM_RESID 32
+#endif
+#ifndef WS_RESID_EARLY
+#define WS_RESID_EARLY 1   // lab, K = N = 512: 90.5 us early vs 96.4 us one row block ahead
+#endif
 template <int EPI> constexpr int ws_tm() {
-  return (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU) ? 32 : EPI == NT_EPI_RESID_BN ? 32
+  return (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU) ? WS_TM_RESID : EPI == NT_EPI_RESID_BN ? 32
          : EPI == NT_EPI_DROP_BN ? 64 : WS_TM_PLAIN;
 }
-template <int EPI> constexpr bool ws_ops_early() { return EPI == NT_EPI_RESID_BN; }
+template <int EPI> constexpr bool ws_ops_early() {
+  return EPI == NT_EPI_RESID_BN ||
+         (WS_RESID_EARLY && (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU));
+}
 // X-tile buffers in the LDS ring: the next NB-1 tiles are in flight while one
 // is consumed.  Only the epilogues without operand loads can use NB > 2 (an
 // operand load's wait would also wait for every older tile DMA).
