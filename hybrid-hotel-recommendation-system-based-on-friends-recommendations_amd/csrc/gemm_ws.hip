@@ -47,15 +47,21 @@ constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
 #ifndef WS_TM_RESID
 #define WS_TM_RESID 32
 #endif
+#ifndef WS_TM_DROP
+#define WS_TM_DROP 32   // lab, K = N = 512, 1-bit masks: 104.7 us (32 rows, early) vs 111.9 us (64 rows, late)
+#endif
+#ifndef WS_DROP_EARLY
+#define WS_DROP_EARLY 1
+#endif
 #ifndef WS_RESID_EARLY
 #define WS_RESID_EARLY 1   // lab, K = N = 512: 90.5 us early vs 96.4 us one row block ahead
 #endif
 template <int EPI> constexpr int ws_tm() {
   return (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU) ? WS_TM_RESID : EPI == NT_EPI_RESID_BN ? 32
-         : EPI == NT_EPI_DROP_BN ? 64 : WS_TM_PLAIN;
+         : EPI == NT_EPI_DROP_BN ? WS_TM_DROP : WS_TM_PLAIN;
 }
 template <int EPI> constexpr bool ws_ops_early() {
-  return EPI == NT_EPI_RESID_BN ||
+  return EPI == NT_EPI_RESID_BN || (WS_DROP_EARLY && EPI == NT_EPI_DROP_BN) ||
          (WS_RESID_EARLY && (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU));
 }
 // X-tile buffers in the LDS ring: the next NB-1 tiles are in flight while one

@@ -61,6 +61,12 @@ int main(int argc, char** argv) {
   a.R = R; a.ldr = ldc; a.H = H; a.ldh = ldc; a.T = T; a.ldt = ldc; a.hscale = 2.5f;
   a.mean = mean; a.invstd = istd;
   if (epi >= dcnr::NT_EPI_RESID_BN) a.bias = nullptr;
+  if (argc > 6 && atoi(argv[6])) {   // 1-bit keep masks (the production RESID_BN / DROP_BN form)
+    uint32_t* hb;
+    hipMalloc(&hb, M * (N / 32) * 4);
+    hipMemset(hb, 0x5a, M * (N / 32) * 4);
+    a.Hb = hb; a.ldhb = N / 32;
+  }
   int np1 = 0, np2 = 0;
   if (check) {
     dcnr::NtArgs a1 = a, a2 = a;
