@@ -47,6 +47,9 @@ constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
 #ifndef WS_TM_RESID
 #define WS_TM_RESID 32
 #endif
+#ifndef WS_TM_RBN
+#define WS_TM_RBN 32
+#endif
 #ifndef WS_TM_DROP
 #define WS_TM_DROP 32   // lab, K = N = 512, 1-bit masks: 104.7 us (32 rows, early) vs 111.9 us (64 rows, late)
 #endif
@@ -57,7 +60,7 @@ constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
 #define WS_RESID_EARLY 1   // lab, K = N = 512: 90.5 us early vs 96.4 us one row block ahead
 #endif
 template <int EPI> constexpr int ws_tm() {
-  return (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU) ? WS_TM_RESID : EPI == NT_EPI_RESID_BN ? 32
+  return (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU) ? WS_TM_RESID : EPI == NT_EPI_RESID_BN ? WS_TM_RBN
          : EPI == NT_EPI_DROP_BN ? WS_TM_DROP : WS_TM_PLAIN;
 }
 template <int EPI> constexpr bool ws_ops_early() {

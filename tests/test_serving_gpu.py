@@ -130,3 +130,24 @@ def test_device_loader_matches_dataloader(dev):
         for g, r in zip(got, ref):
             for a, b in zip(g, r):
                 assert torch.equal(a.cpu(), b)
+
+
+@pytest.mark.parametrize("n,d,top_k", [(400, 64, 20), (700, 64, 12), (1500, 16, 10),
+                                       (3000, 16, 6)])
+def test_mmr_lds_and_table_paths(dev, n, d, top_k):
+    """dcnr_mmr_rerank stages the candidates' rows in LDS when n*(d+1)+n floats
+    fit 128 KiB (400 x 64, 1500 x 16) and re-reads the table otherwise
+    (700 x 64, 3000 x 16): both against the rerank_with_mmr restatement, with
+    rows absent from the mapping (-1) mixed in."""
+    from dcnr import serving
+    rng = np.random.default_rng(n + d)
+    n_items = 5000
+    emb = rng.standard_normal((n_items, d)).astype(np.float32)
+    rows = rng.choice(n_items, n, replace=False).astype(np.int64)
+    rows[rng.choice(np.arange(1, n), n // 50, replace=False)] = -1
+    scores = np.sort(rng.random(n).astype(np.float32))[::-1].copy()
+    table = torch.from_numpy(emb).to(dev)
+    inv = serving.row_inv_norms(table)
+    got = serving.mmr_positions(table, inv, torch.from_numpy(rows), torch.from_numpy(scores),
+                                0.7, top_k).cpu().tolist()
+    assert got == orc.mmr_rerank(emb, rows.tolist(), scores, 0.7, top_k)
