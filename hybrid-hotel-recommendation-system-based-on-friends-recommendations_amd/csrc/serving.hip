@@ -26,7 +26,7 @@ namespace {
 
 constexpr int SV_NT = 1024;
 constexpr int SV_MAX = 4096;   // max candidates per call (LDS sort capacity)
-constexpr size_t MMR_LDS_MAX = 128 * 1024;   // dynamic LDS of mmr_lds_kernel
+constexpr size_t MMR_LDS_MAX = 152 * 1024;   // dynamic LDS of mmr_lds_kernel (+ ~4 KiB static)
 
 // ascending bitonic sort of n2 (power of two) (key, val) pairs in LDS;
 // less(a, b) on (key, val)
@@ -206,18 +206,21 @@ __global__ __launch_bounds__(SV_NT) void mmr_kernel(const float* table, const fl
   if (threadIdx.x == 0) *out_count = cnt;
 }
 
+// The same greedy MMR with everything a selection round touches on chip:
+// the candidates' raw rows (stride d+1: one row per thread, conflict-free)
+// and inverse norms in LDS, each thread's candidates (t = tid + j*SV_NT) --
+// validity, score, max similarity, taken -- in registers, so a round is one
+// dot product per candidate and a block argmax (its two barriers), with no
+// global loads.  Arithmetic as in mmr_kernel: s = sum_c row[c] * (sel[c] * is)
+// in c order, then * inv.
 __global__ __launch_bounds__(SV_NT) void mmr_lds_kernel(const float* table, const float* inv, int d,
                                                     const int64_t* rows, const float* scores,
                                                     int n, float lambda, int top_k,
                                                     int64_t* out_pos, int32_t* out_count) {
-  __shared__ float maxsim[SV_MAX];
-  __shared__ unsigned char taken[SV_MAX];
+  constexpr int MR = SV_MAX / SV_NT;   // candidates per thread
   __shared__ float sv[SV_NT / 64];
   __shared__ int sp[SV_NT / 64];
-  __shared__ float selv[256];
-  __shared__ int any_sel;
-  // the candidates' raw rows (stride d+1: one row per thread, conflict-free)
-  // and inverse norms, loaded once instead of re-read every selection round
+  __shared__ unsigned char vld[SV_MAX];
   extern __shared__ float lds_rows[];
   float* invs = lds_rows + (size_t)n * (d + 1);
   for (int e = threadIdx.x; e < n * d; e += SV_NT) {
@@ -225,46 +228,59 @@ __global__ __launch_bounds__(SV_NT) void mmr_lds_kernel(const float* table, cons
     const int64_t r = rows[t];
     lds_rows[t * (d + 1) + c] = r >= 0 ? table[r * d + c] : 0.f;
   }
-  for (int t = threadIdx.x; t < n; t += SV_NT) invs[t] = rows[t] >= 0 ? inv[rows[t]] : 0.f;
-  for (int t = threadIdx.x; t < n; t += SV_NT) { maxsim[t] = -FLT_MAX; taken[t] = 0; }
-  if (threadIdx.x == 0) { any_sel = 0; taken[0] = 1; out_pos[0] = 0; }
+  bool ok[MR], tk[MR];
+  float sc[MR], ms[MR];
+#pragma unroll
+  for (int j = 0; j < MR; ++j) {
+    const int t = threadIdx.x + j * SV_NT;
+    const int64_t r = t < n ? rows[t] : -1;
+    ok[j] = r >= 0;
+    tk[j] = t == 0;
+    sc[j] = t < n ? scores[t] : 0.f;
+    ms[j] = -FLT_MAX;
+    if (t < n) {
+      invs[t] = r >= 0 ? inv[r] : 0.f;
+      vld[t] = r >= 0;
+    }
+  }
+  if (threadIdx.x == 0) out_pos[0] = 0;
   __syncthreads();
   const int want = min(top_k, n);
   int cnt = 1, last = 0;
+  bool sel = false;
   for (;;) {
     // fold the last selected item into every candidate's max similarity
-    const int64_t sr = rows[last];
-    if (sr >= 0) {
+    if (vld[last]) {
       const float is = invs[last];
-      for (int t = threadIdx.x; t < d; t += SV_NT) selv[t] = lds_rows[last * (d + 1) + t] * is;
-      __syncthreads();
-      for (int t = threadIdx.x; t < n; t += SV_NT) {
-        const int64_t r = rows[t];
-        if (r < 0 || taken[t]) continue;
+      const float* sr = lds_rows + last * (d + 1);
+#pragma unroll
+      for (int j = 0; j < MR; ++j) {
+        const int t = threadIdx.x + j * SV_NT;
+        if (t >= n || !ok[j] || tk[j]) continue;
         const float* rw = lds_rows + t * (d + 1);
         float s = 0.f;
-        for (int c = 0; c < d; ++c) s += rw[c] * selv[c];
+        for (int c = 0; c < d; ++c) s += rw[c] * (sr[c] * is);
         s *= invs[t];
-        maxsim[t] = fmaxf(maxsim[t], s);
+        ms[j] = fmaxf(ms[j], s);
       }
-      if (threadIdx.x == 0) any_sel = 1;
-      __syncthreads();
+      sel = true;
     }
     if (cnt >= want) break;
     float v = -FLT_MAX;
     int p = INT_MAX;
-    const bool sel = any_sel != 0;
-    for (int t = threadIdx.x; t < n; t += SV_NT) {
-      if (taken[t] || rows[t] < 0) continue;
-      const float m = lambda * scores[t] - (1.f - lambda) * (sel ? maxsim[t] : 0.f);
+#pragma unroll
+    for (int j = 0; j < MR; ++j) {
+      const int t = threadIdx.x + j * SV_NT;
+      if (t >= n || tk[j] || !ok[j]) continue;
+      const float m = lambda * sc[j] - (1.f - lambda) * (sel ? ms[j] : 0.f);
       if (p == INT_MAX || m > v || (m == v && t < p)) { v = m; p = t; }
     }
     float bv;
     int bp;
     block_argmax(v, p, sv, sp, bv, bp);
     if (bp == INT_MAX) break;
-    if (threadIdx.x == 0) { taken[bp] = 1; out_pos[cnt] = bp; }
-    __syncthreads();
+    if (bp % SV_NT == (int)threadIdx.x) tk[bp / SV_NT] = true;   // the owner thread
+    if (threadIdx.x == 0) out_pos[cnt] = bp;
     ++cnt;
     last = bp;
   }

@@ -136,7 +136,7 @@ def test_device_loader_matches_dataloader(dev):
                                        (3000, 16, 6)])
 def test_mmr_lds_and_table_paths(dev, n, d, top_k):
     """dcnr_mmr_rerank stages the candidates' rows in LDS when n*(d+1)+n floats
-    fit 128 KiB (400 x 64, 1500 x 16) and re-reads the table otherwise
+    fit 152 KiB (400 x 64, 1500 x 16) and re-reads the table otherwise
     (700 x 64, 3000 x 16): both against the rerank_with_mmr restatement, with
     rows absent from the mapping (-1) mixed in."""
     from dcnr import serving
