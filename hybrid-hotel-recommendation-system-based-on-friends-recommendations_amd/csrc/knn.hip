@@ -436,19 +436,31 @@ __global__ __launch_bounds__(K2_NT) void scan3_kernel(const float* __restrict__ 
 // distance <= the k-th best of any subset, so rows above the bound are never
 // appended: the wave lists then see a handful of rows instead of refilling
 // and re-sorting while their own thresholds converge.
-constexpr int TH_S = 512;
+#ifndef KNN_TH_S
+#define KNN_TH_S 512
+#endif
+constexpr int TH_S = KNN_TH_S;   // sample rows: the bound sits near quantile k / TH_S
 constexpr float TH_MARGIN = 1e-5f;
 
+// The k-th smallest sample distance by a 2-pass radix select over the
+// distances' bits (exponent + 7 mantissa bits): the upper edge of the
+// selected bin, an upper bound within 2^-7 relative of the exact k-th value.
 template <int DV>
 __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict__ tab,
                                                         const float* __restrict__ inv, int64_t N,
                                                         const float* __restrict__ qn, int k,
                                                         float* thr0) {
-  __shared__ float key[TH_S];
+  constexpr int PT = TH_S / 256;
+  __shared__ unsigned hist[256];
+  __shared__ unsigned sel_prefix, sel_need;
+  __shared__ int sel_fail;
   const int64_t qq = blockIdx.x;
   const float4* qv = reinterpret_cast<const float4*>(qn + qq * DV * 4);
   const int S = (int)min<int64_t>(N, TH_S);
-  for (int t = threadIdx.x; t < TH_S; t += 256) {
+  unsigned key[PT];
+#pragma unroll 4
+  for (int j = 0; j < PT; ++j) {
+    const int t = threadIdx.x + j * 256;
     float dist = FLT_MAX;
     if (t < S) {
       const float4* rp = reinterpret_cast<const float4*>(tab + (int64_t)t * DV * 4);
@@ -463,20 +475,52 @@ __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict_
       }
       dist = fminf(fmaxf(1.f - s * inv[t], 0.f), 2.f);
     }
-    key[t] = dist;
+    key[j] = __float_as_uint(dist) & 0x7fffffffu;   // >= 0: bits order like values
   }
-  __syncthreads();
-  for (int k2 = 2; k2 <= TH_S; k2 <<= 1)
-    for (int j = k2 >> 1; j > 0; j >>= 1) {
-      {
-        const int t = threadIdx.x;
-        const int lo = ((t & ~(j - 1)) << 1) | (t & (j - 1)), hi = lo + j;
-        const float a = key[lo], b = key[hi];
-        if (((lo & k2) == 0) == (b < a)) { key[lo] = b; key[hi] = a; }
+  if (threadIdx.x == 0) { sel_prefix = 0; sel_need = (unsigned)k; sel_fail = S < k; }
+  unsigned mask = 0;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int sh = 24 - 8 * pass;
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    const unsigned prefix = sel_prefix;
+#pragma unroll
+    for (int j = 0; j < PT; ++j)
+      if ((key[j] & mask) == prefix) atomicAdd(&hist[(key[j] >> sh) & 255u], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      const unsigned need = sel_need;
+      unsigned h[4], sum = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) { h[b] = hist[4 * lane + b]; sum += h[b]; }
+      unsigned incl = sum;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const unsigned v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
       }
-      __syncthreads();
+      unsigned cum = incl - sum;
+      if (cum < need && need <= incl) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (cum + h[b] >= need) {
+            sel_prefix = prefix | ((unsigned)(4 * lane + b) << sh);
+            sel_need = need - cum;
+            break;
+          }
+          cum += h[b];
+        }
+      }
     }
-  if (threadIdx.x == 0) thr0[qq] = S >= k ? key[k - 1] + TH_MARGIN : FLT_MAX;
+    mask |= 255u << sh;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float kth = __uint_as_float(sel_prefix | 0xffffu);
+    thr0[qq] = (sel_fail || !(kth < 2.5f)) ? FLT_MAX : kth + TH_MARGIN;
+  }
 }
 
 __global__ void fill_kernel(float* p, int64_t n, float v) {
