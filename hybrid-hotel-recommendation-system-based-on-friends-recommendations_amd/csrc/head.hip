@@ -23,6 +23,49 @@ __global__ __launch_bounds__(NT) void row_dot_kernel(const T* X, int ld, int N, 
   }
 }
 
+// bf16 rows, N % 8 == 0, N <= 64 * CPL: 8 lanes per row, each lane CPL
+// 16-byte chunks (chunks j, j+8, ... of 8 columns: 128 B contiguous per 8
+// lanes and load), its w slice held in registers; 3-step lane-group sum.
+template <int CPL>
+__global__ __launch_bounds__(NT) void row_dot8_kernel(const bf16* X, int ld, int N, const float* w,
+                                                      int64_t B, float* out) {
+  const int lane = threadIdx.x & 63, g = lane >> 3, j = lane & 7;
+  const int nch = N / 8;
+  float wr[CPL][8];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i) {
+    const int c = j + 8 * i;
+    const float4 lo = c < nch ? reinterpret_cast<const float4*>(w + 8 * c)[0] : float4{0.f, 0.f, 0.f, 0.f};
+    const float4 hi = c < nch ? reinterpret_cast<const float4*>(w + 8 * c)[1] : float4{0.f, 0.f, 0.f, 0.f};
+    wr[i][0] = lo.x; wr[i][1] = lo.y; wr[i][2] = lo.z; wr[i][3] = lo.w;
+    wr[i][4] = hi.x; wr[i][5] = hi.y; wr[i][6] = hi.z; wr[i][7] = hi.w;
+  }
+  const int64_t nwv = (int64_t)gridDim.x * (NT / WAVE);
+  for (int64_t r0 = ((int64_t)blockIdx.x * (NT / WAVE) + (threadIdx.x >> 6)) * 8; r0 < B; r0 += nwv * 8) {
+    const int64_t b = r0 + g;
+    float sum = 0.f;
+    if (b < B) {
+      u32x4 v[CPL];
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const int c = j + 8 * i;
+        v[i] = c < nch ? *reinterpret_cast<const u32x4*>(X + b * ld + 8 * c) : u32x4{0, 0, 0, 0};
+      }
+#pragma unroll
+      for (int i = 0; i < CPL; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          sum += __uint_as_float(v[i][e] << 16) * wr[i][2 * e];
+          sum += __uint_as_float(v[i][e] & 0xffff0000u) * wr[i][2 * e + 1];
+        }
+    }
+    sum += __shfl_xor(sum, 1, 64);
+    sum += __shfl_xor(sum, 2, 64);
+    sum += __shfl_xor(sum, 4, 64);
+    if (j == 0 && b < B) out[b] = sum;
+  }
+}
+
 __global__ void logits_kernel(const float* zdeep, const float* zc, const float* bf, int64_t B,
                               float* z) {
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -108,7 +151,14 @@ dcnr_status row_dot(int precision, const void* X, int ld, int N, const float* w,
                     float* out, hipStream_t s) {
   if (B <= 0) return DCNR_OK;
   int64_t blocks = std::min<int64_t>(cdiv(B, NT / WAVE), 4096);
-  if (precision == DCNR_PREC_BF16)
+  if (precision == DCNR_PREC_BF16 && N % 8 == 0 && ld % 8 == 0 && N <= 512 &&
+      ((uintptr_t)X & 15) == 0 && ((uintptr_t)w & 15) == 0) {
+    const int64_t b8 = std::min<int64_t>(cdiv(B, 8 * (NT / WAVE)), 1024);
+    if (N <= 256)
+      hipLaunchKernelGGL(row_dot8_kernel<4>, dim3((unsigned)b8), dim3(NT), 0, s, (const bf16*)X, ld, N, w, B, out);
+    else
+      hipLaunchKernelGGL(row_dot8_kernel<8>, dim3((unsigned)b8), dim3(NT), 0, s, (const bf16*)X, ld, N, w, B, out);
+  } else if (precision == DCNR_PREC_BF16)
     hipLaunchKernelGGL(row_dot_kernel<bf16>, dim3((unsigned)blocks), dim3(NT), 0, s,
                        (const bf16*)X, ld, N, w, B, out);
   else
