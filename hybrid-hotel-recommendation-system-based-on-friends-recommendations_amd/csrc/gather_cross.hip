@@ -24,7 +24,9 @@
 // atomics (128-B row segments, executed memory-side and overlapped with the
 // kernel's own work).  Measured alternative (kept out): privatising the small
 // categorical tables in LDS (per-sample dcat stores + an LDS-atomic per-table
-// pass) cost 285 us against +30 us for the inline atomics at cfg3.
+// pass) cost 285 us against +30 us for the inline atomics at cfg3 (an early
+// version of this kernel; on the current one the scatter costs 142 of 306 us,
+// tools/gather_lab.hip modes 0 / 8, so the privatised form is worth a retry).
 #include "dcnr_internal.h"
 
 #include <cstring>
