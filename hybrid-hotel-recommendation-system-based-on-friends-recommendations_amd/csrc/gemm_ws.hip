@@ -47,6 +47,9 @@ constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
 #ifndef WS_TM_RESID
 #define WS_TM_RESID 32
 #endif
+#ifndef WS_TM_BNRELU
+#define WS_TM_BNRELU 32   // lab, K = N = 512: 71.5 us vs 75.4-77.2 us at 64 rows
+#endif
 #ifndef WS_TM_RBN
 #define WS_TM_RBN 32
 #endif
@@ -61,7 +64,7 @@ constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
 #endif
 template <int EPI> constexpr int ws_tm() {
   return (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU) ? WS_TM_RESID : EPI == NT_EPI_RESID_BN ? WS_TM_RBN
-         : EPI == NT_EPI_DROP_BN ? WS_TM_DROP : WS_TM_PLAIN;
+         : EPI == NT_EPI_DROP_BN ? WS_TM_DROP : EPI == NT_EPI_BN_RELU ? WS_TM_BNRELU : WS_TM_PLAIN;
 }
 template <int EPI> constexpr bool ws_ops_early() {
   return EPI == NT_EPI_RESID_BN || (WS_DROP_EARLY && EPI == NT_EPI_DROP_BN) ||

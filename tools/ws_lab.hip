@@ -60,6 +60,7 @@ int main(int argc, char** argv) {
   a.X = X; a.ldx = ldx; a.M = M; a.K = K; a.W = W; a.ldw = K; a.N = N; a.ldc = ldc; a.bias = b;
   a.R = R; a.ldr = ldc; a.H = H; a.ldh = ldc; a.T = T; a.ldt = ldc; a.hscale = 2.5f;
   a.mean = mean; a.invstd = istd;
+  a.bn_scale = istd; a.bn_shift = mean;   // eval BN epilogues (6, 7)
   if (epi >= dcnr::NT_EPI_RESID_BN) a.bias = nullptr;
   if (argc > 6 && atoi(argv[6])) {   // 1-bit keep masks (the production RESID_BN / DROP_BN form)
     uint32_t* hb;
