@@ -379,19 +379,11 @@ dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train
   return DCNR_OK;
 }
 
-// The bf16 streaming GEMM: weight-stationary kernel (gemm_ws.hip), or the
-// weight-in-LDS one (gemm_nt.hip) when DCNR_GEMM_NT is set (A/B comparisons).
-dcnr_status gemm_stream(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr) {
-  static const bool nt = getenv("DCNR_GEMM_NT") != nullptr;
-  return nt ? gemm_nt(epi, a, s, nparts) : gemm_ws(epi, a, s, nparts);
-}
-
-// C = A . B^T with k-contiguous operands: bf16 -> the weight-resident streaming
-// kernel (gemm_nt.hip) when the weight fits LDS; otherwise the generic tiled
-// MFMA kernel (fp32 parity path, K > 512).
+// C = A . B^T with k-contiguous operands: bf16 -> the weight-stationary
+// streaming kernel (gemm_ws.hip) when the weight fits its registers (K <= 512);
+// otherwise the generic tiled MFMA kernel (fp32 parity path, K > 512).
 dcnr_status gemm_nn(int prec, int epi, const GemmArgs& g, int splits, hipStream_t s) {
-  if (prec == DCNR_PREC_BF16 && splits == 1 && gemm_nt_supported(g.K, g.N) &&
-      getenv("DCNR_DISABLE_GEMM_NT") == nullptr) {
+  if (prec == DCNR_PREC_BF16 && splits == 1 && gemm_ws_supported(g.K, g.N)) {
     NtArgs a;
     memset(&a, 0, sizeof(a));
     a.X = (const bf16*)g.A; a.ldx = g.lda; a.M = g.M; a.K = (int)g.K;
@@ -399,7 +391,7 @@ dcnr_status gemm_nn(int prec, int epi, const GemmArgs& g, int splits, hipStream_
     a.C = g.C; a.ldc = g.ldc; a.bias = g.bias;
     a.R = g.resid; a.ldr = g.ldr;
     int ne = epi == EPI_STORE_RESID ? NT_EPI_RESID : (g.out_f32 ? NT_EPI_F32 : NT_EPI_BIAS);
-    return gemm_stream(ne, a, s);
+    return gemm_ws(ne, a, s);
   }
   return gemm(prec, false, false, epi, g, splits, s);
 }
@@ -416,32 +408,12 @@ dcnr_status linear_fwd(const Dims& d, const void* A, int lda, const void* W, int
 
 // Stats epilogues of the streaming GEMM (BN column partials produced by the
 // GEMM that writes the BN input / the BN output gradient) -- bf16 only.
-bool epi_stats_ok(const Dims& d) {
-  static const bool off = getenv("DCNR_DISABLE_EPI_STATS") != nullptr ||
-                          getenv("DCNR_DISABLE_GEMM_NT") != nullptr;
-  return d.prec == DCNR_PREC_BF16 && !off && gemm_nt_supported(d.Hp, d.Hp);
-}
-
-// t = A W^T + b  and  part = BN column partials of t, shifted by b
-// In-kernel BN finalize (gemm_ws last-arriver) when no SyncBN hook has to see
-// the sums first and the GEMM is one launch.
-bool gemm_final_ok(const dcnr_model_desc* desc, const NtArgs& a, int epi) {
-  // opt-in: the last-arriver tail costs more than the reduce launch it saves
-  // (its fixed-order reduction is a serial chain of dependent loads)
-  static const bool off = getenv("DCNR_GEMM_NT") != nullptr ||
-                          getenv("DCNR_GEMM_FINAL") == nullptr;
-  return !off && !desc->bn_allreduce && gemm_ws_single_launch(a, epi);
-}
+bool epi_stats_ok(const Dims& d) { return masks_ok(d) && gemm_ws_supported(d.Hp, d.Hp); }
 
 // Eval forward with BatchNorm (running statistics) + ReLU (+ residual) in the
 // streaming GEMM's epilogue: no t1/t2 round trip through HBM and no rowwise
 // passes (bf16, gemm_ws shapes).
-bool eval_fuse_ok(const Dims& d) {
-  static const bool off = getenv("DCNR_DISABLE_EVAL_FUSE") != nullptr ||
-                          getenv("DCNR_GEMM_NT") != nullptr ||
-                          getenv("DCNR_DISABLE_GEMM_NT") != nullptr;
-  return d.prec == DCNR_PREC_BF16 && !off && gemm_nt_supported(d.Hp, d.Hp);
-}
+bool eval_fuse_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && gemm_ws_supported(d.Hp, d.Hp); }
 
 // out = relu((A W^T + b) * bn.scale + bn.shift [+ R])
 dcnr_status linear_bn_relu(const Dims& d, const void* A, const void* W, const float* bias,
@@ -456,11 +428,9 @@ dcnr_status linear_bn_relu(const Dims& d, const void* A, const void* W, const fl
   return gemm_ws(R ? NT_EPI_BN_RESID_RELU : NT_EPI_BN_RELU, a, s);
 }
 
-// *fin_done = 1 when rf was applied inside the GEMM (else the caller reduces
-// the nc partial rows in L.part)
-dcnr_status linear_fwd_stats(const dcnr_model_desc* desc, const Dims& d, const Layout& L,
-                             const void* A, int lda, const void* W, int K, const float* bias,
-                             void* out, int64_t B, const RedFinal& rf, int* nc, int* fin_done,
+// t = A W^T + b  and  part = BN column partials of t, shifted by b (nc rows)
+dcnr_status linear_fwd_stats(const Dims& d, const Layout& L, const void* A, int lda, const void* W,
+                             int K, const float* bias, void* out, int64_t B, int* nc,
                              hipStream_t s) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
@@ -468,36 +438,25 @@ dcnr_status linear_fwd_stats(const dcnr_model_desc* desc, const Dims& d, const L
   a.W = (const bf16*)W; a.ldw = K; a.N = d.Hp;
   a.C = out; a.ldc = d.Hp; a.bias = bias;
   a.part = L.part;
-  *fin_done = gemm_final_ok(desc, a, NT_EPI_BIAS_STATS) ? 1 : 0;
-  if (*fin_done) {
-    a.fin = 1; a.fin_shift = 1; a.fin_nr = d.H; a.rf = rf;
-    a.rf.counter = L.red_cnt + RED_MAX_CGRP;
-  }
-  return gemm_stream(NT_EPI_BIAS_STATS, a, s, nc);
+  return gemm_ws(NT_EPI_BIAS_STATS, a, s, nc);
 }
 
 // C = mask(H) * (X W^T [+ R]) and part = [sum C, sum C*xhat(T)] (BN backward)
-dcnr_status linear_dx_bn(const dcnr_model_desc* desc, const Dims& d, const Layout& L, int epi,
-                         const void* X, const void* Wt, const void* R, void* C, const void* H,
-                         const uint8_t* Hbits, float hscale, const void* T, const BnBufs& bn,
-                         int64_t B, const RedFinal& rf, int* nc, int* fin_done, hipStream_t s) {
+dcnr_status linear_dx_bn(const Dims& d, const Layout& L, int epi, const void* X, const void* Wt,
+                         const void* R, void* C, const uint8_t* Hbits, float hscale,
+                         const void* T, const BnBufs& bn, int64_t B, int* nc, hipStream_t s) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
   a.X = (const bf16*)X; a.ldx = d.Hp; a.M = B; a.K = d.Hp;
   a.W = (const bf16*)Wt; a.ldw = d.Hp; a.N = d.Hp;
   a.C = C; a.ldc = d.Hp;
   a.R = R; a.ldr = d.Hp;
-  a.H = (const bf16*)H; a.ldh = d.Hp; a.hscale = hscale;
+  a.hscale = hscale;
   a.Hb = (const uint32_t*)Hbits; a.ldhb = d.Hp / 32;
   a.T = (const bf16*)T; a.ldt = d.Hp;
   a.mean = bn.mean; a.invstd = bn.invstd;
   a.part = L.part;
-  *fin_done = gemm_final_ok(desc, a, epi) ? 1 : 0;
-  if (*fin_done) {
-    a.fin = 1; a.fin_shift = 0; a.fin_nr = d.H; a.rf = rf;
-    a.rf.counter = L.red_cnt + RED_MAX_CGRP;
-  }
-  return gemm_stream(epi, a, s, nc);
+  return gemm_ws(epi, a, s, nc);
 }
 
 // dW[N][Kc] = sum_b dY[b][n] X[b][k]   (real extents Nr x Kr written to out)
@@ -525,8 +484,7 @@ dcnr_status wgrad_bf16(const void* dY, int64_t ldy, int N, const void* X, int64_
 dcnr_status linear_dw(const Dims& d, const Layout& L, const void* dY, int ldy, int N,
                       const void* X, int ldx, int Kc, int64_t B, float* out, int Nr, int Kr,
                       int accumulate, hipStream_t s) {
-  if (d.prec == DCNR_PREC_BF16 && gemm_dw_supported(N, Kc, ldy, ldx, B) &&
-      getenv("DCNR_DISABLE_GEMM_DW") == nullptr)
+  if (d.prec == DCNR_PREC_BF16 && gemm_dw_supported(N, Kc, ldy, ldx, B))
     return wgrad_bf16(dY, ldy, N, X, ldx, Kc, B, L.slab, L.slab_elems, out, Nr, Kr, accumulate, s);
   int64_t tiles = cdiv(N, 128) * cdiv(Kc, 128);
   int64_t S = std::max<int64_t>(1, std::min<int64_t>(512 / tiles, cdiv(B, 256)));
@@ -757,32 +715,24 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   for (int j = 0; j < d.R; ++j) {
     const auto& Bk = P.blk[j];
     const bool fuse = train && epi_stats_ok(d);   // BN partials from the GEMM epilogue
-    int nc = 0, fin = 0;
+    int nc = 0;
     if (fuse)
-      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(desc, d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j],
-                                             L.t1[j], B,
-                                             bn_fwd_rf(L, B, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
-                                                       L.bn[2 * j]),
-                                             &nc, &fin, s));
+      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j],
+                                             B, &nc, s));
     else
       TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
-    if (!fin)
-      TRY(bn_layer_fwd(desc, d, L, L.t1[j], B, train, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
-                       L.bn[2 * j], s, nc, fuse ? L.b1p[j] : nullptr));
+    TRY(bn_layer_fwd(desc, d, L, L.t1[j], B, train, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
+                     L.bn[2 * j], s, nc, fuse ? L.b1p[j] : nullptr));
     void* a1 = train ? L.a1s[j] : L.a1;
     TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
                      dropout_seed, j, s, train ? L.mask_a1[j] : nullptr));
     if (fuse)
-      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(desc, d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j],
-                                             L.t2[j], B,
-                                             bn_fwd_rf(L, B, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
-                                                       L.bn[2 * j + 1]),
-                                             &nc, &fin, s));
+      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B,
+                                             &nc, s));
     else
       TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
-    if (!fin)
-      TRY(bn_layer_fwd(desc, d, L, L.t2[j], B, train, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
-                       L.bn[2 * j + 1], s, nc, fuse ? L.b2p[j] : nullptr));
+    TRY(bn_layer_fwd(desc, d, L, L.t2[j], B, train, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
+                     L.bn[2 * j + 1], s, nc, fuse ? L.b2p[j] : nullptr));
     const bool head = j == d.R - 1 && bn_add_relu_head_supported(d.prec, d.Hp);
     if (head)   // last block: residual + ReLU + deep head dot + logits in one pass
       TRYP(DCNR_K_ROWWISE, bn_add_relu_head(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
@@ -833,7 +783,6 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   const bool fuse = epi_stats_ok(d);   // BN partials from the dX GEMM epilogues
   int nc_du = 0;   // > 0: L.du and its BN2 partials were made by the previous dX GEMM
-  int fin_du = 0;  // ... and that GEMM also finalised them (BN2 backward done)
   for (int j = d.R - 1; j >= 0; --j) {
     const auto& Bk = P.blk[j];
     auto& Gk = Gr.blk[j];
@@ -842,9 +791,8 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     int nc = 0;
     // ---- out = relu(BN2(t2) + h_j):  du, BN2 backward
     if (nc_du) {
-      if (!fin_du)
-        TRY(bn_bwd_reduce(desc, d, L, nc_du, 2, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, nullptr,
-                          Gk.b2, accumulate, s));
+      TRY(bn_bwd_reduce(desc, d, L, nc_du, 2, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, nullptr,
+                        Gk.b2, accumulate, s));
     } else {
       TRYP(DCNR_K_ROWWISE, bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean,
                                           bn2.invstd, B, Hp, Hp, L.du, L.part, &nc, s));
@@ -856,18 +804,13 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
                        L.dt2, L.part, &nc, s));
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
     TRY(linear_dw(d, L, L.dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s));
-    int fin1 = 0;
     if (fuse) {
       // dy1 = (dt2 W2) * [a1 != 0] / (1-p): relu and dropout masks from the
       // saved activation, BN1 partials (and, without SyncBN, its backward
       // coefficients and dgamma/dbeta) in the same pass
-      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(desc, d, L, NT_EPI_DROP_BN, L.dt2, L.W2t[j], nullptr, L.da,
-                                        L.a1s[j], L.mask_a1[j], p > 0.f ? 1.f / (1.f - p) : 1.f,
-                                        L.t1[j], bn1,
-                                        B,
-                                        bn_bwd_rf(L, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr,
-                                                  Gk.b1, accumulate),
-                                        &nc, &fin1, s));
+      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(d, L, NT_EPI_DROP_BN, L.dt2, L.W2t[j], nullptr, L.da,
+                                        L.mask_a1[j], p > 0.f ? 1.f / (1.f - p) : 1.f, L.t1[j],
+                                        bn1, B, &nc, s));
     } else {
       GemmArgs g;
       memset(&g, 0, sizeof(g));
@@ -878,8 +821,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRYP(DCNR_K_ROWWISE, bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean,
                                          bn1.invstd, B, Hp, Hp, p, dropout_seed, j, L.part, &nc, s));
     }
-    if (!fin1)
-      TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
+    TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
                         accumulate, s));
     TRYP(DCNR_K_ROWWISE, bwd_bn1_apply2(d.prec, L.da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, L.a1,
                        L.part, &nc, s));
@@ -889,12 +831,8 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       // G is only consumed by block j-1's BN2 backward: emit its du = G * [h_j > 0]
       // (in place over this block's du, the residual operand) and the partials
       const BnBufs& bp = L.bn[2 * (j - 1) + 1];
-      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(desc, d, L, NT_EPI_RESID_BN, L.a1, L.W1t[j], L.du, L.du,
-                                        L.h[j], L.mask_h[j], 1.f, L.t2[j - 1], bp, B,
-                                        bn_bwd_rf(L, B, P.blk[j - 1].g2, bp.invstd,
-                                                  Gr.blk[j - 1].g2, Gr.blk[j - 1].be2, nullptr,
-                                                  Gr.blk[j - 1].b2, accumulate),
-                                        &nc_du, &fin_du, s));
+      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(d, L, NT_EPI_RESID_BN, L.a1, L.W1t[j], L.du, L.du,
+                                        L.mask_h[j], 1.f, L.t2[j - 1], bp, B, &nc_du, s));
       Gin = L.du;
     } else {
       GemmArgs g;
@@ -905,7 +843,6 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRYP(DCNR_K_GEMM_DX, gemm_nn(d.prec, EPI_STORE_RESID, g, 1, s));
       Gin = L.G;
       nc_du = 0;
-      fin_du = 0;
     }
   }
   // ---- initial layer

@@ -303,7 +303,7 @@ __device__ inline void red_finalize(const RedFinal& rf, int n, int N, int Nr, do
   }
 }
 
-// bf16 weight-resident streaming GEMM (gemm_nt.hip): C[M,N] = X[M,K] W[N,K]^T
+// bf16 weight-stationary streaming GEMM (gemm_ws.hip): C[M,N] = X[M,K] W[N,K]^T
 enum NtEpi : int {
   NT_EPI_BIAS = 0,    // C bf16 = acc + bias[n] (bias padded to N, may be null)
   NT_EPI_F32 = 1,     // C f32  = acc
@@ -313,7 +313,7 @@ enum NtEpi : int {
   NT_EPI_BIAS_STATS = 3,   // C = acc + bias; part = [sum(c - bias), sum((c - bias)^2)]
   NT_EPI_RESID_BN = 4,     // C = (acc + R) * [H > 0]; part = [sum c, sum c*xhat(T)]
   NT_EPI_DROP_BN = 5,      // C = acc * [H != 0] * hscale; part = [sum c, sum c*xhat(T)]
-  // eval-mode BatchNorm folded into the epilogue (gemm_ws only; bn_scale /
+  // eval-mode BatchNorm folded into the epilogue (bn_scale /
   // bn_shift = the running-stat affine of bn_finalize2):
   NT_EPI_BN_RELU = 6,        // C = relu((acc + bias) * sc + sh)
   NT_EPI_BN_RESID_RELU = 7,  // C = relu((acc + bias) * sc + sh + R)
@@ -325,26 +325,18 @@ struct NtArgs {
   void* C; int64_t ldc;
   const float* bias;
   const void* R; int64_t ldr;
-  const bf16* H; int64_t ldh; float hscale;         // mask source (RESID_BN, DROP_BN)
-  const uint32_t* Hb; int64_t ldhb;                 // or its 1-bit image (gemm_ws): bit c%32
-                                                    // of word [m][c/32] = keep column c
+  float hscale;                                     // DROP_BN: 1/(1-p)
+  const uint32_t* Hb; int64_t ldhb;                 // 1-bit keep mask (RESID_BN, DROP_BN): bit
+                                                    // c%32 of word [m][c/32] = keep column c
   const bf16* T; int64_t ldt;                       // BN input for xhat
   const float* mean; const float* invstd;
   const float* bn_scale; const float* bn_shift;     // BN_RELU, BN_RESID_RELU
   float* part;                                      // column partials (stats epilogues)
-  // gemm_ws only: fin != 0 -> the last workgroup of each column slice reduces
-  // the partials (fp64, fixed order) and runs red_finalize itself (fin_shift:
-  // forward partials are relative to the bias); counters at rf.counter[slice]
-  int fin; int fin_shift; int fin_nr; RedFinal rf;
-  int nslices, groups; int64_t mtiles;   // filled by gemm_nt
+  int nslices, groups; int64_t mtiles;   // filled by gemm_ws
 };
-bool gemm_nt_supported(int64_t K, int64_t N);
+bool gemm_ws_supported(int64_t K, int64_t N);
 // nparts (stats epilogues): rows of part written (the nchunks of reduce_fused)
-dcnr_status gemm_nt(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
-// the same contract, weight-stationary kernel (gemm_ws.hip)
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
-// whether gemm_ws runs as one launch (a requirement for fin)
-bool gemm_ws_single_launch(const NtArgs& a, int epi);
 inline bool nt_epi_stats(int epi) { return epi >= NT_EPI_BIAS_STATS && epi <= NT_EPI_DROP_BN; }
 
 // bf16 weight-gradient GEMM (gemm_dw.hip): slab[split][n][k] = sum over the

@@ -5,7 +5,8 @@
 // The deep tower's Linear layers (train.py:143,105,109) have a huge M (the
 // batch) and a small N x K weight: one pass over the activations.  Compared
 // with gemm_nt.hip (W slice in LDS, X fragments streamed per wave) this
-// kernel halves the X bytes each CU has to pull per FLOP:
+// kernel halves the X bytes each CU has to pull per FLOP (measured in round 1;
+// the W-in-LDS kernel has been retired):
 //  * a workgroup owns a 256-column slice of W and keeps it in REGISTERS for
 //    its whole lifetime: each of the 8 waves holds 32 columns x K as MFMA
 //    A-operand fragments (K = 512: 128 VGPRs per lane);
@@ -27,59 +28,26 @@
 #ifndef WS_LAB_MODE
 #define WS_LAB_MODE 0   // tools/ws_lab.hip: 1 no C stores, 2 no X DMAs, 4 no MFMAs, 8 no epilogue
 #endif
+#ifndef WS_PREFETCH_PIN
+#define WS_PREFETCH_PIN 1
+#endif
 
 namespace dcnr {
 namespace {
 
 // Per-epilogue tile rows and operand-load placement (measured with
 // tools/ws_lab.hip, M = 131072, K = N = 512): 64-row tiles where registers
-// allow; RESID_BN (three operands) needs 32-row tiles to have its operands in
-// flight during the MFMAs ("early"); RESID and DROP_BN load theirs one row
-// block ahead of use ("late").
-#ifndef WS_PREFETCH_PIN
-#define WS_PREFETCH_PIN 1
-#endif
-#ifndef WS_TM_PLAIN
-#define WS_TM_PLAIN 64
-#endif
+// allow; the epilogues with operands use 32-row tiles and issue every
+// operand load before the MFMAs ("early": RESID 90.5 vs 96.4 us one row block
+// ahead, DROP_BN 104.7 vs 111.9 us at 64 rows); eval BN_RELU at 32 rows
+// (71.5 vs 75.4-77.2 us at 64).
 constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
-
-#ifndef WS_TM_RESID
-#define WS_TM_RESID 32
-#endif
-#ifndef WS_TM_BNRELU
-#define WS_TM_BNRELU 32   // lab, K = N = 512: 71.5 us vs 75.4-77.2 us at 64 rows
-#endif
-#ifndef WS_TM_RBN
-#define WS_TM_RBN 32
-#endif
-#ifndef WS_TM_DROP
-#define WS_TM_DROP 32   // lab, K = N = 512, 1-bit masks: 104.7 us (32 rows, early) vs 111.9 us (64 rows, late)
-#endif
-#ifndef WS_DROP_EARLY
-#define WS_DROP_EARLY 1
-#endif
-#ifndef WS_RESID_EARLY
-#define WS_RESID_EARLY 1   // lab, K = N = 512: 90.5 us early vs 96.4 us one row block ahead
-#endif
-template <int EPI> constexpr int ws_tm() {
-  return (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU) ? WS_TM_RESID : EPI == NT_EPI_RESID_BN ? WS_TM_RBN
-         : EPI == NT_EPI_DROP_BN ? WS_TM_DROP : EPI == NT_EPI_BN_RELU ? WS_TM_BNRELU : WS_TM_PLAIN;
-}
+template <int EPI> constexpr int ws_tm() { return EPI <= NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS ? 64 : 32; }
 template <int EPI> constexpr bool ws_ops_early() {
-  return EPI == NT_EPI_RESID_BN || (WS_DROP_EARLY && EPI == NT_EPI_DROP_BN) ||
-         (WS_RESID_EARLY && (EPI == NT_EPI_RESID || EPI == NT_EPI_BN_RESID_RELU));
+  return EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN || EPI == NT_EPI_BN_RESID_RELU;
 }
-// X-tile buffers in the LDS ring: the next NB-1 tiles are in flight while one
-// is consumed.  Only the epilogues without operand loads can use NB > 2 (an
-// operand load's wait would also wait for every older tile DMA).
-#ifndef WS_NB_PLAIN
-#define WS_NB_PLAIN 2
-#endif
-template <int EPI> constexpr int ws_nb() {
-  return (EPI == NT_EPI_BIAS || EPI == NT_EPI_BIAS_STATS || EPI == NT_EPI_F32 || EPI == NT_EPI_BN_RELU)
-             ? WS_NB_PLAIN : 2;
-}
+// X-tile buffers in the LDS ring: one tile in flight while one is consumed.
+template <int EPI> constexpr int ws_nb() { return 2; }
 
 template <int KTP, int TM, int NB = 2> struct WsCfg {
   static constexpr int P = KTP * 64;                      // LDS bytes per X row
@@ -134,7 +102,7 @@ __device__ __forceinline__ void issue_tile(u32x4 xr, int64_t ldx, int K, uint32_
   }
 }
 
-template <int KTP, int EPI, int HB = 0>
+template <int KTP, int EPI>
 __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   constexpr int WS_TM = ws_tm<EPI>();
   constexpr int NB = ws_nb<EPI>();
@@ -210,10 +178,9 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
       __builtin_amdgcn_make_buffer_rsrc(a.C, (short)0, (int)(a.M * a.ldc * es), 0x00020000);
   const __amdgpu_buffer_rsrc_t rr_ = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.R, (short)0, HAS_R ? (int)(a.M * a.ldr * 2) : 0, 0x00020000);
-  constexpr bool hbits = HAS_HT && HB;   // 1-bit keep mask (a.Hb) instead of bf16 H
+  // 1-bit keep mask (a.Hb): bit c%32 of word [m][c/32]
   const __amdgpu_buffer_rsrc_t hr = __builtin_amdgcn_make_buffer_rsrc(
-      hbits ? (void*)a.Hb : (void*)a.H, (short)0,
-      HAS_HT ? (int)(hbits ? a.M * a.ldhb * 4 : a.M * a.ldh * 2) : 0, 0x00020000);
+      (void*)a.Hb, (short)0, HAS_HT ? (int)(a.M * a.ldhb * 4) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.T, (short)0, HAS_HT ? (int)(a.M * a.ldt * 2) : 0, 0x00020000);
 
@@ -242,19 +209,16 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     // row block ahead of their use)
     constexpr bool WS_OPS_EARLY = ws_ops_early<EPI>();
     constexpr int NSLOT = WS_OPS_EARLY ? WS_RB : 2;
-    u32x4 rv[NSLOT], hv[NSLOT], tv[NSLOT];
-    uint32_t hw[NSLOT];   // the mask word of columns nw .. nw+31 (hbits)
+    u32x4 rv[NSLOT], tv[NSLOT];
+    uint32_t hw[NSLOT];   // the mask word of columns nw .. nw+31
     auto load_ops = [&](int rb, int slot) {
       const int64_t m = m0 + rb * 16 + l15;
       const bool ok = m < a.M && nst < a.N;
       if constexpr (HAS_R)
         rv[slot] = __builtin_amdgcn_raw_buffer_load_b128(rr_, ok ? (int)((m * a.ldr + nst) * 2) : OOR, 0, 0);
       if constexpr (HAS_HT) {
-        if constexpr (hbits)
-          hw[slot] = __builtin_amdgcn_raw_buffer_load_b32(
-              hr, (m < a.M && nw < a.N) ? (int)((m * a.ldhb + (nw >> 5)) * 4) : OOR, 0, 0);
-        else
-          hv[slot] = __builtin_amdgcn_raw_buffer_load_b128(hr, ok ? (int)((m * a.ldh + nst) * 2) : OOR, 0, 0);
+        hw[slot] = __builtin_amdgcn_raw_buffer_load_b32(
+            hr, (m < a.M && nw < a.N) ? (int)((m * a.ldhb + (nw >> 5)) * 4) : OOR, 0, 0);
         tv[slot] = __builtin_amdgcn_raw_buffer_load_b128(tr, ok ? (int)((m * a.ldt + nst) * 2) : OOR, 0, 0);
       }
     };
@@ -321,13 +285,10 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
       const bool mok = m < a.M;
       if (!WS_OPS_EARLY && rb + 1 < WS_RB) load_ops(rb + 1, (rb + 1) & 1);
       const int slot = WS_OPS_EARLY ? rb : rb & 1;
-      u32x2 o[2], rf[2], hf[2], tf[2];
+      u32x2 o[2], rf[2], tf[2];
       u32x4 of[2];
       if constexpr (HAS_R) to_acc_layout(rv[slot], rf);
-      if constexpr (HAS_HT) {
-        if constexpr (!hbits) to_acc_layout(hv[slot], hf);
-        to_acc_layout(tv[slot], tf);
-      }
+      if constexpr (HAS_HT) to_acc_layout(tv[slot], tf);
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int cl = wave * WS_WC + cb * 16 + q * 4;   // column within the slice
@@ -366,15 +327,9 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
           // DROP_BN: keep where h != 0 (the saved dropout activation)
 #pragma unroll
           for (int d = 0; d < 2; ++d) {
-            if constexpr (hbits) {   // bits 16cb + 4q + 2d (+1) of the wave's 32 columns
-              const uint32_t kb = hw[slot] >> (16 * cb + 4 * q + 2 * d);
-              o[cb][d] &= ((kb & 1u) * 0xffffu) | (((kb >> 1) & 1u) * 0xffff0000u);
-            } else {
-              const uint32_t hb = hf[cb][d];
-              uint32_t keep = ((hb & 0x7fff7fffu) + 0x7fff7fffu) & 0x80008000u;
-              if constexpr (EPI == NT_EPI_RESID_BN) keep &= ~hb;
-              o[cb][d] &= (keep >> 15) * 0xffffu;
-            }
+            // bits 16cb + 4q + 2d (+1) of the wave's 32 columns
+            const uint32_t kb = hw[slot] >> (16 * cb + 4 * q + 2 * d);
+            o[cb][d] &= ((kb & 1u) * 0xffffu) | (((kb >> 1) & 1u) * 0xffff0000u);
           }
         }
         if constexpr (STATS) {
@@ -453,58 +408,25 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     const int k = (lane >> 2) & 1, cb = (lane >> 3) & 1, r = 2 * (lane & 1) + ((lane >> 1) & 1);
     const int n = nw + cb * 16 + q * 4 + r;
     if (n < a.N) a.part[((int64_t)group * 2 + k) * a.N + n] = x[0];
-    if (a.fin) {
-      // the last workgroup of this column slice to finish sums the slice's
-      // partial rows in fixed group order (fp64) and finalises the columns
-      int* flag = reinterpret_cast<int*>(lds + NB * C::TILE + 3 * WS_TN * 4);
-      if (last_arriver(a.rf.counter + slice, groups, flag) && tid < WS_TN) {
-        const int nc = n0 + tid;
-        if (nc < a.N) {
-          const float* pp = a.part + nc;
-          double v0 = 0.0, v1 = 0.0;
-          int g2 = 0;
-          for (; g2 + 8 <= groups; g2 += 8) {
-            float u0[8], u1[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              u0[i] = pp[(int64_t)(g2 + i) * 2 * a.N];
-              u1[i] = pp[((int64_t)(g2 + i) * 2 + 1) * a.N];
-            }
-#pragma unroll
-            for (int i = 0; i < 8; ++i) { v0 += (double)u0[i]; v1 += (double)u1[i]; }
-          }
-          for (; g2 < groups; ++g2) {
-            v0 += (double)pp[(int64_t)g2 * 2 * a.N];
-            v1 += (double)pp[((int64_t)g2 * 2 + 1) * a.N];
-          }
-          red_finalize(a.rf, nc, a.N, a.fin_nr, v0, v1, 0.0, a.fin_shift != 0,
-                       a.fin_shift ? (double)a.bias[nc] : 0.0);
-        }
-      }
-    }
   }
 }
 
-template <int KTP, int EPI, int HB = 0>
+template <int KTP, int EPI>
 dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   constexpr int WS_TM = ws_tm<EPI>();
   using C = WsCfg<KTP, WS_TM, ws_nb<EPI>()>;
   static bool attr_set = false;
   if (!attr_set) {
-    DCNR_HIP(hipFuncSetAttribute((const void*)gemm_ws_kernel<KTP, EPI, HB>,
+    DCNR_HIP(hipFuncSetAttribute((const void*)gemm_ws_kernel<KTP, EPI>,
                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES));
     attr_set = true;
   }
   a.nslices = (int)cdiv(a.N, WS_TN);
   // 32-bit buffer offsets: launch in M-chunks of < 2^29 bytes per operand
-  const int64_t maxld = std::max<int64_t>({a.ldx, a.ldc * 2, a.R ? a.ldr : 0, a.H ? a.ldh : 0,
+  const int64_t maxld = std::max<int64_t>({a.ldx, a.ldc * 2, a.R ? a.ldr : 0, a.Hb ? a.ldhb * 2 : 0,
                                            a.T ? a.ldt : 0});
   const int64_t mchunk = std::max<int64_t>(WS_TM, ((int64_t(1) << 29) / (maxld * 2)) / WS_TM * WS_TM);
   if (a.M > mchunk) {
-    if (a.fin) {
-      set_error("gemm_ws: in-kernel finalize needs a single launch");
-      return DCNR_UNSUPPORTED_SHAPE;
-    }
     int total = 0;
     for (int64_t m0 = 0; m0 < a.M; m0 += mchunk) {
       NtArgs b = a;
@@ -512,12 +434,11 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
       b.X = a.X + m0 * a.ldx;
       b.C = (char*)a.C + m0 * a.ldc * (EPI == NT_EPI_F32 ? 4 : 2);
       if (a.R) b.R = (const char*)a.R + m0 * a.ldr * 2;
-      if (a.H) b.H = a.H + m0 * a.ldh;
       if (a.Hb) b.Hb = a.Hb + m0 * a.ldhb;
       if (a.T) b.T = a.T + m0 * a.ldt;
       if (a.part) b.part = a.part + (int64_t)total * 2 * a.N;
       int np = 0;
-      dcnr_status st = launch_ws<KTP, EPI, HB>(b, s, &np);
+      dcnr_status st = launch_ws<KTP, EPI>(b, s, &np);
       if (st != DCNR_OK) return st;
       total += np;
     }
@@ -531,36 +452,30 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   if (need < grid) grid = (int)(cdiv(need, unit) * unit);
   a.groups = grid / a.nslices;
   if (nparts) *nparts = a.groups;
-  hipLaunchKernelGGL((gemm_ws_kernel<KTP, EPI, HB>), dim3(grid), dim3(WS_NT), C::LDS_BYTES, s, a);
+  hipLaunchKernelGGL((gemm_ws_kernel<KTP, EPI>), dim3(grid), dim3(WS_NT), C::LDS_BYTES, s, a);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
 
-template <int EPI, int HB = 0>
+template <int EPI>
 dcnr_status dispatch_ws(const NtArgs& a, hipStream_t s, int* nparts) {
-  if (a.K <= 128) return launch_ws<4, EPI, HB>(a, s, nparts);
-  if (a.K <= 256) return launch_ws<8, EPI, HB>(a, s, nparts);
-  return launch_ws<16, EPI, HB>(a, s, nparts);
+  if (a.K <= 128) return launch_ws<4, EPI>(a, s, nparts);
+  if (a.K <= 256) return launch_ws<8, EPI>(a, s, nparts);
+  return launch_ws<16, EPI>(a, s, nparts);
 }
 
 }  // namespace
 
-bool gemm_ws_single_launch(const NtArgs& a, int epi) {
-  (void)epi;   // (64-row rounding below is conservative for 32-row tiles too)
-  const int64_t maxld = std::max<int64_t>({a.ldx, a.ldc * 2, a.R ? a.ldr : 0, a.H ? a.ldh : 0,
-                                           a.T ? a.ldt : 0});
-  const int64_t mchunk = std::max<int64_t>(64, ((int64_t(1) << 29) / (maxld * 2)) / 64 * 64);
-  return a.M <= mchunk;
-}
+bool gemm_ws_supported(int64_t K, int64_t N) { return K <= 512 && K % 8 == 0 && N % 8 == 0; }
 
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
   if (nparts) *nparts = 0;
   if (a.M <= 0 || a.N <= 0) return DCNR_OK;
   const bool ht = epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN;
-  if (!gemm_nt_supported(a.K, a.N) || a.ldx % 8 || a.ldw % 8 || a.ldc % 8 ||
+  if (!gemm_ws_supported(a.K, a.N) || a.ldx % 8 || a.ldw % 8 || a.ldc % 8 ||
       ((epi == NT_EPI_RESID || epi == NT_EPI_RESID_BN || epi == NT_EPI_BN_RESID_RELU) && (a.ldr % 8 || !a.R)) ||
       (epi >= NT_EPI_BN_RELU && (!a.bn_scale || !a.bn_shift)) ||
-      (ht && (!a.H || !a.T || !a.mean || !a.invstd || a.ldh % 8 || a.ldt % 8)) ||
+      (ht && (!a.Hb || !a.T || !a.mean || !a.invstd || a.ldt % 8)) ||
       (nt_epi_stats(epi) && !a.part)) {
     set_error("gemm_ws: unsupported K=%d N=%d / missing epilogue operand", a.K, a.N);
     return DCNR_UNSUPPORTED_SHAPE;
@@ -571,13 +486,11 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
     case NT_EPI_RESID: return dispatch_ws<NT_EPI_RESID>(a, s, nparts);
     case NT_EPI_BIAS_STATS: return dispatch_ws<NT_EPI_BIAS_STATS>(a, s, nparts);
     case NT_EPI_RESID_BN:
-      return a.Hb ? dispatch_ws<NT_EPI_RESID_BN, 1>(a, s, nparts)
-                  : dispatch_ws<NT_EPI_RESID_BN, 0>(a, s, nparts);
+      return dispatch_ws<NT_EPI_RESID_BN>(a, s, nparts);
     case NT_EPI_BN_RELU: return dispatch_ws<NT_EPI_BN_RELU>(a, s, nparts);
     case NT_EPI_BN_RESID_RELU: return dispatch_ws<NT_EPI_BN_RESID_RELU>(a, s, nparts);
     case NT_EPI_DROP_BN:
-      return a.Hb ? dispatch_ws<NT_EPI_DROP_BN, 1>(a, s, nparts)
-                  : dispatch_ws<NT_EPI_DROP_BN, 0>(a, s, nparts);
+      return dispatch_ws<NT_EPI_DROP_BN>(a, s, nparts);
   }
   set_error("gemm_ws: bad epilogue");
   return DCNR_BAD_ARG;
