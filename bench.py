@@ -54,6 +54,18 @@ CFG2_B = 65536
 CFG2_BYTES = 14 * 8 + 14 * 32 * 4 + 8 * 4 + D * 4
 PEAK_BF16 = 2.5e15     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12
+CLASS_KERNELS = {
+    "gather_cross": "gather_cross_v4_kernel (train forward)",
+    "gemm_fwd": "gemm_ws_kernel (deep-tower Linear forward)",
+    "gemm_dx": "gemm_ws_kernel (deep-tower dX with BN-backward epilogues)",
+    "gemm_dw": "gemm_dw_kernel (deep-tower weight gradient)",
+    "rowwise": "rowcol_kernel (BN apply / statistics passes)",
+    "reduce": "reduce / split-K combine kernels",
+    "cross_bwd": "cross_bwd_v4_kernel (cross backward + embedding-grad scatter)",
+    "head": "row_dot / logits / bce kernels",
+    "adam": "adam_kernel (fused AdamW)",
+    "pack": "pack / zero-fill kernels",
+}
 
 
 def make_batch(gen, B, dev):
@@ -66,10 +78,41 @@ def make_batch(gen, B, dev):
     return user, item, cat, num, y
 
 
-def cpu_baseline(B_cpu=32768, steps=4):
-    """The oracle (numpy fp32 restatement of train.py:155-226) timed on the
-    host: forward + BCE + backward + AdamW on a bounded sample of the same
-    workload.  Reported only; not the optimisation target."""
+def cpu_threads():
+    return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+
+def cpu_baseline(B_cpu=32768, steps=3):
+    """The reference's own training step (train.py:155-226: forward, BCE,
+    backward, AdamW) as torch-CPU ops in the reference's order
+    (oracle/torch_cpu.py, validated within 10 % of the imported reference by
+    tools/validate_cpu_baseline.py), timed on the host cores at a bounded
+    batch of the same model.  Reported only; not the optimisation target."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch_cpu as tc
+    th = cpu_threads()
+    torch.set_num_threads(th)
+    cat = list(CFG["cat_dims"].values())
+    p = CFG["params"]
+    step = tc.TorchCPUStep(CFG["n_users"], CFG["n_items"], cat, CFG["n_num"], p["emb_dim"],
+                           p["hidden_dim"], p["n_cross_layers"], p["n_res_blocks"], p["dropout"],
+                           lr=1e-3, weight_decay=1e-4)
+    batches = [tc.make_cpu_batch(CFG["n_users"], CFG["n_items"], cat, CFG["n_num"], B_cpu, k)
+               for k in range(steps + 1)]
+    t = tc.time_steps(step.step, batches, warmup=1)
+    del step, batches
+    return {"value": B_cpu / t, "unit": "samples/s", "cores": th, "kind": "port",
+            "validated": "step time within 10 % of the imported reference train.py step on the "
+                         "same host (tools/validate_cpu_baseline.py, profiles/r02_cpu_baseline.txt)",
+            "sample": f"{steps} timed train steps (zero_grad, fwd, BCEWithLogits, bwd, AdamW) at "
+                      f"batch {B_cpu} of the bench model, fp32 torch-CPU ops in train.py:155-226 "
+                      f"order (oracle/torch_cpu.py), {steps * t:.1f} s",
+            "numpy_port": cpu_port_baseline()}
+
+
+def cpu_port_baseline(B_cpu=16384, steps=2):
+    """Secondary figure: the numpy fp32 oracle (restatement of train.py:155-226)
+    on the same model, forward + BCE + backward + AdamW."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import dcnr_oracle as orc
     import dcnr
@@ -98,10 +141,8 @@ def cpu_baseline(B_cpu=32768, steps=4):
             sd[k] = p.astype(np.float32)
             mom[k] = (mm, vv)
     el = time.perf_counter() - t0
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": steps * B_cpu / el, "unit": "samples/s", "cores": cores, "kind": "port",
-            "sample": f"{steps} train steps (fwd+BCE+bwd+AdamW) at batch {B_cpu} of the same "
-                      f"model/tables, numpy fp32 oracle, {el:.1f} s"}
+    return {"value": steps * B_cpu / el, "unit": "samples/s", "kind": "port",
+            "sample": f"{steps} steps at batch {B_cpu}, numpy fp32 oracle, {el:.1f} s"}
 
 
 def bench_cfg2(model, gen, dev, iters, world):
@@ -131,6 +172,7 @@ def bench_cfg2(model, gen, dev, iters, world):
     ms, cnt = _lib.profile_collect()["gather_cross"]
     t_launch = ms / cnt / 1e3
     achieved = CFG2_BYTES * CFG2_B / t_launch / 1e9
+    traffic = pmc_traffic("gather_cross_cfg2")
     return {"workload": "BASELINE configs[1]: embedding gather + x0 + 3-layer cross forward, fp32, "
                         "1M x 32 / 100k x 32 / 12 x 1000 x 32 tables, 8 dense",
             "batch": CFG2_B, "dtype": "f32",
@@ -139,7 +181,10 @@ def bench_cfg2(model, gen, dev, iters, world):
             "roofline": {"bound": "hbm", "kernel": "gather_cross_v4_kernel (dcnr_gather_cross)",
                          "achieved": achieved, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                          "frac": achieved / (PEAK_HBM / 1e9),
-                         "traffic": pmc_traffic("gather_cross_cfg2"),
+                         "traffic": traffic,
+                         # the 12 categorical tables (1.5 MB) stay in L2: the
+                         # HBM-side rate is the PMC bytes over the same time
+                         "traffic_rate_gbs": traffic / t_launch / 1e9 if traffic else None,
                          "bytes_per_sample": CFG2_BYTES, "avg_launch_ms": ms / cnt}}
 
 
@@ -221,6 +266,34 @@ def bench_cfg5(dev, iters, cpu):
     return out
 
 
+def bench_fp32(B, dev, pool, world, steps=5, warmup=2):
+    """The fp32 parity mode (f32 MFMA GEMMs, fp32 activations: the path pinned
+    element-wise to the reference's fixtures) at the same workload: train
+    steps per second on the same batches."""
+    import dcnr
+    torch.manual_seed(42)
+    m = dcnr.DCN_RecSys(CFG["n_users"], CFG["n_items"], CFG["cat_dims"], CFG["n_num"],
+                        dict(CFG["params"]), precision="fp32").to(dev)
+    tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, optimizer_name="AdamW")
+    for k in range(warmup):
+        tr.step(*pool[k % len(pool)])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        tr.step(*pool[(warmup + k) % len(pool)])
+    torch.cuda.synchronize()
+    el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    del tr, m
+    torch.cuda.empty_cache()
+    return {"samples_per_sec": world * B * steps / el, "ms_per_step": el / steps * 1e3,
+            "steps": steps, "dtype": "f32"}
+
+
 def pmc_traffic(kernel_class):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -239,7 +312,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=131072)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--pool", type=int, default=8)
+    ap.add_argument("--pool", type=int, default=0,
+                    help="distinct synthetic batches (default: warmup + steps, a fresh batch "
+                         "every step)")
+    ap.add_argument("--no-fp32", action="store_true", help="skip the fp32 parity-mode line")
     ap.add_argument("--eval-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-serving", action="store_true", help="skip the configs[4] top-k leg")
@@ -249,7 +325,24 @@ def main():
                          "all-reduce of the rest")
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # --gpus N without a launcher: start N ranks (one process per GPU)
+        # under torch.distributed.run before anything touches the GPU, and
+        # exit with the launcher's status
+        import socket
+        import subprocess
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+               f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+               f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.run(cmd).returncode)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -268,10 +361,13 @@ def main():
                                 exchange=args.exchange)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 * rank)
-    pool = [make_batch(gen, B, dev) for _ in range(max(1, args.pool))]
+    npool = args.pool if args.pool > 0 else args.warmup + args.steps
+    pool = [make_batch(gen, B, dev) for _ in range(npool)]
 
     for k in range(args.warmup):
         trainer.step(*pool[k % len(pool)])
+    trainer.check_indices()
+    off = args.warmup   # timed steps use batches no warmup step saw
 
     def timed(instrumented):
         torch.cuda.synchronize()
@@ -283,7 +379,7 @@ def main():
             _lib.profile_collect()
         t0 = time.perf_counter()
         for k in range(args.steps):
-            last = trainer.step(*pool[k % len(pool)])
+            last = trainer.step(*pool[(off + k) % len(pool)])
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -292,7 +388,7 @@ def main():
         prof = None
         if instrumented:
             _lib.profile_enable(False)
-            prof = _lib.profile_collect()
+            prof = _lib.profile_collect(with_bytes=True)
         el_t = torch.tensor([el], device=dev, dtype=torch.float64)
         if world > 1:
             dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
@@ -304,6 +400,7 @@ def main():
     # on its stream (per-kernel-class durations for the roofline); the events
     # serialise launches, so this pass is not the throughput number
     el_prof, prof, _ = timed(True)
+    trainer.check_indices()
     final_loss = float(loss.item())
 
     # scored pairs/s: eval-mode forward (running-stat BN, no dropout) per GPU
@@ -324,6 +421,7 @@ def main():
     if world > 1:
         dist.all_reduce(ev, op=dist.ReduceOp.MAX)
     pairs_per_s = world * B * args.eval_steps / float(ev.item())
+    fp32 = None if args.no_fp32 else bench_fp32(B, dev, pool, world)
     cfg2 = bench_cfg2(model, gen, dev, max(args.steps, 10), world)
     cfg5 = bench_cfg5(dev, 10, world == 1 and rank == 0 and not args.no_cpu_baseline) \
         if not args.no_serving else None
@@ -332,19 +430,34 @@ def main():
         samples = world * B * args.steps
         per_step_ms = {k: v[0] / args.steps for k, v in prof.items() if v[1]}
         launches = {k: v[1] / args.steps for k, v in prof.items() if v[1]}
-        # dominant kernel class: the 9 forward Linears per step (gemm_ws_kernel,
-        # 8 with the BN-statistics epilogue).  K = 512, N = 512 bf16 is below
-        # the MFMA/HBM ridge (256 < 312 FLOP/B): the binding roof is HBM.
-        gemm_cls = "gemm_fwd"
-        ms, cnt = prof[gemm_cls]
-        flop_launch = GEMM_FLOP[gemm_cls] * B * args.steps / cnt
-        bytes_launch = (GEMM_FWD_BYTES_PER_SAMPLE * B + GEMM_FWD_W_BYTES) * args.steps / cnt
-        t_launch = ms / cnt / 1e3
-        achieved = flop_launch / t_launch / 1e12
-        achieved_gbs = bytes_launch / t_launch / 1e9
-        g_ms, g_cnt = prof["gather_cross"]
+        # every kernel class priced against HBM with the library's per-launch
+        # algorithmic bytes (dcnr_profile_collect_bytes); the dominant class
+        # (largest time per step among the accounted ones) is `roofline`
+        table = {}
+        for k, (ms, cnt, nb) in prof.items():
+            if not cnt or nb <= 0:
+                continue
+            t_l = ms / cnt / 1e3
+            b_l = nb / cnt
+            table[k] = {"ms_per_step": ms / args.steps, "launches_per_step": cnt / args.steps,
+                        "avg_launch_ms": ms / cnt, "bytes_per_launch": b_l,
+                        "achieved_gbs": b_l / t_l / 1e9, "frac": b_l / t_l / PEAK_HBM,
+                        "kernel": CLASS_KERNELS.get(k, k)}
+        dom = max(table, key=lambda k: table[k]["ms_per_step"])
+        dt = table[dom]
+        roof = {"bound": "hbm", "class": dom, "kernel": dt["kernel"],
+                "achieved": dt["achieved_gbs"], "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+                "frac": dt["frac"], "traffic": pmc_traffic(dom),
+                "bytes_per_launch": dt["bytes_per_launch"], "avg_launch_ms": dt["avg_launch_ms"]}
+        if dom in GEMM_FLOP:
+            flop_launch = GEMM_FLOP[dom] * B * args.steps / prof[dom][1]
+            roof["mfma_view"] = {"achieved_tflops": flop_launch / (dt["avg_launch_ms"] / 1e3) / 1e12,
+                                 "peak_tflops": PEAK_BF16 / 1e12 if args.precision == "bf16"
+                                 else 157.3, "flop_per_launch": flop_launch}
+        deep_ms = sum(per_step_ms.get(k, 0.0) for k in GEMM_FLOP)
+        deep_flop = sum(GEMM_FLOP.values()) * B
+        g_ms, g_cnt, _ = prof["gather_cross"]
         gather_gbs = GATHER_BYTES * B * args.steps / g_cnt / (g_ms / g_cnt / 1e3) / 1e9
-        traffic = pmc_traffic(gemm_cls)
         out = {
             "metric": "fwd+bwd samples/sec (DCN-R train step) + scored (user,hotel) pairs/sec",
             "value": samples / el,
@@ -358,7 +471,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.precision,
-            "data": "synthetic (uniform ids, U[0,1) dense, Bernoulli labels; weights seed 42, "
+            "data": "synthetic (uniform ids, U[0,1) dense, Bernoulli labels; a distinct batch per "
+                    "step, generated on the device before the timed region; weights seed 42, "
                     "torch default init)",
             "config": {"workload": "DCN-R train step: fwd (train BN, dropout 0.6) + BCE + bwd + "
                                    "AdamW (+grad all-reduce), BASELINE configs[2]/[3]",
@@ -370,17 +484,13 @@ def main():
                            else "reduce-scatter + sharded AdamW + all-gather")},
             "scored_pairs_per_sec": pairs_per_s,
             "final_loss": final_loss,
-            "roofline": {"bound": "hbm",
-                         "kernel": "gemm_ws_kernel (deep-tower Linear fwd, class gemm_fwd)",
-                         "achieved": achieved_gbs, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                         "frac": achieved_gbs / (PEAK_HBM / 1e9),
-                         "traffic": traffic,
-                         "bytes_per_launch": bytes_launch,
-                         "avg_launch_ms": ms / cnt,
-                         "mfma_view": {"achieved_tflops": achieved,
-                                       "peak_tflops": PEAK_BF16 / 1e12 if args.precision == "bf16"
-                                       else 157.3,
-                                       "flop_per_launch": flop_launch}},
+            "roofline": roof,
+            "roofline_by_class": table,
+            "deep_tower_mfma": {"gemm_ms_per_step": deep_ms, "flop_per_step": deep_flop,
+                                "achieved_tflops": deep_flop / (deep_ms / 1e3) / 1e12 if deep_ms else None,
+                                "frac_of_bf16_peak": deep_flop / (deep_ms / 1e3) / PEAK_BF16 if deep_ms else None,
+                                "step_tflops": deep_flop / (el / args.steps) / 1e12},
+            "fp32_parity_mode": fp32,
             "roofline_gather": {"bound": "hbm", "kernel": "gather_cross", "achieved": gather_gbs,
                                 "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                                 "frac": gather_gbs / (PEAK_HBM / 1e9),

@@ -34,7 +34,10 @@ void set_error(const char* fmt, ...) {
 
 // ------------------------------------------------------------ profiling
 // Optional per-launch HIP-event timing by kernel class (dcnr_profile_*).
-struct ProfRec { int cat; hipEvent_t a, b; };
+// Each record carries the launch's ALGORITHMIC bytes (the operands the
+// function must move: inputs read once, outputs written once; 0 = not
+// accounted) so the bench prices every kernel class against HBM.
+struct ProfRec { int cat; double bytes; hipEvent_t a, b; };
 static std::mutex g_pm;
 static bool g_prof = false;
 static std::vector<ProfRec> g_recs;
@@ -48,8 +51,8 @@ static hipEvent_t prof_event() {
 }
 
 struct ProfScope {
-  int cat; hipStream_t s; hipEvent_t a = nullptr;
-  ProfScope(int c, hipStream_t st) : cat(c), s(st) {
+  int cat; hipStream_t s; double bytes; hipEvent_t a = nullptr;
+  ProfScope(int c, hipStream_t st, double nbytes = 0.0) : cat(c), s(st), bytes(nbytes) {
     if (!g_prof) return;
     std::lock_guard<std::mutex> lk(g_pm);
     a = prof_event();
@@ -60,7 +63,7 @@ struct ProfScope {
     std::lock_guard<std::mutex> lk(g_pm);
     hipEvent_t b = prof_event();
     (void)hipEventRecord(b, s);
-    g_recs.push_back(ProfRec{cat, a, b});
+    g_recs.push_back(ProfRec{cat, bytes, a, b});
   }
 };
 
@@ -77,6 +80,13 @@ namespace {
     ProfScope ps_(cat, s);           \
     dcnr_status st_ = (x);           \
     if (st_ != DCNR_OK) return st_;  \
+  } while (0)
+// ... and its algorithmic bytes
+#define TRYB(cat, nbytes, x)                 \
+  do {                                       \
+    ProfScope ps_(cat, s, (double)(nbytes)); \
+    dcnr_status st_ = (x);                   \
+    if (st_ != DCNR_OK) return st_;          \
   } while (0)
 
 constexpr int MAX_CAT = 64;
@@ -145,6 +155,18 @@ dcnr_status make_dims(const dcnr_model_desc* d, Dims* o) {
   return DCNR_OK;
 }
 
+// ------------------------------------------------- algorithmic byte counts
+// (profiling only): one [B][Hp] activation, its 1-bit mask, one gathered
+// input row (ids + embedding rows + dense features), a weight
+double act_b(const Dims& d, int64_t B) { return (double)B * d.Hp * d.es; }
+double mask_b(const Dims& d, int64_t B) { return (double)B * d.Hp / 8.0; }
+double gather_row_b(const Dims& d, int n_num) {
+  double w = 0;
+  for (int t = 0; t < 2 + d.K; ++t) w += d.widths[t];
+  return 8.0 * (2 + d.K) + 4.0 * w + 4.0 * n_num;
+}
+double w_b(const Dims& d, int K) { return (double)d.Hp * K * d.es; }
+
 // ------------------------------------------------------------- workspace
 struct Bump {
   char* base; size_t off = 0;
@@ -175,6 +197,9 @@ struct Layout {
   double* red2; int* red_cnt;   // reduce_fused scratch (counters zeroed by pack_all)
   // backward
   void* G; void* dt2; void* du; void* da;
+  // per-block backward buffers: all alias G/dt2/du/da/a1 unless
+  // DCNR_FLAG_KEEP_INTERMEDIATES gives each block its own
+  void* duk[MAX_RES]; void* dt2k[MAX_RES]; void* dak[MAX_RES]; void* dt1k[MAX_RES];
   float* dx0; float* slab; int64_t slab_elems; float* cpart; size_t cpart_elems;
   // 1-bit keep masks for the backward GEMM epilogues (bf16, Hp % 32 == 0):
   // mask_a1[j] = [a1_j != 0], mask_h[j] = [h_j > 0] (j >= 1)
@@ -187,8 +212,9 @@ struct Layout {
 // the backward GEMM epilogues read 1-bit keep masks (bf16 path, mask rows of
 // whole 32-bit words) instead of the bf16 activations
 bool masks_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && d.Hp % 32 == 0; }
+bool keep_of(const dcnr_model_desc* desc) { return (desc->flags & DCNR_FLAG_KEEP_INTERMEDIATES) != 0; }
 
-Layout make_layout(const Dims& d, int64_t B, int mode, void* ws) {
+Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = false) {
   Layout L;
   memset(&L, 0, sizeof(L));
   Bump b(ws);
@@ -251,6 +277,12 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws) {
     L.cpart = (float*)b.take(L.cpart_elems * 4);
     L.cred2_elems = cross_red2_elems(d.D, d.L);
     L.cred2 = (float*)b.take(L.cred2_elems * 4);
+    for (int j = 0; j < d.R; ++j) {
+      L.duk[j] = keep ? b.take(act) : L.du;
+      L.dt2k[j] = keep ? b.take(act) : L.dt2;
+      L.dak[j] = keep ? b.take(act) : L.da;
+      L.dt1k[j] = keep ? b.take(act) : L.a1;
+    }
 
   }
   L.bce_part = (double*)b.take(bce_ws_bytes());
@@ -476,8 +508,9 @@ dcnr_status wgrad_bf16(const void* dY, int64_t ldy, int N, const void* X, int64_
   a.C = slab; a.ldc = Kc; a.slab_stride = (int64_t)N * Kc;
   a.Btot = B; a.k_per_split = rup(cdiv(B, S), 64);
   a.N = N; a.K = Kc; a.splits = S;
-  TRYP(DCNR_K_GEMM_DW, gemm_dw(a, s));
-  TRYP(DCNR_K_REDUCE, splitk_reduce(slab, S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s));
+  TRYB(DCNR_K_GEMM_DW, 2.0 * B * (N + Kc) + 4.0 * Nr * Kr * (accumulate ? 2 : 1), gemm_dw(a, s));
+  TRYB(DCNR_K_REDUCE, 4.0 * S * N * Kc + 4.0 * Nr * Kr * (accumulate ? 2 : 1),
+       splitk_reduce(slab, S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s));
   return DCNR_OK;
 }
 
@@ -500,8 +533,9 @@ dcnr_status linear_dw(const Dims& d, const Layout& L, const void* dY, int ldy, i
   g.A = dY; g.lda = ldy; g.B = X; g.ldb = ldx;
   g.C = L.slab; g.ldc = Kc;
   g.M = N; g.N = Kc; g.K = B; g.k_per_split = kps; g.slab_stride = (int64_t)N * Kc;
-  TRYP(DCNR_K_GEMM_DW, gemm(d.prec, true, true, EPI_SPLITK, g, (int)S, s));
-  TRYP(DCNR_K_REDUCE, splitk_reduce(L.slab, (int)S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s));
+  TRYB(DCNR_K_GEMM_DW, (double)d.es * B * (N + Kc) + 4.0 * Nr * Kr, gemm(d.prec, true, true, EPI_SPLITK, g, (int)S, s));
+  TRYB(DCNR_K_REDUCE, 4.0 * S * N * Kc + 4.0 * Nr * Kr * (accumulate ? 2 : 1),
+       splitk_reduce(L.slab, (int)S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s));
   return DCNR_OK;
 }
 
@@ -550,7 +584,7 @@ dcnr_status bn_layer_fwd(const dcnr_model_desc* desc, const Dims& d, const Layou
   if (train) {
     int nc = nc_pre;
     const void* shift = nc_pre ? nullptr : t;
-    if (!nc_pre) TRYP(DCNR_K_ROWWISE, col_stats(d.prec, t, B, d.Hp, d.Hp, L.part, &nc, s));
+    if (!nc_pre) TRYB(DCNR_K_ROWWISE, act_b(d, B), col_stats(d.prec, t, B, d.Hp, d.Hp, L.part, &nc, s));
     if (!desc->bn_allreduce) {  // local BN: reduce + finalize in one launch
       RedFinal rf = red_init(L, RED_BN_FWD, (double)B, 0);
       rf.f = f;
@@ -620,7 +654,44 @@ dcnr_status dcnr_workspace_size(const dcnr_model_desc* desc, int64_t B, int mode
   Dims d;
   TRY(make_dims(desc, &d));
   if (!bytes || B < 0) { set_error("bad args"); return DCNR_BAD_ARG; }
-  *bytes = make_layout(d, B, mode, nullptr).total;
+  *bytes = make_layout(d, B, mode, nullptr, keep_of(desc)).total;
+  return DCNR_OK;
+}
+
+dcnr_status dcnr_workspace_offset(const dcnr_model_desc* desc, int64_t B, int mode, int kind,
+                                  int index, int64_t* offset) {
+  Dims d;
+  TRY(make_dims(desc, &d));
+  if (!offset || B < 0 || kind < 0 || kind >= DCNR_WS_KINDS) { set_error("bad args"); return DCNR_BAD_ARG; }
+  // a null base yields offsets as pointers from 0 (Bump takes nullptr -> nullptr),
+  // so lay out against a fake non-null base
+  char* base = (char*)(uintptr_t)4096;
+  Layout L = make_layout(d, B, mode, base, keep_of(desc));
+  const bool train = mode == DCNR_TRAIN;
+  const int R = d.R;
+  auto blk = [&](int n) { return index >= 0 && index < n; };
+  const void* p = nullptr;
+  switch (kind) {
+    case DCNR_WS_X0: p = L.x0; break;
+    case DCNR_WS_H: if (blk(R + 1)) p = L.h[index]; break;
+    case DCNR_WS_T1: if (blk(R)) p = L.t1[index]; break;
+    case DCNR_WS_T2: if (blk(R)) p = L.t2[index]; break;
+    case DCNR_WS_A1: if (blk(R) && train) p = L.a1s[index]; break;
+    case DCNR_WS_MASK_A1: if (blk(R)) p = L.mask_a1[index]; break;
+    case DCNR_WS_MASK_H: if (blk(R)) p = L.mask_h[index]; break;
+    case DCNR_WS_BN_MEAN: if (blk(2 * R)) p = L.bn[index].mean; break;
+    case DCNR_WS_BN_INVSTD: if (blk(2 * R)) p = L.bn[index].invstd; break;
+    case DCNR_WS_BN_SCALE: if (blk(2 * R)) p = L.bn[index].scale; break;
+    case DCNR_WS_BN_SHIFT: if (blk(2 * R)) p = L.bn[index].shift; break;
+    case DCNR_WS_DU: if (blk(R) && train) p = L.duk[index]; break;
+    case DCNR_WS_DT2: if (blk(R) && train) p = L.dt2k[index]; break;
+    case DCNR_WS_DA: if (blk(R) && train) p = L.dak[index]; break;
+    case DCNR_WS_DT1: if (blk(R) && train) p = L.dt1k[index]; break;
+    case DCNR_WS_G: if (train) p = L.G; break;
+    case DCNR_WS_DX0: if (train) p = L.dx0; break;
+    case DCNR_WS_ZC: p = L.zc; break;
+  }
+  *offset = p ? (int64_t)((const char*)p - base) : -1;
   return DCNR_OK;
 }
 
@@ -648,8 +719,8 @@ dcnr_status dcnr_gather_cross(const dcnr_model_desc* desc, void* const* params,
   CrossParams cp = make_cross(d, P);
   const GcOut o{cross_out, x0, nullptr, (int)ld_cross, (int)ld_x0};
   const int check = oob_flag != nullptr;
-  TRYP(DCNR_K_GATHER_CROSS, gather_cross_out(g, cp, user_ids, item_ids, cat_features, num_features,
-                                             B, o, 0, oob_flag, check, s));
+  TRYB(DCNR_K_GATHER_CROSS, (double)B * (gather_row_b(d, desc->n_num) + 4.0 * d.D * ((x0 ? 1 : 0) + (cross_out ? 1 : 0))),
+       gather_cross_out(g, cp, user_ids, item_ids, cat_features, num_features, B, o, 0, oob_flag, check, s));
   return DCNR_OK;
 }
 
@@ -671,7 +742,7 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     set_error("Expected more than 1 value per channel when training");
     return DCNR_BAD_ARG;
   }
-  Layout L = make_layout(d, B, mode, ws);
+  Layout L = make_layout(d, B, mode, ws, keep_of(desc));
   if (ws_bytes < L.total) {
     set_error("workspace too small: %zu < %zu", ws_bytes, L.total);
     return DCNR_WORKSPACE_TOO_SMALL;
@@ -685,10 +756,12 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   CrossParams cp = make_cross(d, P);
   {
     const GcOut o{nullptr, L.x0, L.zc, 0, d.Dp};
-    TRYP(DCNR_K_GATHER_CROSS, gather_cross_out(g, cp, user_ids, item_ids, cat_features, num_features,
-                                               B, o, d.prec == DCNR_PREC_BF16, L.err, check, s));
+    TRYB(DCNR_K_GATHER_CROSS, (double)B * (gather_row_b(d, desc->n_num) + (double)d.Dp * d.es + 4.0),
+         gather_cross_out(g, cp, user_ids, item_ids, cat_features, num_features, B, o,
+                          d.prec == DCNR_PREC_BF16, L.err, check, s));
   }
-  TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.x0, d.Dp, L.W0p, d.Dp, L.b0p, L.h[0], B, s));
+  TRYB(DCNR_K_GEMM_FWD, (double)B * d.Dp * d.es + act_b(d, B) + w_b(d, d.Dp),
+       linear_fwd(d, L.x0, d.Dp, L.W0p, d.Dp, L.b0p, L.h[0], B, s));
   if (!train && eval_fuse_ok(d)) {
     // every layer's running-stat affine in one launch
     BnEvalBatch eb;
@@ -703,12 +776,13 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     }
     TRYP(DCNR_K_REDUCE, bn_eval_finalize(eb, s));
     for (int j = 0; j < d.R; ++j) {
-      TRYP(DCNR_K_GEMM_FWD, linear_bn_relu(d, L.h[j], L.W1p[j], L.b1p[j], L.bn[2 * j], nullptr, L.a1, B, s));
-      TRYP(DCNR_K_GEMM_FWD, linear_bn_relu(d, L.a1, L.W2p[j], L.b2p[j], L.bn[2 * j + 1], L.h[j], L.h[j + 1],
-                                           B, s));
+      TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
+           linear_bn_relu(d, L.h[j], L.W1p[j], L.b1p[j], L.bn[2 * j], nullptr, L.a1, B, s));
+      TRYB(DCNR_K_GEMM_FWD, 3 * act_b(d, B) + w_b(d, d.Hp),
+           linear_bn_relu(d, L.a1, L.W2p[j], L.b2p[j], L.bn[2 * j + 1], L.h[j], L.h[j + 1], B, s));
     }
-    TRYP(DCNR_K_HEAD, row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
-    TRYP(DCNR_K_HEAD, head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
+    TRYB(DCNR_K_HEAD, act_b(d, B) + 4.0 * B, row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
+    TRYB(DCNR_K_HEAD, 12.0 * B, head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
     return DCNR_OK;
   }
   const float p = train ? d.dropout : 0.f;
@@ -717,35 +791,37 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     const bool fuse = train && epi_stats_ok(d);   // BN partials from the GEMM epilogue
     int nc = 0;
     if (fuse)
-      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j],
-                                             B, &nc, s));
+      TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
+           linear_fwd_stats(d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, &nc, s));
     else
-      TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
+      TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
+           linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
     TRY(bn_layer_fwd(desc, d, L, L.t1[j], B, train, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1,
                      L.bn[2 * j], s, nc, fuse ? L.b1p[j] : nullptr));
     void* a1 = train ? L.a1s[j] : L.a1;
-    TRYP(DCNR_K_ROWWISE, bn_relu_drop(d.prec, L.t1[j], a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
+    TRYB(DCNR_K_ROWWISE, 2 * act_b(d, B) + (train ? mask_b(d, B) : 0), bn_relu_drop(d.prec, L.t1[j], a1, B, d.Hp, d.Hp, L.bn[2 * j].scale, L.bn[2 * j].shift, p,
                      dropout_seed, j, s, train ? L.mask_a1[j] : nullptr));
     if (fuse)
-      TRYP(DCNR_K_GEMM_FWD, linear_fwd_stats(d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B,
-                                             &nc, s));
+      TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
+           linear_fwd_stats(d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, &nc, s));
     else
-      TRYP(DCNR_K_GEMM_FWD, linear_fwd(d, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
+      TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
+           linear_fwd(d, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
     TRY(bn_layer_fwd(desc, d, L, L.t2[j], B, train, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2,
                      L.bn[2 * j + 1], s, nc, fuse ? L.b2p[j] : nullptr));
     const bool head = j == d.R - 1 && bn_add_relu_head_supported(d.prec, d.Hp);
     if (head)   // last block: residual + ReLU + deep head dot + logits in one pass
-      TRYP(DCNR_K_ROWWISE, bn_add_relu_head(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
+      TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B) + 12.0 * B, bn_add_relu_head(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
                                             L.bn[2 * j + 1].scale, L.bn[2 * j + 1].shift, P.wf,
                                             d.H, L.zc, P.bf, logits, s));
     else
-      TRYP(DCNR_K_ROWWISE, bn_add_relu2(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
+      TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B) + (train && j + 1 < d.R ? mask_b(d, B) : 0), bn_add_relu2(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
                                         L.bn[2 * j + 1].scale, L.bn[2 * j + 1].shift, s,
                                         train && j + 1 < d.R ? L.mask_h[j + 1] : nullptr));
   }
   if (!bn_add_relu_head_supported(d.prec, d.Hp)) {
-    TRYP(DCNR_K_HEAD, row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
-    TRYP(DCNR_K_HEAD, head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
+    TRYB(DCNR_K_HEAD, act_b(d, B) + 4.0 * B, row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
+    TRYB(DCNR_K_HEAD, 12.0 * B, head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
   }
   return DCNR_OK;
 }
@@ -762,7 +838,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     set_error("dcnr_backward: bad argument");
     return DCNR_BAD_ARG;
   }
-  Layout L = make_layout(d, B, DCNR_TRAIN, ws);
+  Layout L = make_layout(d, B, DCNR_TRAIN, ws, keep_of(desc));
   if (ws_bytes < L.total) {
     set_error("workspace too small: %zu < %zu", ws_bytes, L.total);
     return DCNR_WORKSPACE_TOO_SMALL;
@@ -777,7 +853,9 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     void* zp[2 + MAX_CAT];
     int64_t zn[2 + MAX_CAT];
     for (int t = 0; t < 2 + d.K; ++t) { zp[t] = Gr.tab[t]; zn[t] = d.rows[t] * d.widths[t] * 4; }
-    TRYP(DCNR_K_PACK, fill_zero_multi(2 + d.K, zp, zn, s));
+    double zb = 0;
+    for (int t = 0; t < 2 + d.K; ++t) zb += (double)zn[t];
+    TRYB(DCNR_K_PACK, zb, fill_zero_multi(2 + d.K, zp, zn, s));
   }
 
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
@@ -789,65 +867,71 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     const BnBufs& bn1 = L.bn[2 * j];
     const BnBufs& bn2 = L.bn[2 * j + 1];
     int nc = 0;
+    // this block's backward buffers (one shared set unless KEEP_INTERMEDIATES)
+    void* du = L.duk[j];
+    void* dt2 = L.dt2k[j];
+    void* da = L.dak[j];
+    void* dt1 = L.dt1k[j];
     // ---- out = relu(BN2(t2) + h_j):  du, BN2 backward
     if (nc_du) {
       TRY(bn_bwd_reduce(desc, d, L, nc_du, 2, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, nullptr,
                         Gk.b2, accumulate, s));
     } else {
-      TRYP(DCNR_K_ROWWISE, bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean,
-                                          bn2.invstd, B, Hp, Hp, L.du, L.part, &nc, s));
+      TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B) + (Gin ? act_b(d, B) : 4.0 * B), bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean,
+                                          bn2.invstd, B, Hp, Hp, du, L.part, &nc, s));
       // dbeta2, dgamma2 and (last block only) dW_f[:H]
       TRY(bn_bwd_reduce(desc, d, L, nc, 3, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2,
                         Gin ? nullptr : Gr.wf, Gk.b2, accumulate, s));
     }
-    TRYP(DCNR_K_ROWWISE, bwd_bn2_apply2(d.prec, L.du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
-                       L.dt2, L.part, &nc, s));
+    TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn2_apply2(d.prec, du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
+                       dt2, L.part, &nc, s));
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
-    TRY(linear_dw(d, L, L.dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s));
+    TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s));
     if (fuse) {
       // dy1 = (dt2 W2) * [a1 != 0] / (1-p): relu and dropout masks from the
       // saved activation, BN1 partials (and, without SyncBN, its backward
       // coefficients and dgamma/dbeta) in the same pass
-      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(d, L, NT_EPI_DROP_BN, L.dt2, L.W2t[j], nullptr, L.da,
+      TRYB(DCNR_K_GEMM_DX, 3 * act_b(d, B) + mask_b(d, B) + w_b(d, d.Hp), linear_dx_bn(d, L, NT_EPI_DROP_BN, dt2, L.W2t[j], nullptr, da,
                                         L.mask_a1[j], p > 0.f ? 1.f / (1.f - p) : 1.f, L.t1[j],
                                         bn1, B, &nc, s));
     } else {
       GemmArgs g;
       memset(&g, 0, sizeof(g));
-      g.A = L.dt2; g.lda = Hp; g.B = L.W2t[j]; g.ldb = Hp; g.C = L.da; g.ldc = Hp;
+      g.A = dt2; g.lda = Hp; g.B = L.W2t[j]; g.ldb = Hp; g.C = da; g.ldc = Hp;
       g.M = B; g.N = Hp; g.K = Hp; g.k_per_split = Hp;
-      TRYP(DCNR_K_GEMM_DX, gemm_nn(d.prec, EPI_STORE, g, 1, s));
+      TRYB(DCNR_K_GEMM_DX, 2 * act_b(d, B) + w_b(d, d.Hp), gemm_nn(d.prec, EPI_STORE, g, 1, s));
       // ---- relu/dropout + BN1 backward
-      TRYP(DCNR_K_ROWWISE, bwd_bn1_stats(d.prec, L.da, L.t1[j], bn1.scale, bn1.shift, bn1.mean,
+      TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_stats(d.prec, da, L.t1[j], bn1.scale, bn1.shift, bn1.mean,
                                          bn1.invstd, B, Hp, Hp, p, dropout_seed, j, L.part, &nc, s));
     }
     TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
                         accumulate, s));
-    TRYP(DCNR_K_ROWWISE, bwd_bn1_apply2(d.prec, L.da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, L.a1,
+    TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_apply2(d.prec, da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, dt1,
                        L.part, &nc, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
-    TRY(linear_dw(d, L, L.a1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s));
+    TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s));
     if (fuse && j > 0) {
       // G is only consumed by block j-1's BN2 backward: emit its du = G * [h_j > 0]
-      // (in place over this block's du, the residual operand) and the partials
+      // (in place over this block's du, the residual operand, unless
+      // KEEP_INTERMEDIATES) and the partials
       const BnBufs& bp = L.bn[2 * (j - 1) + 1];
-      TRYP(DCNR_K_GEMM_DX, linear_dx_bn(d, L, NT_EPI_RESID_BN, L.a1, L.W1t[j], L.du, L.du,
+      TRYB(DCNR_K_GEMM_DX, 4 * act_b(d, B) + mask_b(d, B) + w_b(d, d.Hp), linear_dx_bn(d, L, NT_EPI_RESID_BN, dt1, L.W1t[j], du, L.duk[j - 1],
                                         L.mask_h[j], 1.f, L.t2[j - 1], bp, B, &nc_du, s));
-      Gin = L.du;
+      Gin = L.duk[j - 1];
     } else {
       GemmArgs g;
       memset(&g, 0, sizeof(g));
-      g.A = L.a1; g.lda = Hp; g.B = L.W1t[j]; g.ldb = Hp; g.C = L.G; g.ldc = Hp;
-      g.resid = L.du; g.ldr = Hp;
+      g.A = dt1; g.lda = Hp; g.B = L.W1t[j]; g.ldb = Hp; g.C = L.G; g.ldc = Hp;
+      g.resid = du; g.ldr = Hp;
       g.M = B; g.N = Hp; g.K = Hp; g.k_per_split = Hp;
-      TRYP(DCNR_K_GEMM_DX, gemm_nn(d.prec, EPI_STORE_RESID, g, 1, s));
+      TRYB(DCNR_K_GEMM_DX, 3 * act_b(d, B) + w_b(d, d.Hp), gemm_nn(d.prec, EPI_STORE_RESID, g, 1, s));
       Gin = L.G;
       nc_du = 0;
     }
   }
   // ---- initial layer
   int nc = 0;
-  TRYP(DCNR_K_ROWWISE, col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
+  TRYB(DCNR_K_ROWWISE, act_b(d, B), col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
   TRY(bias_reduce(d, L, nc, Gr.b0, accumulate, s));
   TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s));
   {
@@ -855,7 +939,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     memset(&g, 0, sizeof(g));
     g.A = L.G; g.lda = Hp; g.B = L.W0t; g.ldb = Hp; g.C = L.dx0; g.ldc = d.Dp; g.out_f32 = 1;
     g.M = B; g.N = d.Dp; g.K = Hp; g.k_per_split = Hp;
-    TRYP(DCNR_K_GEMM_DX, gemm_nn(d.prec, EPI_STORE, g, 1, s));
+    TRYB(DCNR_K_GEMM_DX, act_b(d, B) + 4.0 * B * d.Dp + w_b(d, d.Dp), gemm_nn(d.prec, EPI_STORE, g, 1, s));
   }
   // ---- cross stack + head bias + embedding scatter
   GatherDesc g = make_gather(d, P, desc->n_num);
@@ -867,7 +951,11 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   cb.dbf = Gr.bf;
   for (int t = 0; t < 2 + d.K; ++t) cb.emb_grad[t] = Gr.tab[t];
   CrossBwdScratch cws{L.cpart, L.cpart_elems, L.cred2, L.cred2_elems, L.red_cnt, CNT_SLOTS};
-  TRYP(DCNR_K_CROSS_BWD, cross_bwd_scatter(g, cb, user_ids, item_ids, cat_features, num_features, dz, B, L.dx0, d.Dp,
+  // re-gather + dx0 + dz read, one fp32 add per embedding element
+  double ew = 0;
+  for (int t = 0; t < 2 + d.K; ++t) ew += d.widths[t];
+  TRYB(DCNR_K_CROSS_BWD, (double)B * (gather_row_b(d, desc->n_num) + 4.0 * d.Dp + 4.0 + 4.0 * ew),
+       cross_bwd_scatter(g, cb, user_ids, item_ids, cat_features, num_features, dz, B, L.dx0, d.Dp,
                         cws, accumulate, s));
   return DCNR_OK;
 }
@@ -968,7 +1056,9 @@ dcnr_status dcnr_adam_step(int32_t n_tensors, float* const* params, const float*
     return DCNR_BAD_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  TRYP(DCNR_K_ADAM, adam(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, lr, beta1, beta2,
+  double nparam = 0;
+  for (int i = 0; i < n_tensors; ++i) nparam += (double)numel[i];
+  TRYB(DCNR_K_ADAM, 28.0 * nparam, adam(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, lr, beta1, beta2,
                          eps, weight_decay, step, decoupled, s));
   return DCNR_OK;
 }
@@ -999,7 +1089,7 @@ dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t
     return DCNR_BAD_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  TRYP(DCNR_K_KNN, cosine_topk(table, inv_norms, N, d, queries, Q, k, idx, dist, ws, ws_bytes, s));
+  TRYB(DCNR_K_KNN, (double)N * (4.0 * d + 4.0), cosine_topk(table, inv_norms, N, d, queries, Q, k, idx, dist, ws, ws_bytes, s));
   return DCNR_OK;
 }
 
@@ -1044,12 +1134,20 @@ void dcnr_profile_enable(int on) {
 }
 
 dcnr_status dcnr_profile_collect(double* ms, int64_t* launches, int32_t n) {
+  return dcnr_profile_collect_bytes(ms, launches, nullptr, n);
+}
+
+dcnr_status dcnr_profile_collect_bytes(double* ms, int64_t* launches, double* bytes, int32_t n) {
   std::vector<ProfRec> recs;
   {
     std::lock_guard<std::mutex> lk(g_pm);
     recs.swap(g_recs);
   }
-  for (int i = 0; i < n; ++i) { if (ms) ms[i] = 0.0; if (launches) launches[i] = 0; }
+  for (int i = 0; i < n; ++i) {
+    if (ms) ms[i] = 0.0;
+    if (launches) launches[i] = 0;
+    if (bytes) bytes[i] = 0.0;
+  }
   dcnr_status st = DCNR_OK;
   for (auto& r : recs) {
     float t = 0.f;
@@ -1060,6 +1158,7 @@ dcnr_status dcnr_profile_collect(double* ms, int64_t* launches, int32_t n) {
     if (r.cat >= 0 && r.cat < n) {
       if (ms) ms[r.cat] += t;
       if (launches) launches[r.cat] += 1;
+      if (bytes) bytes[r.cat] += r.bytes;
     }
   }
   std::lock_guard<std::mutex> lk(g_pm);

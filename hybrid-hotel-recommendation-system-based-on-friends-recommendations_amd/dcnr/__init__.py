@@ -12,6 +12,8 @@ System-Based-on-Friends-Recommendations):
   serving.rerank_with_mmr            main.py:133-169
   serving.RankingPipeline            the /recommendations + /similar_items core
                                      (main.py:196-230, 294-332)
+  artifacts.save_artifacts /         final_dcn_model.pth + item_embeddings.npy
+  artifacts.load_artifacts           (train.py:391-394, main.py:256-270)
 
 All compute runs in libdcnr.so (C ABI: include/dcnr.h) on the HIP device.
 """
@@ -22,5 +24,6 @@ from .train import FusedTrainer  # noqa: F401
 from . import serving  # noqa: F401
 from .data import DeviceLoader  # noqa: F401
 from .serving import RankingPipeline, rerank_with_mmr  # noqa: F401
+from . import artifacts  # noqa: F401
 
 __version__ = "0.1.0"

@@ -21,6 +21,10 @@ DCNR_OK, DCNR_BAD_ARG, DCNR_INDEX_OOB, DCNR_HIP_ERROR, DCNR_UNSUPPORTED_SHAPE, \
 PREC_FP32, PREC_BF16 = 0, 1
 EVAL, TRAIN = 0, 1
 FLAG_CHECK_INDICES = 1
+FLAG_KEEP_INTERMEDIATES = 2
+# dcnr_ws_tensor (include/dcnr.h)
+WS_KINDS = ["x0", "h", "t1", "t2", "a1", "mask_a1", "mask_h", "bn_mean", "bn_invstd", "bn_scale",
+            "bn_shift", "du", "dt2", "da", "dt1", "G", "dx0", "zc"]
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.c_void_p)
@@ -54,6 +58,8 @@ _SIGS = {
     "dcnr_input_dim": (_I64, [ctypes.POINTER(ModelDesc)]),
     "dcnr_workspace_size": (ctypes.c_int, [ctypes.POINTER(ModelDesc), _I64, ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_size_t)]),
+    "dcnr_workspace_offset": (ctypes.c_int, [ctypes.POINTER(ModelDesc), _I64, ctypes.c_int,
+                                             ctypes.c_int, ctypes.c_int, ctypes.POINTER(_I64)]),
     "dcnr_forward": (ctypes.c_int, [ctypes.POINTER(ModelDesc), _P, _P, _P, _P, _P, _I64,
                                     ctypes.c_int, ctypes.c_uint64, _P, _P, ctypes.c_size_t, _P]),
     "dcnr_gather_cross": (ctypes.c_int, [ctypes.POINTER(ModelDesc), _P, _P, _P, _P, _P, _I64, _P,
@@ -86,6 +92,7 @@ _SIGS = {
                                               ctypes.c_size_t, _P]),
     "dcnr_profile_enable": (None, [ctypes.c_int]),
     "dcnr_profile_collect": (ctypes.c_int, [_P, _P, ctypes.c_int32]),
+    "dcnr_profile_collect_bytes": (ctypes.c_int, [_P, _P, _P, ctypes.c_int32]),
 }
 
 KERNEL_CLASSES = ["gather_cross", "gemm_fwd", "gemm_dx", "gemm_dw", "rowwise", "reduce",
@@ -96,13 +103,18 @@ def profile_enable(on: bool):
     load().dcnr_profile_enable(1 if on else 0)
 
 
-def profile_collect():
-    """{class: (total_ms, launches)} since the last collect (synchronises)."""
+def profile_collect(with_bytes: bool = False):
+    """{class: (total_ms, launches)} since the last collect (synchronises);
+    with_bytes: {class: (total_ms, launches, algorithmic_bytes)}."""
     n = len(KERNEL_CLASSES)
     ms = (ctypes.c_double * n)()
     cnt = (ctypes.c_int64 * n)()
-    check(load().dcnr_profile_collect(ctypes.cast(ms, ctypes.c_void_p),
-                                      ctypes.cast(cnt, ctypes.c_void_p), n), "profile")
+    nb = (ctypes.c_double * n)()
+    check(load().dcnr_profile_collect_bytes(ctypes.cast(ms, ctypes.c_void_p),
+                                            ctypes.cast(cnt, ctypes.c_void_p),
+                                            ctypes.cast(nb, ctypes.c_void_p), n), "profile")
+    if with_bytes:
+        return {k: (ms[i], cnt[i], nb[i]) for i, k in enumerate(KERNEL_CLASSES)}
     return {k: (ms[i], cnt[i]) for i, k in enumerate(KERNEL_CLASSES)}
 
 _lib = None

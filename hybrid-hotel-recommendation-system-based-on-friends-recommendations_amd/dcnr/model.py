@@ -62,12 +62,39 @@ class ResBlock(nn.Module):
 
 _PRECISIONS = {"fp32": _lib.PREC_FP32, "bf16": _lib.PREC_BF16}
 
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x: int) -> int:
+    x = (x + 0x9E3779B97F4A7C15) & _M64
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & _M64
+    return x ^ (x >> 31)
+
+
+def dropout_seed(dev: torch.device, advance: bool = True) -> int:
+    """The 64-bit dropout seed of the next train-mode forward on ``dev``.
+
+    The reference trains on cuda (train.py:32), where ``nn.Dropout`` draws
+    from the device's default generator (Philox seed + offset) and leaves the
+    CPU generator -- the one ``DataLoader``/``RandomSampler`` draw each
+    epoch's permutation from (train.py:195-196) -- untouched.  The seed is
+    therefore derived from the device generator's (initial_seed, offset) and
+    the offset is advanced, as a Philox launch would: ``torch.manual_seed``
+    reproduces the sequence and the CPU generator's stream is not consumed."""
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    g = torch.cuda.default_generators[idx]
+    off = int(g.get_offset())
+    if advance:
+        g.set_offset(off + 4)
+    return _splitmix64((int(g.initial_seed()) & _M64) ^ _splitmix64(off))
+
 
 class DCN_RecSys(nn.Module):
     """Deep & Cross Network with residual deep tower (train.py:125-170)."""
 
     def __init__(self, n_users, n_items, cat_dims, n_num_features, params, precision="fp32",
-                 check_indices=False):
+                 check_indices=True):
         super().__init__()
         emb_dim = params['emb_dim']
         hidden_dim = params['hidden_dim']
@@ -96,6 +123,7 @@ class DCN_RecSys(nn.Module):
                           n_num=n_num_features, emb_dim=emb_dim, hidden=hidden_dim,
                           n_cross=n_cross_layers, n_res=n_res_blocks, dropout=float(dropout),
                           input_dim=input_dim)
+        self.keep_intermediates = False   # tests: per-block backward buffers (stage checks)
         self.bn_allreduce = None   # set by dcnr.parallel for SyncBN
         self._sync_bn_hook = None
         self._active_ws = None
@@ -116,7 +144,8 @@ class DCN_RecSys(nn.Module):
         desc.n_res = d['n_res']
         desc.dropout = d['dropout']
         desc.precision = _PRECISIONS[self.precision]
-        desc.flags = _lib.FLAG_CHECK_INDICES if self.check_indices else 0
+        desc.flags = (_lib.FLAG_CHECK_INDICES if self.check_indices else 0) | \
+            (_lib.FLAG_KEEP_INTERMEDIATES if getattr(self, 'keep_intermediates', False) else 0)
         if self.bn_allreduce is not None:
             desc.bn_allreduce = self.bn_allreduce
         return desc
@@ -180,6 +209,17 @@ class DCN_RecSys(nn.Module):
                    "dcnr_workspace_size")
         return int(n.value)
 
+    def workspace_offset(self, B: int, mode: int, kind: str, index: int = 0) -> int:
+        """Byte offset of a stored tensor in the workspace (dcnr_workspace_offset;
+        -1 if not materialised)."""
+        lib = _lib.load()
+        off = ctypes.c_int64(0)
+        desc = self.desc()
+        _lib.check(lib.dcnr_workspace_offset(ctypes.byref(desc), int(B), int(mode),
+                                             _lib.WS_KINDS.index(kind), int(index),
+                                             ctypes.byref(off)), "dcnr_workspace_offset")
+        return int(off.value)
+
     def _check_device(self, *tensors):
         dev = self.final_linear.weight.device
         if dev.type != 'cuda':
@@ -190,8 +230,12 @@ class DCN_RecSys(nn.Module):
                 raise RuntimeError(f"input on {t.device} but model on {dev}")
         return dev
 
-    def forward(self, user_ids, item_ids, cat_features, num_features):
-        dev = self._check_device(user_ids, item_ids, cat_features, num_features)
+    def prepare_inputs(self, user_ids, item_ids, cat_features, num_features):
+        """The forward's inputs as the native call takes them: contiguous
+        int64 ids [B], int64 [B, n_cat], fp32 [B, n_num] on the model's
+        device (the reference's loop passes column views such as
+        ``X_collab_b[:, 0]``, train.py:220)."""
+        self._check_device(user_ids, item_ids, cat_features, num_features)
         user_ids = user_ids.reshape(-1).to(torch.int64).contiguous()
         item_ids = item_ids.reshape(-1).to(torch.int64).contiguous()
         B = user_ids.shape[0]
@@ -201,13 +245,20 @@ class DCN_RecSys(nn.Module):
             raise RuntimeError("input shapes do not match the model")
         cat_features = cat_features.to(torch.int64).reshape(B, K).contiguous()
         num_features = num_features.to(torch.float32).reshape(B, F).contiguous()
+        return user_ids, item_ids, cat_features, num_features
+
+    def forward(self, user_ids, item_ids, cat_features, num_features):
+        dev = self._check_device(user_ids, item_ids, cat_features, num_features)
+        user_ids, item_ids, cat_features, num_features = self.prepare_inputs(
+            user_ids, item_ids, cat_features, num_features)
+        B = user_ids.shape[0]
         train = self.training
         if train and B == 1:
             raise ValueError("Expected more than 1 value per channel when training, "
                              "got input size torch.Size([1, %d])" % self._dims['hidden'])
         params = self.param_tensors()
         needs_grad = torch.is_grad_enabled() and any(p.requires_grad for p in params)
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item()) if train else 0
+        seed = dropout_seed(dev) if train else 0
         if needs_grad:
             logits = _DCNRFunction.apply(self, train, seed, user_ids, item_ids, cat_features,
                                          num_features, *params)
@@ -286,7 +337,11 @@ def _hook_error(model):
 
 
 def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
-                ws: Optional[torch.Tensor] = None):
+                ws: Optional[torch.Tensor] = None, defer_index_check: bool = False):
+    """One native forward.  With ``model.check_indices`` an out-of-range id
+    raises IndexError here (host sync), or -- ``defer_index_check`` -- is left
+    in the workspace's error word (``ws[:4]``) for the caller to read later
+    (FusedTrainer polls it without stalling the stream)."""
     lib = _lib.load()
     B = user.shape[0]
     dev = user.device
@@ -305,7 +360,7 @@ def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
     model._active_ws = None
     _hook_error(model)
     _lib.check(st, "dcnr_forward")
-    if model.check_indices:
+    if model.check_indices and not defer_index_check:
         _lib.check(lib.dcnr_check_errors(ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)),
                    "embedding")
     return logits, ws

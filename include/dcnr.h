@@ -85,6 +85,11 @@ typedef enum { DCNR_PREC_FP32 = 0, DCNR_PREC_BF16 = 1 } dcnr_precision;
 typedef enum { DCNR_EVAL = 0, DCNR_TRAIN = 1 } dcnr_mode;
 
 #define DCNR_FLAG_CHECK_INDICES 1u
+/* Train workspace keeps every residual block's backward intermediates (du,
+ * dt2, da, dt1) in buffers of their own instead of reusing one set: the
+ * stage-by-stage parity tests read them (dcnr_workspace_offset).  Same
+ * kernels, same results; more workspace. */
+#define DCNR_FLAG_KEEP_INTERMEDIATES 2u
 
 /* Optional collective hook for SyncBN across data-parallel ranks: called
  * (stream-ordered, from the calling thread) with a device buffer of `count`
@@ -119,6 +124,23 @@ int64_t dcnr_input_dim(const dcnr_model_desc* desc);
 /* Workspace bytes for a batch of B in `mode`.  A train-mode workspace holds
  * the saved activations that dcnr_backward consumes. */
 dcnr_status dcnr_workspace_size(const dcnr_model_desc* desc, int64_t B, int mode, size_t* bytes);
+
+/* Where a stored tensor lives in the workspace of (desc, B, mode), for tests
+ * that check each stage against a recomputation from the kernels' own stored
+ * inputs.  Row-major with leading dimension Hp = hidden rounded up to 8
+ * (Dp for x0 / dx0); element type bf16 in bf16 mode, else fp32 (masks: 1 bit
+ * per element, Hp/8 bytes per row; BN vectors, zc, dx0: fp32).  `index` is
+ * the block j (h: 0..n_res; bn_*: 2j for bn1, 2j+1 for bn2).  *offset = -1
+ * when that tensor is not materialised in this configuration. */
+typedef enum {
+  DCNR_WS_X0 = 0, DCNR_WS_H = 1, DCNR_WS_T1 = 2, DCNR_WS_T2 = 3, DCNR_WS_A1 = 4,
+  DCNR_WS_MASK_A1 = 5, DCNR_WS_MASK_H = 6, DCNR_WS_BN_MEAN = 7, DCNR_WS_BN_INVSTD = 8,
+  DCNR_WS_BN_SCALE = 9, DCNR_WS_BN_SHIFT = 10, DCNR_WS_DU = 11, DCNR_WS_DT2 = 12,
+  DCNR_WS_DA = 13, DCNR_WS_DT1 = 14, DCNR_WS_G = 15, DCNR_WS_DX0 = 16, DCNR_WS_ZC = 17,
+  DCNR_WS_KINDS = 18
+} dcnr_ws_tensor;
+dcnr_status dcnr_workspace_offset(const dcnr_model_desc* desc, int64_t B, int mode, int kind,
+                                  int index, int64_t* offset);
 
 /* DCN_RecSys.forward: logits[B] (fp32, device).  mode = DCNR_TRAIN uses
  * batch statistics (B >= 2), updates BN running stats and
@@ -274,6 +296,11 @@ void dcnr_profile_enable(int on);
 /* Synchronises the recorded events and returns, per class, the summed kernel
  * milliseconds and launch counts since the last collect (arrays of n). */
 dcnr_status dcnr_profile_collect(double* ms, int64_t* launches, int32_t n);
+/* ... plus, per class, the summed ALGORITHMIC bytes of those launches (the
+ * operands each function must move: inputs read once, outputs written once;
+ * split-K slabs count only in their reduction) -- the numerator of each
+ * class's HBM roofline fraction. */
+dcnr_status dcnr_profile_collect_bytes(double* ms, int64_t* launches, double* bytes, int32_t n);
 
 /* Synchronises `stream` and reports kernel-side errors recorded in ws
  * (DCNR_INDEX_OOB when DCNR_FLAG_CHECK_INDICES saw an out-of-range id). */

@@ -261,6 +261,154 @@ def backward(p, spec: ModelSpec, c: Cache, dz, user, item, cat, dt=np.float64):
 
 
 # --------------------------------------------------------------------------
+# bf16 storage emulation of the same step (the precision="bf16" path)
+# --------------------------------------------------------------------------
+def bf16_round(a) -> np.ndarray:
+    """Round to bfloat16 (round-to-nearest-even on the fp32 bits), returned
+    as float64 -- the value a bf16 store keeps."""
+    f = np.array(a, dtype=np.float32, copy=True, order='C')
+    u = f.view(np.uint32)
+    r = (u >> 16) & 1
+    r += 0x7FFF
+    u += r            # wraps only for NaN payloads (not produced here)
+    u &= 0xFFFF0000
+    return f.astype(np.float64)
+
+
+def _bf16_as(a, dt):
+    f = np.array(a, dtype=np.float32, copy=True, order='C')
+    u = f.view(np.uint32)
+    r = (u >> 16) & 1
+    r += 0x7FFF
+    u += r
+    u &= 0xFFFF0000
+    return f if dt == np.float32 else f.astype(dt)
+
+
+def train_step_bf16(p: Dict[str, np.ndarray], spec: ModelSpec, user, item, cat, num, y,
+                    dropout_masks: Optional[List[np.ndarray]] = None, dt=np.float64):
+    """The reference's train step (train.py:155-170 forward, 206/224 BCE, 225
+    backward) with every tensor the bf16 path STORES rounded to bf16 at the
+    point the kernels store it, the rest in ``dt`` (float64, or float32 for
+    full-size runs):
+
+      forward   x0 (GEMM operand), deep weights, h_j, t1_j, a1_j, t2_j, h_{j+1};
+                BN statistics of the stored t; cross stack not rounded
+      backward  du_j (= dh * [h_{j+1} > 0]), dt2_j, da_j, dt1_j, G = dh_0;
+                dW = dY^T X over the stored operands; dx0 = G W0 (fp32 out)
+
+    It isolates kernel errors from bf16's own rounding: the bf16 step's
+    gradients are compared to THIS to tight bounds (fp64 vs bf16 storage
+    alone differ by ~15 % on the first blocks' weight gradients at cfg3r:
+    BN's backward subtracts the batch means of the column gradients,
+    amplifying the storage rounding block by block).  Updates the BN running
+    statistics in ``p`` as forward() does.  Returns (logits, loss, grads)."""
+    R, H, B = spec.n_res, spec.hidden, user.shape[0]
+    rb = lambda a: _bf16_as(a, dt)                          # noqa: E731
+    W = lambda k: np.asarray(p[k], dtype=dt)               # noqa: E731
+    Wb = lambda k: rb(p[k])                                 # noqa: E731
+    pdrop = spec.dropout
+    inv_keep = dt(np.float32(1.0 / (1.0 - pdrop))) if pdrop > 0 else dt(1.0)
+    x0f = gather_x0(p, spec, user, item, cat, num, dt)   # fp32 values, exact
+    x0 = rb(x0f)
+    h = rb(x0 @ Wb('initial_deep_layer.weight').T + W('initial_deep_layer.bias'))
+
+    def bn_stats(t, prefix):
+        mu = t.mean(axis=0, dtype=np.float64)
+        var = np.maximum(np.square(t, dtype=np.float64).mean(axis=0) - mu * mu, 0.0)
+        rm, rv = p[prefix + '.running_mean'], p[prefix + '.running_var']
+        p[prefix + '.running_mean'] = ((1 - BN_MOMENTUM) * rm + BN_MOMENTUM * mu).astype(rm.dtype)
+        p[prefix + '.running_var'] = ((1 - BN_MOMENTUM) * rv + BN_MOMENTUM * var * B / (B - 1)).astype(rv.dtype)
+        p[prefix + '.num_batches_tracked'] = np.asarray(p[prefix + '.num_batches_tracked']) + 1
+        inv = (1.0 / np.sqrt(var + BN_EPS)).astype(np.float32)          # fp32 as the finalize
+        sc = np.asarray(p[prefix + '.weight'], np.float32) * inv
+        sh = np.asarray(p[prefix + '.bias'], np.float32) - mu.astype(np.float32) * sc
+        return mu.astype(np.float32).astype(dt), inv.astype(dt), sc.astype(dt), sh.astype(dt)
+
+    hs, t1s, t2s, a1s, st1, st2 = [h], [], [], [], [], []
+    for j in range(R):
+        pre = f'res_blocks.{j}'
+        t1 = rb(h @ Wb(pre + '.layer1.weight').T + W(pre + '.layer1.bias'))
+        s1 = bn_stats(t1, pre + '.bn1')
+        a1 = np.maximum(t1 * s1[2] + s1[3], 0)
+        if pdrop > 0:
+            a1 = a1 * dropout_masks[j].astype(dt) * inv_keep
+        a1 = rb(a1)
+        t2 = rb(a1 @ Wb(pre + '.layer2.weight').T + W(pre + '.layer2.bias'))
+        s2 = bn_stats(t2, pre + '.bn2')
+        h = rb(np.maximum(t2 * s2[2] + s2[3] + h, 0))
+        t1s.append(t1); t2s.append(t2); a1s.append(a1); st1.append(s1); st2.append(s2)
+        hs.append(h)
+    x = x0f
+    xs, ss = [], []
+    for l in range(spec.n_cross):
+        xs.append(x)
+        x, sl = cross_layer(x, W(f'cross_network.{l}.w.weight')[0], W(f'cross_network.{l}.b'))
+        ss.append(sl)
+    wf = W('final_linear.weight')[0]
+    z = hs[R] @ wf[:H] + x @ wf[H:] + W('final_linear.bias')[0]
+    loss, dz = bce_with_logits(z, y)
+    dz = dz.astype(dt)
+
+    g = {}
+    g['final_linear.weight'] = np.concatenate([hs[R].T @ dz, x.T @ dz])[None, :]
+    g['final_linear.bias'] = np.array([dz.sum(dtype=np.float64)])
+    dx = dz[:, None] * wf[H:][None, :]
+    for l in reversed(range(spec.n_cross)):
+        xl, sl = xs[l], ss[l]
+        wl = W(f'cross_network.{l}.w.weight')[0]
+        g[f'cross_network.{l}.b'] = dx.sum(axis=0)
+        gx = (dx * xl).sum(axis=1)
+        g[f'cross_network.{l}.w.weight'] = (gx[:, None] * xl).sum(axis=0)[None, :]
+        dx = dx * (1.0 + sl)[:, None] + gx[:, None] * wl[None, :]
+
+    def bn_back_b(dr, t, st, prefix):
+        mu, inv, _, _ = st
+        xh = (t - mu) * inv
+        s0, s1 = dr.sum(axis=0, dtype=np.float64), (dr * xh).sum(axis=0, dtype=np.float64)
+        g[prefix + '.weight'] = s1
+        g[prefix + '.bias'] = s0
+        a = np.asarray(p[prefix + '.weight'], np.float32) * inv.astype(np.float32)
+        k1 = (a.astype(np.float64) * s1 / B).astype(np.float32)
+        k2 = (a.astype(np.float64) * s0 / B).astype(np.float32)
+        return rb(a.astype(dt) * dr - k1.astype(dt) * xh - k2.astype(dt))
+
+    dhR = dz[:, None] * wf[:H][None, :]             # gradient wrt h_R (fp32)
+    du = rb(dhR * (hs[R] > 0).astype(dt))
+    for j in reversed(range(R)):
+        pre = f'res_blocks.{j}'
+        dt2 = bn_back_b(du, t2s[j], st2[j], pre + '.bn2')
+        g[pre + '.layer2.weight'] = dt2.T @ a1s[j]
+        g[pre + '.layer2.bias'] = np.zeros(H, dt)    # exactly 0 (BN removes it)
+        da = dt2 @ Wb(pre + '.layer2.weight') * inv_keep
+        da = rb(da) * (a1s[j] != 0).astype(dt)
+        dt1 = bn_back_b(da, t1s[j], st1[j], pre + '.bn1')
+        g[pre + '.layer1.weight'] = dt1.T @ hs[j]
+        g[pre + '.layer1.bias'] = np.zeros(H, dt)
+        G = rb(dt1 @ Wb(pre + '.layer1.weight') + du)
+        du = G * (hs[j] > 0).astype(dt) if j > 0 else G
+    G = du
+    g['initial_deep_layer.weight'] = G.T @ x0
+    g['initial_deep_layer.bias'] = G.sum(axis=0, dtype=np.float64)
+    dx0 = G @ Wb('initial_deep_layer.weight') + dx
+    e = spec.emb_dim
+    off = 0
+
+    def scatter(name, idx, width):
+        nonlocal off
+        gt = np.zeros(np.asarray(p[name]).shape, dtype=dt)
+        np.add.at(gt, idx, dx0[:, off:off + width])
+        off += width
+        g[name] = gt
+
+    scatter('user_embedding.weight', user, e)
+    scatter('item_embedding.weight', item, e)
+    for k, n in enumerate(spec.cat_dims):
+        scatter(f'cat_embeddings.{k}.weight', cat[:, k], cat_width(n))
+    return z, loss, g
+
+
+# --------------------------------------------------------------------------
 # optimizer (train.py:201-204, 226)
 # --------------------------------------------------------------------------
 def adam_step(param, grad, m, v, step, lr, beta1=0.9, beta2=0.999, eps=1e-8,

@@ -87,3 +87,25 @@ def dropout_mask_np(seed: int, layer: int, B: int, H: int, p: float) -> np.ndarr
     bits16 = np.where(odd, x >> U(16), x & U(0xFFFF))
     thresh = min(65536, int(np.floor(float(np.float32(p)) * 65536.0 + 0.5)))
     return (bits16.astype(np.int64) >= thresh).astype(np.float64)
+
+
+def dropout_mask_torch(seed: int, layer: int, B: int, H: int, p: float, device) -> "torch.Tensor":
+    """dropout_mask_np on the device (int64 arithmetic kept to 32 bits): the
+    same keep mask, for full-size batches."""
+    M = 0xFFFFFFFF
+
+    def fmix(x):
+        x = x ^ (x >> 16)
+        x = (x * 0x85EBCA6B) & M
+        x = x ^ (x >> 13)
+        x = (x * 0xC2B2AE35) & M
+        return x ^ (x >> 16)
+
+    rows = torch.arange(B, dtype=torch.int64, device=device)[:, None]
+    pairs = (torch.arange(H, dtype=torch.int64, device=device) >> 1)[None, :]
+    x = fmix(((rows * 0x9E3779B1) & M) ^ (seed & M) ^ ((layer * 0x7FEB352D) & M))
+    x = fmix((((x + pairs * 0x846CA68B) & M) ^ ((seed >> 32) & M)))
+    odd = (torch.arange(H, device=device) & 1).bool()[None, :]
+    bits16 = torch.where(odd, x >> 16, x & 0xFFFF)
+    thresh = min(65536, int(np.floor(float(np.float32(p)) * 65536.0 + 0.5)))
+    return (bits16 >= thresh)

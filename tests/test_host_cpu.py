@@ -122,3 +122,32 @@ def test_device_loader_permutation_is_dataloaders():
                                                   shuffle=True)])
         torch.manual_seed(seed)
         assert torch.equal(randomsampler_permutation(n), ref)
+
+
+def test_reference_artifacts_load_cpu():
+    """F9 (written by the reference's own DCN_RecSys + train.py:391-394's
+    torch.save/np.save): a weights-only load fills our model's state_dict
+    exactly (same keys, shapes, values), and item_embeddings.npy is the item
+    table; save_artifacts writes files the same loaders read back."""
+    import os
+    import tempfile
+    import golden_common as gc
+    import dcnr
+    d = os.path.join(os.path.dirname(__file__), "golden", "f9_artifacts")
+    sd = torch.load(os.path.join(d, "final_dcn_model.pth"), map_location="cpu", weights_only=True)
+    torch.manual_seed(0)
+    m = dcnr.DCN_RecSys(gc.CFG1["n_users"], gc.CFG1["n_items"], gc.CFG1["cat_dims"],
+                        gc.CFG1["n_num"], dict(gc.CFG1["params"]))
+    assert list(sd.keys()) == list(m.state_dict().keys())
+    m.load_state_dict(sd)
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "f1_cfg1_eval.npz"))
+    ck = gc.state_checksums(m)
+    np.testing.assert_allclose(np.stack([ck[k] for k in fx["ck_names"]]), fx["ck"], rtol=1e-12,
+                               atol=1e-9)
+    emb = np.load(os.path.join(d, "item_embeddings.npy"), allow_pickle=False)
+    assert np.array_equal(emb, m.item_embedding.weight.detach().numpy())
+    with tempfile.TemporaryDirectory() as t:
+        dcnr.artifacts.save_artifacts(m, t)
+        sd2 = torch.load(os.path.join(t, "final_dcn_model.pth"), weights_only=True)
+        assert all(torch.equal(sd2[k], v) for k, v in sd.items())
+        assert np.array_equal(np.load(os.path.join(t, "item_embeddings.npy")), emb)

@@ -301,9 +301,9 @@ def test_dropout_train_step_exact_masks(dev):
     sd = np_state(m)
     B = 256
     u, i, c, n, y = gc.make_inputs(cfg, B, 21)
+    from dcnr.model import dropout_seed
     torch.manual_seed(1234)
-    seed = int(torch.randint(0, 2 ** 62, (1,)).item())   # what forward will draw
-    torch.manual_seed(1234)
+    seed = dropout_seed(dev, advance=False)   # what forward will draw
     z, loss, grads = run_train(m, dev, u, i, c, n, y)
     masks = [dropout_mask_np(seed, j, B, spec.hidden, 0.6) for j in range(spec.n_res)]
     assert 0.3 < masks[0].mean() < 0.5
@@ -493,3 +493,24 @@ def test_linear_wgrad_bf16_vs_torch(dev, B, N, K, acc):
     ref = dY.float().t() @ X.float() + (base if acc else 0)
     err = ((dW - ref).norm() / ref.norm()).item()
     assert err <= 1e-5, err
+
+
+def test_reference_artifacts_score_on_gpu(dev):
+    """(f)3: the reference's saved artifacts (F9: final_dcn_model.pth +
+    item_embeddings.npy, written by train.py:391-394's code) loaded the way
+    main.py:256-270 loads them (weights-only), scored on the GPU on F1's
+    inputs: F1's logits (the reference's eval forward of that model)."""
+    import os
+    import dcnr
+    d = os.path.join(os.path.dirname(__file__), "golden", "f9_artifacts")
+    cfg = gc.CFG1
+    model_dims = (cfg["n_users"], cfg["n_items"], cfg["cat_dims"], cfg["n_num"])
+    m, emb, index = dcnr.artifacts.load_artifacts(d, model_dims, dict(cfg["params"]), device=dev)
+    fx = golden("f1_cfg1_eval.npz")
+    with torch.no_grad():
+        z = m(*to_dev(dev, fx["user"], fx["item"], fx["cat"], fx["num"])).cpu().numpy()
+    assert logits_err(z, fx["logits64"]) <= 1e-4
+    assert logits_err(z, fx["logits"]) <= 1e-4
+    # the index serves /similar_items on the same table (main.py:296-302)
+    dist_, idx = index.kneighbors(emb[:3], n_neighbors=5)
+    assert np.array_equal(np.asarray(idx)[:, 0], np.arange(3))

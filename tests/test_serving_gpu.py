@@ -132,6 +132,67 @@ def test_device_loader_matches_dataloader(dev):
                 assert torch.equal(a.cpu(), b)
 
 
+def test_device_loader_epochs_with_dropout_steps(dev):
+    """The reference trains on cuda (train.py:32): its dropout draws from the
+    device generator, so the CPU generator -- and with it every epoch's
+    DataLoader permutation -- is untouched by the training steps.  Two
+    DeviceLoader epochs with dropout-0.6 FusedTrainer steps in between must
+    give the batches of two DataLoader(shuffle=True) epochs with no steps."""
+    from torch.utils.data import DataLoader, TensorDataset
+    import dcnr
+    rng = np.random.default_rng(1)
+    n = 700
+    collab = torch.from_numpy(np.stack([rng.integers(0, 300, n), rng.integers(0, 120, n)], 1))
+    cat = torch.from_numpy(rng.integers(0, 40, (n, 2)))
+    num = torch.from_numpy(rng.random((n, 3), dtype=np.float32))
+    y = torch.from_numpy((rng.random(n) < 0.5).astype(np.float32))
+    torch.manual_seed(5)
+    ref = [list(DataLoader(TensorDataset(collab, cat, num, y), batch_size=100, shuffle=True))
+           for _ in range(2)]
+    torch.manual_seed(0)
+    m = dcnr.DCN_RecSys(300, 120, {"a": 40, "b": 40}, 3,
+                        dict(emb_dim=8, hidden_dim=64, n_cross_layers=2, n_res_blocks=2,
+                             dropout=0.6)).to(dev)
+    tr = dcnr.FusedTrainer(m, lr=1e-3)
+    torch.manual_seed(5)
+    loader = dcnr.DeviceLoader(collab, cat, num, y, batch_size=100, shuffle=True)
+    for ep in range(2):
+        got = []
+        for b in loader:
+            got.append(b)
+            cb, ct, nm, yy = b
+            tr.step(cb[:, 0], cb[:, 1], ct, nm, yy)
+        assert len(got) == len(ref[ep])
+        for g, r in zip(got, ref[ep]):
+            for a, b in zip(g, r):
+                assert torch.equal(a.cpu(), b)
+    tr.check_indices()
+
+
+def test_fused_trainer_reports_bad_ids(dev):
+    """An out-of-range id in a FusedTrainer batch surfaces as IndexError (the
+    id check is read back asynchronously and reported by a later step or by
+    check_indices())."""
+    import dcnr
+    torch.manual_seed(0)
+    m = dcnr.DCN_RecSys(300, 120, {"a": 40}, 3,
+                        dict(emb_dim=8, hidden_dim=64, n_cross_layers=1, n_res_blocks=1,
+                             dropout=0.0)).to(dev)
+    tr = dcnr.FusedTrainer(m, lr=1e-3)
+    B = 64
+    u = torch.randint(0, 300, (B,), device=dev)
+    i = torch.randint(0, 120, (B,), device=dev)
+    c = torch.randint(0, 40, (B, 1), device=dev)
+    n = torch.rand((B, 3), device=dev)
+    y = (torch.rand(B, device=dev) < 0.5).float()
+    tr.step(u, i, c, n, y)
+    tr.check_indices()
+    c[5, 0] = 40
+    with pytest.raises(IndexError):
+        tr.step(u, i, c, n, y)
+        tr.check_indices()
+
+
 @pytest.mark.parametrize("n,d,top_k", [(400, 64, 20), (700, 64, 12), (1500, 16, 10),
                                        (3000, 16, 6)])
 def test_mmr_lds_and_table_paths(dev, n, d, top_k):
