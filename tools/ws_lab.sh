@@ -5,7 +5,7 @@ cd "$(dirname "$0")"
 mkdir -p lab_bin
 C=../hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd/csrc
 for m in ${MODES:-0}; do
-  hipcc --offload-arch=gfx950 -O3 -std=c++17 -Wno-unused-result -Wno-unused-value -DWS_LAB_MODE=$m $EXTRA \
-    ws_lab.hip $C/gemm_nt.hip $C/gemm_ws.hip -o lab_bin/ws_lab_$m$SUFFIX &
+  hipcc --offload-arch=gfx950 -O3 -std=c++17 -Wno-unused-result -Wno-unused-value -DWS_LAB_MODE=$m \
+    $EXTRA ws_lab.hip $C/gemm_ws.hip -o lab_bin/ws_lab_$m$SUFFIX &
 done
 wait
