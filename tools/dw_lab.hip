@@ -5,6 +5,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <vector>
 
 namespace dcnr {
 void set_error(const char* fmt, ...) {
@@ -24,7 +25,17 @@ int main() {
   const int S = dcnr::gemm_dw_splits(N, K, B);
   (void)hipMalloc(&A, B * N * 2); (void)hipMalloc(&X, B * K * 2);
   (void)hipMalloc(&slab, (size_t)S * N * K * 4);
-  (void)hipMemset(A, 0x3c, B * N * 2); (void)hipMemset(X, 0x3c, B * K * 2);
+  {   // random bf16 in [-1, 1) (constant data runs at a higher clock than real data)
+    std::vector<uint16_t> h(B * (size_t)std::max(N, K));
+    uint32_t st = 12345;
+    for (auto& v : h) {
+      st = st * 1664525u + 1013904223u;
+      const float f = (float)(st >> 8) / 8388608.f - 1.f;
+      v = (uint16_t)(__builtin_bit_cast(uint32_t, f) >> 16);
+    }
+    (void)hipMemcpy(A, h.data(), B * N * 2, hipMemcpyHostToDevice);
+    (void)hipMemcpy(X, h.data() + 3, B * K * 2, hipMemcpyHostToDevice);
+  }
   dcnr::DwArgs a;
   std::memset(&a, 0, sizeof(a));
   a.A = A; a.lda = N; a.B = X; a.ldb = K; a.C = slab; a.ldc = K; a.slab_stride = (int64_t)N * K;
