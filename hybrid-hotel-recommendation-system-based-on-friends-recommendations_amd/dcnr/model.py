@@ -10,9 +10,15 @@ native call (``dcnr_forward``); the backward is one native call
 (``dcnr_backward``).  There is no CPU path: calling forward with CPU tensors
 raises.
 
-Extra keyword (not in the reference): ``precision`` -- ``"fp32"`` (default,
+Extra keywords (not in the reference): ``precision`` -- ``"fp32"`` (default,
 f32 MFMA, parity with the reference) or ``"bf16"`` (bf16 MFMA deep tower with
-fp32 accumulation and fp32 master weights).
+fp32 accumulation and fp32 master weights); ``check_indices`` -- an
+out-of-range id raises ``IndexError`` as ``nn.Embedding`` does (train.py:
+156-158).  ``True`` (default) checks asynchronously, like the reference on
+cuda where the bad index surfaces as a device-side assert at a later
+synchronisation: the error is raised by the next call on this model or by
+``check_index_errors()``; ``"sync"`` raises in the call itself (a host
+synchronisation per call); ``False`` clamps silently.
 """
 from __future__ import annotations
 
@@ -90,6 +96,43 @@ def dropout_seed(dev: torch.device, advance: bool = True) -> int:
     return _splitmix64((int(g.initial_seed()) & _M64) ^ _splitmix64(off))
 
 
+class IndexErrorWatch:
+    """Deferred id checks: the device error word of each call is copied into
+    a pinned ring slot after the call (stream-ordered, no host wait) and
+    polled without blocking; a set word raises IndexError."""
+    RING = 8
+
+    def __init__(self):
+        self.ring = None
+        self.pending = []
+        self.next = 0
+
+    def push(self, word: torch.Tensor):
+        if self.ring is None:
+            self.ring = torch.zeros(self.RING, dtype=torch.int32, pin_memory=True)
+        if len(self.pending) == self.RING:
+            self.poll(oldest=True)
+        slot = self.next
+        self.next = (slot + 1) % self.RING
+        self.ring[slot:slot + 1].copy_(word.view(torch.int32)[:1], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.pending.append((ev, slot))
+
+    def poll(self, oldest=False, all_=False):
+        keep = []
+        for n, (ev, slot) in enumerate(self.pending):
+            if all_ or (oldest and n == 0):
+                ev.synchronize()
+            elif not ev.query():
+                keep.append((ev, slot))
+                continue
+            if int(self.ring[slot]) != 0:
+                self.pending = []
+                raise IndexError("index out of range in self (ids passed to an earlier call)")
+        self.pending = keep
+
+
 class DCN_RecSys(nn.Module):
     """Deep & Cross Network with residual deep tower (train.py:125-170)."""
 
@@ -117,7 +160,10 @@ class DCN_RecSys(nn.Module):
         if precision not in _PRECISIONS:
             raise ValueError(f"precision must be one of {list(_PRECISIONS)}")
         self.precision = precision
-        self.check_indices = bool(check_indices)
+        if check_indices not in (True, False, "sync"):
+            raise ValueError("check_indices must be True, False or 'sync'")
+        self.check_indices = check_indices
+        self._index_watch = IndexErrorWatch()
         self._cat_rows = (ctypes.c_int64 * max(1, len(cat_dims)))(*[int(n) for n in cat_dims.values()])
         self._dims = dict(n_users=n_users, n_items=n_items, cat_dims=list(cat_dims.values()),
                           n_num=n_num_features, emb_dim=emb_dim, hidden=hidden_dim,
@@ -163,7 +209,14 @@ class DCN_RecSys(nn.Module):
         st = self.__dict__.copy()
         st.pop('_slots', None)
         st.pop('_ptr_cache', None)
+        st['_index_watch'] = IndexErrorWatch()
+        st.pop('_gc_flag', None)
         return st
+
+    def check_index_errors(self):
+        """Wait for every deferred id check of this model; raises IndexError
+        if any call saw an out-of-range id."""
+        self._index_watch.poll(all_=True)
 
     def _state_slots(self):
         slots = self.__dict__.get('_slots')
@@ -249,6 +302,7 @@ class DCN_RecSys(nn.Module):
 
     def forward(self, user_ids, item_ids, cat_features, num_features):
         dev = self._check_device(user_ids, item_ids, cat_features, num_features)
+        self._index_watch.poll()
         user_ids, item_ids, cat_features, num_features = self.prepare_inputs(
             user_ids, item_ids, cat_features, num_features)
         B = user_ids.shape[0]
@@ -286,11 +340,19 @@ class DCN_RecSys(nn.Module):
             raise RuntimeError("input shapes do not match the model")
         cat_features = cat_features.to(torch.int64).reshape(B, K).contiguous()
         num_features = num_features.to(torch.float32).reshape(B, F).contiguous()
+        self._index_watch.poll()
         cross = out if out is not None else torch.empty((B, D), dtype=torch.float32, device=dev)
         if cross.shape != (B, D) or cross.dtype != torch.float32 or not cross.is_contiguous():
             raise ValueError("out must be a contiguous fp32 [B, D] tensor")
         x0 = torch.empty((B, D), dtype=torch.float32, device=dev) if return_x0 else None
-        flag = torch.zeros(1, dtype=torch.int32, device=dev) if self.check_indices else None
+        flag = None
+        if self.check_indices:
+            flag = self.__dict__.get('_gc_flag')
+            if flag is None or flag.device != dev:
+                flag = torch.zeros(1, dtype=torch.int32, device=dev)
+                self.__dict__['_gc_flag'] = flag
+            else:
+                flag.zero_()
         lib = _lib.load()
         desc = self.desc()
         _lib.check(lib.dcnr_gather_cross(ctypes.byref(desc), self.state_ptr_array(),
@@ -301,8 +363,12 @@ class DCN_RecSys(nn.Module):
                                          cross.data_ptr(), D,
                                          flag.data_ptr() if flag is not None else None,
                                          _lib.stream_ptr(dev)), "dcnr_gather_cross")
-        if flag is not None and int(flag.item()) != 0:
-            raise IndexError("index out of range in self")
+        if flag is not None:
+            if self.check_indices == "sync":
+                if int(flag.item()) != 0:
+                    raise IndexError("index out of range in self")
+            else:
+                self._index_watch.push(flag)
         return (x0, cross) if return_x0 else cross
 
     # ----------------------------------------------------------- flat storage
@@ -337,11 +403,10 @@ def _hook_error(model):
 
 
 def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
-                ws: Optional[torch.Tensor] = None, defer_index_check: bool = False):
-    """One native forward.  With ``model.check_indices`` an out-of-range id
-    raises IndexError here (host sync), or -- ``defer_index_check`` -- is left
-    in the workspace's error word (``ws[:4]``) for the caller to read later
-    (FusedTrainer polls it without stalling the stream)."""
+                ws: Optional[torch.Tensor] = None):
+    """One native forward.  With ``model.check_indices`` the workspace's
+    error word (``ws[:4]``) is checked: in this call (``"sync"``) or through
+    the model's deferred watch."""
     lib = _lib.load()
     B = user.shape[0]
     dev = user.device
@@ -360,9 +425,11 @@ def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
     model._active_ws = None
     _hook_error(model)
     _lib.check(st, "dcnr_forward")
-    if model.check_indices and not defer_index_check:
+    if model.check_indices == "sync":
         _lib.check(lib.dcnr_check_errors(ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)),
                    "embedding")
+    elif model.check_indices:
+        model._index_watch.push(ws[:4])
     return logits, ws
 
 

@@ -61,11 +61,6 @@ class FusedTrainer:
         self.step_count = 0
         self._ws = None
         self._grads = [p.grad for p in model.param_tensors()]   # views into gflat
-        # deferred index checks: the forward's error word is copied into a
-        # pinned ring slot after each step and polled without a host sync
-        self._idx_ring = None
-        self._idx_pending = []
-        self._idx_next = 0
         if sync_bn and self.world > 1:
             from .parallel import install_sync_bn
             install_sync_bn(model, process_group)
@@ -78,9 +73,8 @@ class FusedTrainer:
         user, item, cat, num = model.prepare_inputs(user, item, cat, num)
         y = y.reshape(-1).to(torch.float32).contiguous()
         seed = dropout_seed(user.device)
-        logits, self._ws = run_forward(model, True, seed, user, item, cat, num, self._ws,
-                                       defer_index_check=True)
-        self._queue_index_check()
+        model._index_watch.poll()
+        logits, self._ws = run_forward(model, True, seed, user, item, cat, num, self._ws)
         # grad_scale 1/world: the SUM all-reduce then yields the global mean gradient
         loss, dz = bce_with_logits(logits, y, True, 1.0 / self.world)
         run_backward(model, user, item, cat, num, dz, self._ws, self._grads, seed,
@@ -88,44 +82,10 @@ class FusedTrainer:
         self.exchange_and_update(user_ids=user)
         return (loss, logits) if return_logits else loss
 
-    _IDX_RING = 4
-
-    def _queue_index_check(self):
-        """nn.Embedding raises on an out-of-range id (train.py:156-158; on cuda
-        as an asynchronous device assert).  Here the id check's error word is
-        read back asynchronously and reported by a later step (or by
-        ``check_indices()``) as IndexError."""
-        if not self.model.check_indices:
-            return
-        if self._idx_ring is None:
-            self._idx_ring = torch.zeros(self._IDX_RING, dtype=torch.int32, pin_memory=True)
-        if len(self._idx_pending) == self._IDX_RING:
-            self._poll_index_checks(oldest=True)
-        slot = self._idx_next
-        self._idx_next = (slot + 1) % self._IDX_RING
-        self._idx_ring[slot:slot + 1].copy_(self._ws[:4].view(torch.int32), non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self._idx_pending.append((ev, slot))
-        self._poll_index_checks()
-
-    def _poll_index_checks(self, oldest=False, all_=False):
-        keep = []
-        for n, (ev, slot) in enumerate(self._idx_pending):
-            if all_ or (oldest and n == 0):
-                ev.synchronize()
-            elif not ev.query():
-                keep.append((ev, slot))
-                continue
-            if int(self._idx_ring[slot]) != 0:
-                self._idx_pending = []
-                raise IndexError("index out of range in self (ids of a batch passed to an "
-                                 "earlier FusedTrainer.step)")
-        self._idx_pending = keep
-
     def check_indices(self):
-        """Wait for every step's id check; raises IndexError if any failed."""
-        self._poll_index_checks(all_=True)
+        """Wait for every step's id check; raises IndexError if any failed
+        (the checks are otherwise reported by a later step)."""
+        self.model.check_index_errors()
 
     def exchange_and_update(self, adam=None, user_ids=None):
         """The data-parallel gradient exchange and the optimizer step on the

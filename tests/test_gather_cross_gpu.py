@@ -70,9 +70,13 @@ def test_gather_cross_empty_and_oob(dev):
     c[17, 5] = 250      # one past the end of cat table 5
     with pytest.raises(IndexError):
         m.gather_cross(*to_dev(dev, u, i, c, n))
+        m.check_index_errors()
     c[17, 5] = -1
+    m.check_indices = "sync"
     with pytest.raises(IndexError):
         m.gather_cross(*to_dev(dev, u, i, c, n))
+    c[17, 5] = 3
+    m.gather_cross(*to_dev(dev, u, i, c, n))
 
 
 def test_gather_cross_full_size_cfg2(dev):

@@ -270,7 +270,16 @@ def test_index_out_of_range_raises(dev):
     u, i, c, n, _ = gc.make_inputs(cfg, 8, 3)
     u = u.copy()
     u[3] = cfg["n_users"]  # one past the end
+    # default: asynchronous, as the reference on cuda (a later call / check raises)
     with torch.no_grad(), pytest.raises(IndexError):
+        m(*to_dev(dev, u, i, c, n))
+        m.check_index_errors()
+    # "sync": the call itself raises
+    m.check_indices = "sync"
+    with torch.no_grad(), pytest.raises(IndexError):
+        m(*to_dev(dev, u, i, c, n))
+    u[3] = 0
+    with torch.no_grad():
         m(*to_dev(dev, u, i, c, n))
 
 
