@@ -62,7 +62,9 @@ CLASS_KERNELS = {
     "gemm_dw": "gemm_dw_kernel (deep-tower weight gradient)",
     "rowwise": "rowcol_kernel (BN apply / statistics passes)",
     "reduce": "reduce / split-K combine kernels",
-    "cross_bwd": "cross_bwd_v4_kernel (cross backward + embedding-grad scatter)",
+    "cross_bwd": "cross_bwd_v4_kernel (cross backward, total dx0 rows)",
+    "emb_sort": "emb_keys_kernel + rocPRIM radix sort of the ids (side stream, overlapped)",
+    "emb_sum": "emb_runs_short/long_kernel (fixed-order embedding-gradient sums)",
     "head": "row_dot / logits / bce kernels",
     "adam": "adam_kernel (fused AdamW)",
     "pack": "pack / zero-fill kernels",

@@ -89,6 +89,44 @@ namespace {
     if (st_ != DCNR_OK) return st_;          \
   } while (0)
 
+// The id sort of the embedding backward runs on the call's stream unless
+// DCNR_EMB_SORT_SIDE=1 puts it on a side stream overlapped with the deep-tower
+// backward (measured slower: its blocks hold CU slots the GEMMs wait for).
+bool emb_sort_on_side() {
+  static const bool on = [] {
+    const char* e = getenv("DCNR_EMB_SORT_SIDE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+// Fork/join of the embedding-backward side stream within one call.
+struct SideJoin {
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  dcnr_status fork(hipStream_t s, bool use_side) {
+    if (!use_side) { side = s; return DCNR_OK; }
+    TRY(emb_side_stream(&side));
+    DCNR_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+    DCNR_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
+    DCNR_HIP(hipEventRecord(fork_ev, s));
+    DCNR_HIP(hipStreamWaitEvent(side, fork_ev, 0));
+    return DCNR_OK;
+  }
+  dcnr_status record() {
+    if (join_ev) DCNR_HIP(hipEventRecord(join_ev, side));
+    return DCNR_OK;
+  }
+  dcnr_status join(hipStream_t s) {
+    if (join_ev) DCNR_HIP(hipStreamWaitEvent(s, join_ev, 0));
+    return DCNR_OK;
+  }
+  ~SideJoin() {
+    if (fork_ev) (void)hipEventDestroy(fork_ev);
+    if (join_ev) (void)hipEventDestroy(join_ev);
+  }
+};
+
 constexpr int MAX_CAT = 64;
 constexpr int MAX_RES = 8;
 constexpr int MAX_CROSS = 7;
@@ -200,11 +238,13 @@ struct Layout {
   // per-block backward buffers: all alias G/dt2/du/da/a1 unless
   // DCNR_FLAG_KEEP_INTERMEDIATES gives each block its own
   void* duk[MAX_RES]; void* dt2k[MAX_RES]; void* dak[MAX_RES]; void* dt1k[MAX_RES];
-  float* dx0; float* slab; int64_t slab_elems; float* cpart; size_t cpart_elems;
+  float* dx0; float* dx0t;   // dx0t: total dx0 of the tables' columns, table-major
+  float* slab; int64_t slab_elems; float* cpart; size_t cpart_elems;
   // 1-bit keep masks for the backward GEMM epilogues (bf16, Hp % 32 == 0):
   // mask_a1[j] = [a1_j != 0], mask_h[j] = [h_j > 0] (j >= 1)
   uint8_t* mask_a1[MAX_RES]; uint8_t* mask_h[MAX_RES + 1];
   float* cred2; size_t cred2_elems;             // cross partial second stage
+  EmbSortBufs emb;                              // deterministic embedding backward
   double* bce_part;
   size_t total;
 };
@@ -271,12 +311,26 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
     L.du = b.take(act);
     L.da = b.take(act);
     L.dx0 = (float*)b.take((size_t)B * d.Dp * 4);
-    L.slab_elems = (int64_t)64 * d.Hp * std::max(d.Hp, d.Dp);
+    L.dx0t = (float*)b.take((size_t)B * d.Dp * 4);   // table-major, tables' columns only
+    // split-K slabs: the fp32 path adapts its splits to 64; the bf16 kernel's
+    // split count depends on the tile count (narrow H -> more splits)
+    L.slab_elems = std::max<int64_t>({(int64_t)64 * d.Hp * std::max(d.Hp, d.Dp),
+                                      (int64_t)gemm_dw_splits(d.Hp, d.Hp, B) * d.Hp * d.Hp,
+                                      (int64_t)gemm_dw_splits(d.Hp, d.Dp, B) * d.Hp * d.Dp});
     L.slab = (float*)b.take((size_t)L.slab_elems * 4);
     L.cpart_elems = cross_bwd_part_elems(d.D, d.L);
     L.cpart = (float*)b.take(L.cpart_elems * 4);
     L.cred2_elems = cross_red2_elems(d.D, d.L);
     L.cred2 = (float*)b.take(L.cred2_elems * 4);
+    {
+      const int64_t n = (int64_t)(2 + d.K) * B;
+      L.emb.keys = (uint32_t*)b.take((size_t)n * 4);
+      L.emb.vals = (uint32_t*)b.take((size_t)n * 4);
+      L.emb.keys_s = (uint32_t*)b.take((size_t)n * 4);
+      L.emb.vals_s = (uint32_t*)b.take((size_t)n * 4);
+      L.emb.tmp_bytes = emb_sort_tmp_bytes(n);
+      L.emb.tmp = b.take(L.emb.tmp_bytes);
+    }
     for (int j = 0; j < d.R; ++j) {
       L.duk[j] = keep ? b.take(act) : L.du;
       L.dt2k[j] = keep ? b.take(act) : L.dt2;
@@ -690,6 +744,7 @@ dcnr_status dcnr_workspace_offset(const dcnr_model_desc* desc, int64_t B, int mo
     case DCNR_WS_G: if (train) p = L.G; break;
     case DCNR_WS_DX0: if (train) p = L.dx0; break;
     case DCNR_WS_ZC: p = L.zc; break;
+    case DCNR_WS_DX0_TOTAL: if (train) p = L.dx0t; break;
   }
   *offset = p ? (int64_t)((const char*)p - base) : -1;
   return DCNR_OK;
@@ -858,6 +913,24 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     TRYB(DCNR_K_PACK, zb, fill_zero_multi(2 + d.K, zp, zn, s));
   }
 
+  // embedding backward, part 1: sort the ids (they are all it reads) on the
+  // side stream while the deep-tower backward runs on `s`
+  GatherDesc g = make_gather(d, P, desc->n_num);
+  EmbBwdDesc eb;
+  memset(&eb, 0, sizeof(eb));
+  eb.n_tab = g.n_tab;
+  for (int t = 0; t < g.n_tab; ++t) {
+    eb.grad[t] = Gr.tab[t]; eb.rows[t] = g.rows[t]; eb.width[t] = g.width[t]; eb.off[t] = g.off[t];
+  }
+  SideJoin sj;
+  TRY(sj.fork(s, emb_sort_on_side()));
+  {
+    hipStream_t s = sj.side;   // TRYB times the side stream
+    TRYB(DCNR_K_EMB_SORT, 2.0 * 8.0 * g.n_tab * B + 8.0 * B * (2 + d.K) + 4.0 * B * 2,
+         emb_sort(eb, user_ids, item_ids, cat_features, B, L.emb, s));
+  }
+  TRY(sj.record());
+
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   const bool fuse = epi_stats_ok(d);   // BN partials from the dX GEMM epilogues
   int nc_du = 0;   // > 0: L.du and its BN2 partials were made by the previous dX GEMM
@@ -941,8 +1014,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     g.M = B; g.N = d.Dp; g.K = Hp; g.k_per_split = Hp;
     TRYB(DCNR_K_GEMM_DX, act_b(d, B) + 4.0 * B * d.Dp + w_b(d, d.Dp), gemm_nn(d.prec, EPI_STORE, g, 1, s));
   }
-  // ---- cross stack + head bias + embedding scatter
-  GatherDesc g = make_gather(d, P, desc->n_num);
+  // ---- cross stack + head bias + total dx0 rows; embedding backward part 2
   CrossBwdParams cb;
   memset(&cb, 0, sizeof(cb));
   cb.cp = make_cross(d, P);
@@ -950,13 +1022,18 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   cb.dwf_cross = Gr.wf + H;
   cb.dbf = Gr.bf;
   for (int t = 0; t < 2 + d.K; ++t) cb.emb_grad[t] = Gr.tab[t];
+  cb.dx0_tot = L.dx0t;
   CrossBwdScratch cws{L.cpart, L.cpart_elems, L.cred2, L.cred2_elems, L.red_cnt, CNT_SLOTS};
-  // re-gather + dx0 + dz read, one fp32 add per embedding element
+  // re-gather + dx0 read + total dx0 write + dz read
   double ew = 0;
   for (int t = 0; t < 2 + d.K; ++t) ew += d.widths[t];
   TRYB(DCNR_K_CROSS_BWD, (double)B * (gather_row_b(d, desc->n_num) + 4.0 * d.Dp + 4.0 + 4.0 * ew),
        cross_bwd_scatter(g, cb, user_ids, item_ids, cat_features, num_features, dz, B, L.dx0, d.Dp,
                         cws, accumulate, s));
+  // sorted (table row, sample) pairs + the dx0 entries they name -> grad rows
+  TRY(sj.join(s));
+  TRYB(DCNR_K_EMB_SUM, (double)B * (4.0 * ew + 8.0 * g.n_tab),
+       emb_segment_sum(eb, L.emb, B, L.dx0t, accumulate, s));
   return DCNR_OK;
 }
 

@@ -402,7 +402,10 @@ struct CrossBwdParams {
   float* dw[8]; float* db[8];      // grads (final)
   float* dwf_cross;                // grad final_linear.weight + H
   float* dbf;                      // grad final_linear.bias
-  float* emb_grad[MAX_TABLES];     // dense embedding grads (atomic scatter-add)
+  float* emb_grad[MAX_TABLES];     // dense embedding grads (atomic scatter-add) ...
+  float* dx0_tot;                  // ... or, if set, the total dx0 of the table columns
+                                   // stored here table-major (table t: [B][w_t] at
+                                   // B * off_t) for embed_bwd.hip
 };
 struct CrossBwdScratch {
   float* part; size_t part_elems;  // per-block partials
@@ -417,6 +420,27 @@ dcnr_status cross_bwd_scatter(const GatherDesc& g, const CrossBwdParams& p,
                               int accumulate, hipStream_t s);
 
 size_t cross_bwd_part_elems(int D, int L);
+// deterministic embedding gradients (embed_bwd.hip)
+struct EmbBwdDesc {
+  float* grad[MAX_TABLES];       // dense grads, [rows][width] each
+  int64_t rows[MAX_TABLES];
+  int width[MAX_TABLES];
+  int off[MAX_TABLES];           // first x0 column of the table; its dx0 block [B][w]
+                                 // starts at B * off in the table-major dx0_total
+  int n_tab;
+};
+struct EmbSortBufs {
+  uint32_t *keys, *vals;         // [n_tab * B] table-major (key = base_t + id, value = sample)
+  uint32_t *keys_s, *vals_s;     // sorted
+  void* tmp; size_t tmp_bytes;   // rocPRIM scratch
+};
+size_t emb_sort_tmp_bytes(int64_t n);
+dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* item,
+                     const int64_t* cat, int64_t B, const EmbSortBufs& sb, hipStream_t s);
+dcnr_status emb_segment_sum(const EmbBwdDesc& e, const EmbSortBufs& sb, int64_t B,
+                            const float* dx0_total, int accumulate, hipStream_t s);
+dcnr_status emb_side_stream(hipStream_t* out);
+
 size_t cross_red2_elems(int D, int L);
 int cross_red_groups(int D, int L);
 

@@ -129,7 +129,11 @@ dcnr_status dcnr_workspace_size(const dcnr_model_desc* desc, int64_t B, int mode
  * that check each stage against a recomputation from the kernels' own stored
  * inputs.  Row-major with leading dimension Hp = hidden rounded up to 8
  * (Dp for x0 / dx0); element type bf16 in bf16 mode, else fp32 (masks: 1 bit
- * per element, Hp/8 bytes per row; BN vectors, zc, dx0: fp32).  `index` is
+ * per element, Hp/8 bytes per row; BN vectors, zc, dx0: fp32).  dx0 is the
+ * deep tower's part of d loss/d x0; dx0_total (fp32) is deep + cross part of
+ * the embedding tables' columns only, TABLE-MAJOR: table t's [B][w_t] block
+ * starts at float B * off_t (off_t = its first x0 column) -- the rows the
+ * embedding gradients sum.  `index` is
  * the block j (h: 0..n_res; bn_*: 2j for bn1, 2j+1 for bn2).  *offset = -1
  * when that tensor is not materialised in this configuration. */
 typedef enum {
@@ -137,7 +141,7 @@ typedef enum {
   DCNR_WS_MASK_A1 = 5, DCNR_WS_MASK_H = 6, DCNR_WS_BN_MEAN = 7, DCNR_WS_BN_INVSTD = 8,
   DCNR_WS_BN_SCALE = 9, DCNR_WS_BN_SHIFT = 10, DCNR_WS_DU = 11, DCNR_WS_DT2 = 12,
   DCNR_WS_DA = 13, DCNR_WS_DT1 = 14, DCNR_WS_G = 15, DCNR_WS_DX0 = 16, DCNR_WS_ZC = 17,
-  DCNR_WS_KINDS = 18
+  DCNR_WS_DX0_TOTAL = 18, DCNR_WS_KINDS = 19
 } dcnr_ws_tensor;
 dcnr_status dcnr_workspace_offset(const dcnr_model_desc* desc, int64_t B, int mode, int kind,
                                   int index, int64_t* offset);
@@ -170,8 +174,12 @@ dcnr_status dcnr_gather_cross(const dcnr_model_desc* desc, void* const* params,
 
 /* Backward of the last train-mode dcnr_forward on `ws`: given dL/dlogits
  * [B], writes dL/dparam for every parameter into `grads`.  accumulate = 0
- * overwrites (embedding grads are zeroed first, then scatter-added, i.e.
- * embedding_dense_backward semantics); accumulate = 1 adds into grads. */
+ * overwrites (embedding grads are zeroed, then every referenced row gets the
+ * sum of its samples' dx0 rows, i.e. embedding_dense_backward semantics);
+ * accumulate = 1 adds into grads.  Deterministic: the embedding sums run in
+ * ascending sample order after a stable sort of the ids (on a library-owned
+ * side stream, joined back into `stream` before the call's last kernel), so
+ * two calls on the same inputs give bit-identical gradients. */
 dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void* const* grads,
                           const int64_t* user_ids, const int64_t* item_ids,
                           const int64_t* cat_features, const float* num_features, int64_t B,
@@ -289,7 +297,9 @@ typedef enum {
   DCNR_K_KNN = 9,          /* cosine top-k                                  */
   DCNR_K_PACK = 10,        /* weight packing / zero fills                  */
   DCNR_K_SERVE = 11,       /* candidate union, ranking batch, sort, MMR     */
-  DCNR_K_COUNT = 12
+  DCNR_K_EMB_SORT = 12,    /* embedding-backward id sort (side stream)      */
+  DCNR_K_EMB_SUM = 13,     /* embedding-backward per-row segmented sums     */
+  DCNR_K_COUNT = 14
 } dcnr_kernel_class;
 
 void dcnr_profile_enable(int on);

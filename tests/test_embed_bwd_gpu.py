@@ -1,0 +1,211 @@
+"""Deterministic embedding backward (csrc/embed_bwd.hip): the dense
+embedding gradients of loss.backward() (reference train.py:156-158, 225;
+nn.Embedding with sparse=False, i.e. embedding_dense_backward).
+
+grad_t[r] = sum of dx0_total[b, off_t:off_t+w_t] over the samples b with
+id_t[b] == r.  The library sums each row in a FIXED order: runs of <= 16
+samples sequentially in ascending b; longer runs one wave per row, walked in
+blocks of 64 entries, slot s of S lane slots taking entries s, s+S, ... of
+every block in ascending order, slots added in ascending order.  ``emulate_table`` restates that order in numpy fp32, so the
+gradients are checked BIT-EXACT against it, from the kernels' own dx0_total
+(table-major: table t's [B][w_t] block at float offset B * off_t).  The fp64 recomputation of dx0_total itself
+is pinned by tests/test_stages_gpu.py.
+
+Skewed ids exercise both paths: a user id taken by 40 % of the batch, a
+Zipf-like item column, a categorical column with one value (a run of B) and
+one with two values, uniform columns elsewhere.
+"""
+import numpy as np
+import pytest
+import torch
+
+import golden_common as gc
+
+pytestmark = pytest.mark.gpu
+
+SHORT = 16   # embed_bwd.hip LIM
+BLK = 64     # embed_bwd.hip emb_runs_long_kernel block of entries
+
+
+def emulate_table(ids, X, rows, vec):
+    """fp32 gradient of one table in the library's summation order."""
+    B, w = X.shape
+    order = np.argsort(ids, kind="stable")
+    ks = ids[order]
+    heads = np.flatnonzero(np.r_[True, ks[1:] != ks[:-1]])
+    ends = np.r_[heads[1:], B]
+    lens = ends - heads
+    g = np.zeros((rows, w), np.float32)
+    short = lens <= SHORT
+    hs, ls = heads[short], lens[short]
+    acc = np.zeros((len(hs), w), np.float32)
+    for k in range(SHORT):
+        sel = ls > k
+        acc[sel] += X[order[hs[sel] + k]]
+    g[ks[hs]] = acc
+    G = w // vec
+
+    def seq(a):   # sequential fp32 sum over axis 0 (0 if empty)
+        return np.cumsum(a, axis=0, dtype=np.float32)[-1] if len(a) else np.zeros(a.shape[1], np.float32)
+
+    for h, e in zip(heads[~short], ends[~short]):
+        ent = X[order[h:e]]
+        m = e - h
+        out = np.zeros(w, np.float32)
+        for cb in range(0, G, 64):
+            gb = min(64, G - cb)
+            S = 64 // gb
+            cols = slice(cb * vec, (cb + gb) * vec)
+            sub = ent[:, cols]
+            tot = None
+            for s in range(S):   # slot s: entries s, s+S, ... of every BLK-entry block
+                idx = [p + j for p in range(0, m, BLK) for j in range(s, BLK, S) if p + j < m]
+                t = seq(sub[idx])
+                tot = t if tot is None else tot + t
+            out[cols] = tot
+        g[ks[h]] = out
+    return g
+
+
+def _cfg():
+    return dict(n_users=200_000, n_items=5000, cat_dims={f"c{k}": 1000 for k in range(12)},
+                n_num=8, params=dict(emb_dim=32, hidden_dim=256, n_cross_layers=3,
+                                     n_res_blocks=2, dropout=0.0))
+
+
+def _skewed_batch(cfg, B, dev, seed=3):
+    rng = np.random.default_rng(seed)
+    u = rng.integers(0, cfg["n_users"], B)
+    u[rng.random(B) < 0.4] = 7
+    i = np.minimum((cfg["n_items"] * rng.random(B) ** 4).astype(np.int64), cfg["n_items"] - 1)
+    cards = list(cfg["cat_dims"].values())
+    c = np.stack([rng.integers(0, n, B) for n in cards], 1)
+    c[:, 0] = 5
+    c[:, 1] = rng.integers(0, 2, B)
+    n = rng.random((B, cfg["n_num"]), dtype=np.float32)
+    y = (rng.random(B) < 0.5).astype(np.float32)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+    return (t(u, torch.int64), t(i, torch.int64), t(c, torch.int64), t(n, torch.float32),
+            t(y, torch.float32))
+
+
+def _model(cfg, dev, precision="bf16", keep=True):
+    import dcnr
+    torch.manual_seed(11)
+    m = dcnr.DCN_RecSys(cfg["n_users"], cfg["n_items"], cfg["cat_dims"], cfg["n_num"],
+                        dict(cfg["params"]), precision=precision)
+    gc.perturb_state(m, 12)
+    m = m.to(dev).train()
+    m.keep_intermediates = keep
+    return m
+
+
+def _fwd_bwd(m, batch, seed, grads=None, accumulate=False):
+    from dcnr.model import run_backward, run_forward
+    from dcnr.ops import bce_with_logits
+    u, i, c, n, y = batch
+    logits, ws = run_forward(m, True, seed, u, i, c, n)
+    _, dz = bce_with_logits(logits, y)
+    if grads is None:
+        grads = [torch.empty_like(q) for q in m.param_tensors()]
+    run_backward(m, u, i, c, n, dz, ws, grads, seed, accumulate)
+    torch.cuda.synchronize()
+    return grads, ws
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_embedding_grads_bit_exact_skewed(dev, precision):
+    """Every table's gradient equals the fixed-order fp32 emulation from the
+    kernels' own dx0_total, bit for bit; rows no sample references are 0."""
+    from dcnr import _lib
+    cfg = _cfg()
+    B = 65536
+    m = _model(cfg, dev, precision)
+    batch = _skewed_batch(cfg, B, dev)
+    grads, ws = _fwd_bwd(m, batch, seed=77)
+    names = [k for k, _ in m.named_parameters()]
+    gd = dict(zip(names, grads))
+    D = m._dims["input_dim"]
+    Dp = (D + 7) // 8 * 8
+    off = m.workspace_offset(B, _lib.TRAIN, "dx0_total", 0)
+    assert off >= 0
+    X = ws[off:off + B * Dp * 4].view(torch.float32).cpu().numpy()   # table-major blocks
+    u, i, c = (t.cpu().numpy() for t in batch[:3])
+    tabs = [("user_embedding.weight", u), ("item_embedding.weight", i)]
+    tabs += [(f"cat_embeddings.{k}.weight", c[:, k]) for k in range(c.shape[1])]
+    widths = [m.state_dict()[name].shape[1] for name, _ in tabs]
+    vec = 4 if all(w % 4 == 0 for w in widths) and D % 4 == 0 else 1
+    col = 0
+    long_runs = 0
+    for (name, ids), w in zip(tabs, widths):
+        rows = m.state_dict()[name].shape[0]
+        ref = emulate_table(ids, X[B * col:B * (col + w)].reshape(B, w), rows, vec)
+        got = gd[name].cpu().numpy()
+        assert np.array_equal(got, ref), (name, np.abs(got - ref).max())
+        long_runs += int((np.bincount(ids, minlength=rows) > SHORT).sum())
+        col += w
+    assert long_runs > 2000   # both kernels ran
+
+
+def test_embedding_grads_bit_exact_odd_widths(dev):
+    """CFG_ODD (table widths 24, 2, 5, 2: the scalar-column kernels), every
+    run long (B >> rows): bit-exact against the emulation."""
+    from dcnr import _lib
+    cfg = gc.CFG_ODD
+    B = 4096
+    m = _model(cfg, dev, "fp32")
+    u, i, c, n, y = gc.make_inputs(cfg, B, 5)
+    t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+    batch = (t(u, torch.int64), t(i, torch.int64), t(c, torch.int64), t(n, torch.float32),
+             t(y, torch.float32))
+    grads, ws = _fwd_bwd(m, batch, seed=5)
+    gd = dict(zip([k for k, _ in m.named_parameters()], grads))
+    D = m._dims["input_dim"]
+    Dp = (D + 7) // 8 * 8
+    off = m.workspace_offset(B, _lib.TRAIN, "dx0_total", 0)
+    X = ws[off:off + B * Dp * 4].view(torch.float32).cpu().numpy()   # table-major blocks
+    tabs = [("user_embedding.weight", u), ("item_embedding.weight", i)]
+    tabs += [(f"cat_embeddings.{k}.weight", c[:, k]) for k in range(c.shape[1])]
+    col = 0
+    for name, ids in tabs:
+        rows, w = m.state_dict()[name].shape
+        ref = emulate_table(ids, X[B * col:B * (col + w)].reshape(B, w), rows, 1)
+        assert np.array_equal(gd[name].cpu().numpy(), ref), name
+        col += w
+
+
+def test_full_size_backward_bit_identical(dev):
+    """The bench's step (configs[2] shape, B=131072, bf16, dropout 0.6): two
+    backward passes from the same state, batch and dropout seed give
+    bit-identical gradients for every parameter."""
+    import copy
+    cfg = dict(n_users=1_000_000, n_items=100_000, cat_dims={f"c{k}": 1000 for k in range(12)},
+               n_num=8, params=dict(emb_dim=32, hidden_dim=512, n_cross_layers=3,
+                                    n_res_blocks=4, dropout=0.6))
+    m = _model(cfg, dev, "bf16", keep=False)
+    m2 = copy.deepcopy(m)
+    B = 131072
+    g = torch.Generator(device=dev).manual_seed(9)
+    batch = (torch.randint(0, cfg["n_users"], (B,), device=dev, generator=g),
+             torch.randint(0, cfg["n_items"], (B,), device=dev, generator=g),
+             torch.randint(0, 1000, (B, 12), device=dev, generator=g),
+             torch.rand((B, 8), device=dev, generator=g),
+             (torch.rand((B,), device=dev, generator=g) < 0.5).float())
+    g1, _ = _fwd_bwd(m, batch, seed=1234)
+    g2, _ = _fwd_bwd(m2, batch, seed=1234)
+    for k, a, b in zip([k for k, _ in m.named_parameters()], g1, g2):
+        assert torch.equal(a, b), k
+
+
+def test_accumulate_doubles(dev):
+    """accumulate=1 adds into the grads: a second identical step accumulated
+    onto the first gives exactly twice every gradient (the embedding rows
+    included: row = old + fresh sum)."""
+    cfg = _cfg()
+    m = _model(cfg, dev, "bf16", keep=False)
+    batch = _skewed_batch(cfg, 16384, dev, seed=4)
+    g1, _ = _fwd_bwd(m, batch, seed=3)
+    ref = [x.clone() for x in g1]
+    _fwd_bwd(m, batch, seed=3, grads=g1, accumulate=True)
+    for k, a, r in zip([k for k, _ in m.named_parameters()], g1, ref):
+        assert torch.equal(a, 2 * r), k

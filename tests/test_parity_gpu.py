@@ -284,17 +284,16 @@ def test_index_out_of_range_raises(dev):
 
 
 def test_backward_deterministic(dev):
+    """Two backward passes on the same state and batch are bit-identical for
+    EVERY gradient, the embedding tables included (csrc/embed_bwd.hip)."""
     cfg = gc.CFG3R
     m = our_model(cfg).to(dev)
     u, i, c, n, y = gc.make_inputs(cfg, 512, 77)
     m2 = copy.deepcopy(m)
     _, _, g1 = run_train(m, dev, u, i, c, n, y)
     _, _, g2 = run_train(m2, dev, u, i, c, n, y)
-    for k in g1:
-        if "embedding" in k:
-            np.testing.assert_allclose(g1[k], g2[k], rtol=1e-6, atol=1e-9)
-        else:
-            assert np.array_equal(g1[k], g2[k]), k
+    for k in g1:   # embedding grads included (sorted, fixed-order sums)
+        assert np.array_equal(g1[k], g2[k]), k
 
 
 def test_dropout_train_step_exact_masks(dev):

@@ -82,6 +82,17 @@ def check_bf16(name, got, ref, stats, scale):
     assert flips <= FLIP_FRAC, (name, flips)
 
 
+def _table_cols(sd, K):
+    """[(first, end) x0 column of each table]: user, item, cat 0..K-1."""
+    names = ["user_embedding.weight", "item_embedding.weight"]
+    names += [f"cat_embeddings.{k}.weight" for k in range(K)]
+    out, a = [], 0
+    for n in names:
+        out.append((a, a + sd[n].shape[1]))
+        a += sd[n].shape[1]
+    return out
+
+
 def check_rel(name, got, ref, tol=REL):
     got, ref = got.double(), ref.double()
     e = ((got - ref).norm() / ref.norm().clamp_min(1e-300)).item()
@@ -268,6 +279,11 @@ def test_bf16_step_stage_by_stage(dev, full):
         check_rel(f"cross_w[{l}]", gd[f"cross_network.{l}.w.weight"][0], (gx[:, None] * xl).sum(0))
         dx = dx * (1.0 + sl)[:, None] + gx[:, None] * wl[None, :]
     dxe = dx0.double() + dx
+    # dx0_total: the tables' columns of dx0 + dx_cross, table-major ([B][w_t] per table)
+    flat = T("dx0_total", cols=Dp, dtype=f32).reshape(-1)
+    Dt = D - cfg["n_num"]
+    tot = torch.cat([flat[B * a:B * b].view(B, b - a) for a, b in _table_cols(sd0, K)], 1)
+    check_rel("dx0_total", tot, dxe[:, :Dt])
     off = 0
     tabs = [("user_embedding.weight", u), ("item_embedding.weight", i)]
     tabs += [(f"cat_embeddings.{k}.weight", c[:, k]) for k in range(K)]
