@@ -430,11 +430,12 @@ struct EmbBwdDesc {
   int n_tab;
 };
 struct EmbSortBufs {
-  uint32_t *keys, *vals;         // [n_tab * B] table-major (key = base_t + id, value = sample)
+  uint32_t *ids;                 // [n_tab * B] clamped ids, table-major
+  uint32_t *keys, *vals;         // [n_tab * B] level-1 sorted (tables of > 1024 rows)
   uint32_t *keys_s, *vals_s;     // sorted
-  void* tmp; size_t tmp_bytes;   // rocPRIM scratch
+  void* tmp; size_t tmp_bytes;   // per-(bucket, chunk) counts / offsets of the sort
 };
-size_t emb_sort_tmp_bytes(int64_t n);
+size_t emb_sort_tmp_bytes(const int64_t* rows, int n_tab, int64_t B);
 dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* item,
                      const int64_t* cat, int64_t B, const EmbSortBufs& sb, hipStream_t s);
 dcnr_status emb_segment_sum(const EmbBwdDesc& e, const EmbSortBufs& sb, int64_t B,

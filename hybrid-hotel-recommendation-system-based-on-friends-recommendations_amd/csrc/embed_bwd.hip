@@ -8,13 +8,14 @@
 // inputs give bit-identical gradients (the fp32 scatter-atomics they replace
 // did not).  Three steps per step of the backward:
 //
-//   1. emb_keys_kernel: key = base_t + id (all tables in one key space),
-//      value = b, laid out table-major: entries of table t at [t*B, (t+1)*B).
-//   2. rocPRIM radix_sort_pairs (stable): after it table t still occupies
-//      [t*B, (t+1)*B) (its keys lie in [base_t, base_t + rows_t)) and each
-//      run of equal keys lists its samples in ascending b.  Steps 1-2 read
-//      only the ids, so dcnr_backward runs them on a side stream while the
-//      deep-tower backward runs (they join before step 3).
+//   1-2. a stable two-level counting sort of each table's (id, sample)
+//      pairs (below: bucket counts per chunk, a scan, a stable scatter, then
+//      per-bucket sorts on the low id bits); after it table t occupies
+//      [t*B, (t+1)*B) of the sorted arrays (key = base_t + id) and each run
+//      of equal keys lists its samples in ascending b.  It reads only the
+//      ids; DCNR_EMB_SORT_SIDE=1 runs it on a side stream overlapped with
+//      the deep-tower backward.  (rocPRIM's radix_sort_pairs did the same in
+//      ~107 us at the bench size: three look-back-bound 8-bit passes.)
 //   3. emb_runs_short_kernel: the thread at a run's head sums runs of <= LIM
 //      entries sequentially and writes the row; emb_runs_long_kernel: the
 //      wave whose 64 positions hold the head of a longer run (popular ids,
@@ -32,7 +33,7 @@
 
 #include <cstring>
 #include <mutex>
-#include <rocprim/device/device_radix_sort.hpp>
+#include <algorithm>
 
 namespace dcnr {
 namespace {
@@ -63,26 +64,331 @@ EmbTabs make_tabs(const EmbBwdDesc& e) {
   return t;
 }
 
-int key_bits(const EmbBwdDesc& e) {
-  uint64_t total = 0;
-  for (int i = 0; i < e.n_tab; ++i) total += (uint64_t)e.rows[i];
-  int bits = 1;
-  while (bits < 32 && (1ull << bits) < total) ++bits;
-  return bits;
+// ------------------------------------------------------------ id sort
+// Stable two-level counting sort of each table's (id, sample) pairs, table t
+// landing in [t*B, (t+1)*B) of keys_s/vals_s (key = base_t + id) in
+// ascending (id, sample) order -- no global atomics, no look-back chains:
+//   level 1, by bucket = id >> sh_t (<= 4096 buckets per table):
+//     emb_hist_kernel    per (table, chunk of CH samples) bucket counts (LDS)
+//     emb_scan_kernel    per table, exclusive scan over (bucket, chunk)
+//     emb_scatter_kernel per (table, chunk): SC_W waves x CH/SC_W samples, each wave's
+//                        running bucket offsets in LDS, stable ranks inside
+//                        a 64-sample step by matching lanes (match_rank)
+//   level 2 (tables with sh_t > 0), emb_bucket_sort_kernel: one block per
+//     bucket, the same count / scan / stable scatter on id & (2^sh_t - 1).
+// Tables with <= 1024 rows (sh_t = 0) are final after level 1.
+constexpr int CH = 2048;          // samples per level-1 chunk
+constexpr int SC_W = 8;           // emb_scatter_kernel waves per block
+constexpr int SC_T = SC_W * WAVE;
+constexpr int MAXBK = 4096;       // level-1 buckets per table / level-2 bins
+constexpr int SCAN_T = 1024;
+
+struct SortTabs {
+  uint32_t base[MAX_TABLES];
+  int64_t rows[MAX_TABLES];
+  int sh[MAX_TABLES];             // level-1 bucket = id >> sh
+  int nbk[MAX_TABLES];            // level-1 buckets
+  int nbkb[MAX_TABLES];           // bits of a bucket index (<= 12)
+  int gb[MAX_TABLES];             // first global bucket of the table
+  int total_bk;                   // hist/offs are [chunk][total_bk] (chunk-major)
+};
+struct L2Map {                    // level-2 blocks -> (table, bucket)
+  int tab[MAX_TABLES];
+  int first[MAX_TABLES + 1];
+  int n;
+};
+
+int nbits64(uint64_t x) { return x ? 64 - __builtin_clzll(x) : 0; }
+
+struct SortPlan {
+  SortTabs st;
+  L2Map l2;
+  int total_bk = 0, max_bk = 1, max_low = 1, C = 0;
+  bool ok = true;
+};
+
+SortPlan make_plan(const int64_t* rows, int nt, int64_t B) {
+  SortPlan p;
+  memset(&p.st, 0, sizeof(p.st));
+  memset(&p.l2, 0, sizeof(p.l2));
+  p.C = (int)cdiv(B, CH);
+  uint32_t base = 0;
+  for (int t = 0; t < nt; ++t) {
+    const int nb = nbits64((uint64_t)(rows[t] > 0 ? rows[t] - 1 : 0));
+    const int bkb = std::max(10, nb - 12);
+    if (bkb > 12) p.ok = false;   // > 2^24 rows
+    const int sh = std::max(0, nb - bkb);
+    p.st.base[t] = base;
+    p.st.rows[t] = rows[t];
+    p.st.sh[t] = sh;
+    p.st.nbk[t] = (int)(((uint64_t)(rows[t] > 0 ? rows[t] - 1 : 0) >> sh) + 1);
+    p.st.nbkb[t] = nbits64((uint64_t)p.st.nbk[t] - 1);
+    p.st.gb[t] = p.total_bk;
+    p.total_bk += p.st.nbk[t];
+    p.max_bk = std::max(p.max_bk, p.st.nbk[t]);
+    if (sh > 0) {
+      p.l2.tab[p.l2.n] = t;
+      p.l2.first[p.l2.n + 1] = p.l2.first[p.l2.n] + p.st.nbk[t];
+      ++p.l2.n;
+      p.max_low = std::max(p.max_low, 1 << sh);
+    }
+    base += (uint32_t)rows[t];
+  }
+  p.st.total_bk = p.total_bk;
+  return p;
 }
 
-__global__ __launch_bounds__(ENT) void emb_keys_kernel(EmbTabs et, int nt, const int64_t* user,
-                                                       const int64_t* item, const int64_t* cat,
-                                                       int64_t B, uint32_t* keys, uint32_t* vals) {
-  const int64_t i = (int64_t)blockIdx.x * ENT + threadIdx.x;
-  if (i >= (int64_t)nt * B) return;
-  const int t = (int)(i / B);
-  const int64_t b = i - (int64_t)t * B;
-  int64_t id = t == 0 ? user[b] : t == 1 ? item[b] : cat[b * (nt - 2) + (t - 2)];
-  const int64_t rows = et.rows[t];
-  id = id < 0 ? 0 : (id >= rows ? rows - 1 : id);   // the forward gather's clamp
-  keys[i] = et.base[t] + (uint32_t)id;
-  vals[i] = (uint32_t)b;
+// ids[t*B + b] = clamped id of sample b in table t (the forward gather's
+// clamp): one thread per sample reads its user, item and K categorical ids
+// (contiguous), the sort kernels then read each table's ids coalesced.
+__global__ __launch_bounds__(ENT) void emb_ids_kernel(SortTabs st, int nt, const int64_t* user,
+                                                      const int64_t* item, const int64_t* cat,
+                                                      int64_t B, uint32_t* ids) {
+  const int64_t b = (int64_t)blockIdx.x * ENT + threadIdx.x;
+  if (b >= B) return;
+  for (int t = 0; t < nt; ++t) {
+    const int64_t id = t == 0 ? user[b] : t == 1 ? item[b] : cat[b * (nt - 2) + (t - 2)];
+    const int64_t rows = st.rows[t];
+    ids[(int64_t)t * B + b] = (uint32_t)(id < 0 ? 0 : (id >= rows ? rows - 1 : id));
+  }
+}
+
+// Lanes holding the same v (v < 2^nb, among `valid` lanes): this lane's rank
+// among the lower ones, the group size, and whether it is the group's
+// highest lane.  One ballot per value bit (nb <= 12): the peers mask is the
+// AND over bits of (bit set ? ballot : ~ballot) -- a fixed cost, unlike a
+// loop over the distinct values (up to 64 of them per step here).
+__device__ __forceinline__ void match_rank(uint32_t v, bool valid, int nb, int lane, int& rank,
+                                           int& cnt, bool& last) {
+  uint64_t peers = __ballot(valid);
+  for (int i = 0; i < nb; ++i) {
+    const bool bit = (v >> i) & 1u;
+    const uint64_t m = __ballot(bit);
+    peers &= bit ? m : ~m;
+  }
+  const uint64_t below = lane ? (~0ull >> (64 - lane)) : 0ull;
+  rank = __popcll(peers & below);
+  cnt = __popcll(peers);
+  last = valid && (peers >> lane) == 1ull;
+}
+
+__global__ __launch_bounds__(ENT) void emb_hist_kernel(SortTabs st, const uint32_t* ids,
+                                                       int64_t B, int C, uint32_t* hist) {
+  extern __shared__ uint32_t h[];
+  const int c = blockIdx.x, t = blockIdx.y;
+  const int nbk = st.nbk[t], sh = st.sh[t];
+  for (int i = threadIdx.x; i < nbk; i += ENT) h[i] = 0u;
+  __syncthreads();
+  const int64_t b0 = (int64_t)c * CH;
+  for (int i = threadIdx.x; i < CH; i += ENT) {
+    const int64_t b = b0 + i;
+    if (b < B) atomicAdd(&h[ids[(int64_t)t * B + b] >> sh], 1u);
+  }
+  __syncthreads();
+  uint32_t* out = hist + (int64_t)c * st.total_bk + st.gb[t];
+  for (int i = threadIdx.x; i < nbk; i += ENT) out[i] = h[i];
+}
+
+// hist[chunk][gb_t + bucket] -> t*B + exclusive prefix in (bucket, chunk)
+// order.  Thread i owns buckets i, i + SCAN_T, ...: their totals (C
+// counts each, loaded 16 at a time), a block scan of the totals, then the
+// running offsets along each bucket's chunks.
+__global__ __launch_bounds__(SCAN_T) void emb_scan_kernel(SortTabs st, int64_t B, int C,
+                                                          uint32_t* hist) {
+  constexpr int U = 16;
+  __shared__ uint32_t tot[MAXBK];
+  __shared__ uint32_t part[SCAN_T];
+  const int t = blockIdx.x, tid = threadIdx.x, nbk = st.nbk[t];
+  const int64_t TB = st.total_bk;
+  uint32_t* seg = hist + st.gb[t];
+  for (int bk = tid; bk < nbk; bk += SCAN_T) {
+    const uint32_t* row = seg + bk;   // chunk c at row[c * TB]: coalesced across threads
+    uint32_t sum = 0;
+    for (int c0 = 0; c0 < C; c0 += U) {
+      uint32_t v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = c0 + u < C ? row[(c0 + u) * TB] : 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u) sum += v[u];
+    }
+    tot[bk] = sum;
+  }
+  __syncthreads();
+  // exclusive scan of tot[0..nbk): thread-contiguous groups, then across threads
+  const int pg = (nbk + SCAN_T - 1) / SCAN_T;
+  const int ga = min(nbk, tid * pg), gz = min(nbk, ga + pg);
+  uint32_t gsum = 0;
+  for (int i = ga; i < gz; ++i) gsum += tot[i];
+  part[tid] = gsum;
+  __syncthreads();
+  for (int o = 1; o < SCAN_T; o <<= 1) {
+    const uint32_t v = tid >= o ? part[tid - o] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - gsum;
+  for (int i = ga; i < gz; ++i) {
+    const uint32_t v = tot[i];
+    tot[i] = run;
+    run += v;
+  }
+  __syncthreads();
+  for (int bk = tid; bk < nbk; bk += SCAN_T) {
+    uint32_t* row = seg + bk;
+    uint32_t r = (uint32_t)((int64_t)t * B) + tot[bk];
+    for (int c0 = 0; c0 < C; c0 += U) {
+      uint32_t v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) v[u] = c0 + u < C ? row[(c0 + u) * TB] : 0u;
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (c0 + u < C) {
+          row[(c0 + u) * TB] = r;
+          r += v[u];
+        }
+    }
+  }
+}
+
+__global__ __launch_bounds__(SC_T) void emb_scatter_kernel(SortTabs st, int nt, const uint32_t* ids,
+                                                          int64_t B, int C, const uint32_t* offs,
+                                                          uint32_t* mid_k, uint32_t* mid_v,
+                                                          uint32_t* fin_k, uint32_t* fin_v) {
+  extern __shared__ uint32_t wh[];   // [SC_W][nbk]: per-wave counts, then running offsets
+  // XCD-aware block map: every chunk of table t runs on XCD t % 8, so the
+  // scattered 4-B stores into the table's output range combine in one L2
+  const int L8 = blockIdx.x & 7, k8 = blockIdx.x >> 3, jt = k8 / C;
+  const int c = k8 - jt * C, t = L8 + 8 * jt;
+  if (t >= nt) return;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int nbk = st.nbk[t], sh = st.sh[t];
+  for (int i = threadIdx.x; i < SC_W * nbk; i += SC_T) wh[i] = 0u;
+  __syncthreads();
+  const int64_t b0 = (int64_t)c * CH + (int64_t)w * (CH / SC_W);
+  constexpr int Q = CH / SC_W / WAVE;
+  uint32_t id[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int64_t b = b0 + q * WAVE + lane;
+    id[q] = b < B ? ids[(int64_t)t * B + b] : 0u;
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    if (b0 + q * WAVE + lane < B) atomicAdd(&wh[w * nbk + (id[q] >> sh)], 1u);
+  __syncthreads();
+  {
+    constexpr int J = MAXBK / SC_T;
+    const uint32_t* orow = offs + (int64_t)c * st.total_bk + st.gb[t];
+    uint32_t ov[J];
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int i = threadIdx.x + j * SC_T;
+      ov[j] = i < nbk ? orow[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < J; ++j) {
+      const int i = threadIdx.x + j * SC_T;
+      if (i < nbk) {
+        uint32_t acc = ov[j];
+        for (int ww = 0; ww < SC_W; ++ww) {
+          const uint32_t v = wh[ww * nbk + i];
+          wh[ww * nbk + i] = acc;
+          acc += v;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  uint32_t* ok_ = sh ? mid_k : fin_k;
+  uint32_t* ov_ = sh ? mid_v : fin_v;
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
+    const int64_t b = b0 + q * WAVE + lane;
+    const bool valid = b < B;
+    const uint32_t bk = id[q] >> sh;
+    int rank, cnt;
+    bool last;
+    match_rank(bk, valid, st.nbkb[t], lane, rank, cnt, last);
+    uint32_t* slot = &wh[w * nbk + (valid ? bk : 0)];
+    const uint32_t pos = *slot + rank;
+    if (valid) {
+      ok_[pos] = st.base[t] + id[q];
+      ov_[pos] = (uint32_t)b;
+    }
+    if (last) *slot = pos - rank + cnt;
+  }
+}
+
+__global__ __launch_bounds__(ENT) void emb_bucket_sort_kernel(SortTabs st, L2Map mp, int64_t B,
+                                                              int C, const uint32_t* offs,
+                                                              const uint32_t* mid_k,
+                                                              const uint32_t* mid_v,
+                                                              uint32_t* fin_k, uint32_t* fin_v) {
+  extern __shared__ uint32_t wh[];   // [4][nlow]
+  __shared__ uint32_t part[ENT];
+  int j = 0;
+  while (j + 1 < mp.n && (int)blockIdx.x >= mp.first[j + 1]) ++j;
+  const int t = mp.tab[j], bk = (int)blockIdx.x - mp.first[j];
+  const int sh = st.sh[t], nlow = 1 << sh, nbk = st.nbk[t];
+  const uint32_t mask = (uint32_t)nlow - 1u, base = st.base[t];
+  const int64_t start = offs[st.gb[t] + bk];   // chunk 0 row of offs
+  const int64_t end = bk + 1 < nbk ? (int64_t)offs[st.gb[t] + bk + 1]
+                                   : (int64_t)(t + 1) * B;
+  const int64_t ne = end - start;
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  if (ne <= 1) {
+    if (ne == 1 && tid == 0) { fin_k[start] = mid_k[start]; fin_v[start] = mid_v[start]; }
+    return;
+  }
+  const int64_t per = (ne + 3) / 4;
+  const int64_t a = min(end, start + w * per), z = min(end, a + per);
+  for (int i = tid; i < 4 * nlow; i += ENT) wh[i] = 0u;
+  __syncthreads();
+  for (int64_t p = a + lane; p < z; p += WAVE) atomicAdd(&wh[w * nlow + ((mid_k[p] - base) & mask)], 1u);
+  __syncthreads();
+  // exclusive scan over (low bin, wave): each thread a contiguous range of bins
+  const int pl = (nlow + ENT - 1) / ENT;
+  const int la = min(nlow, tid * pl), lz = min(nlow, la + pl);
+  uint32_t sum = 0;
+  for (int l = la; l < lz; ++l)
+    for (int ww = 0; ww < 4; ++ww) sum += wh[ww * nlow + l];
+  part[tid] = sum;
+  __syncthreads();
+  for (int o = 1; o < ENT; o <<= 1) {
+    const uint32_t v = tid >= o ? part[tid - o] : 0u;
+    __syncthreads();
+    part[tid] += v;
+    __syncthreads();
+  }
+  uint32_t run = part[tid] - sum;
+  for (int l = la; l < lz; ++l)
+    for (int ww = 0; ww < 4; ++ww) {
+      const uint32_t v = wh[ww * nlow + l];
+      wh[ww * nlow + l] = run;
+      run += v;
+    }
+  __syncthreads();
+  // stable scatter, 64 entries per step, the next step's loads in flight
+  int64_t p = a + lane;
+  uint32_t kn = p < z ? mid_k[p] : 0u, vn = p < z ? mid_v[p] : 0u;
+  for (int64_t p0 = a; p0 < z; p0 += WAVE) {
+    const bool valid = p0 + lane < z;
+    const uint32_t key = kn, v = vn;
+    p = p0 + WAVE + lane;
+    if (p0 + WAVE < z) { kn = p < z ? mid_k[p] : 0u; vn = p < z ? mid_v[p] : 0u; }
+    const uint32_t low = (key - base) & mask;
+    int rank, cnt;
+    bool last;
+    match_rank(low, valid, sh, lane, rank, cnt, last);
+    uint32_t* slot = &wh[w * nlow + (valid ? low : 0)];
+    const uint32_t pos = *slot + rank;
+    if (valid) {
+      fin_k[start + pos] = key;
+      fin_v[start + pos] = v;
+    }
+    if (last) *slot = pos - rank + cnt;
+  }
 }
 
 template <int VEC> struct Vec;
@@ -259,10 +565,9 @@ bool vec4_ok(const EmbBwdDesc& e, const float* dx0) {
 
 }  // namespace
 
-size_t emb_sort_tmp_bytes(int64_t n) {
-  // rocPRIM's own double buffer (8 B per pair) plus its histograms and
-  // look-back state; dcnr_backward checks the library's exact figure
-  return (size_t)n * 8 + (size_t)n / 4 + ((size_t)1 << 20);
+size_t emb_sort_tmp_bytes(const int64_t* rows, int nt, int64_t B) {
+  const SortPlan p = make_plan(rows, nt, B);
+  return (size_t)p.total_bk * (size_t)std::max(p.C, 1) * 4;
 }
 
 dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* item,
@@ -271,25 +576,49 @@ dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* it
   if (n <= 0) return DCNR_OK;
   uint64_t total = 0;
   for (int i = 0; i < e.n_tab; ++i) total += (uint64_t)e.rows[i];
-  if (total >= (1ull << 32) || B >= (1ll << 32) || n >= (1ll << 31)) {
-    set_error("embedding backward: %llu table rows / B=%lld beyond 32-bit keys",
-              (unsigned long long)total, (long long)B);
+  const SortPlan p = make_plan(e.rows, e.n_tab, B);
+  if (!p.ok || total >= (1ull << 32) || n >= (1ll << 32)) {
+    set_error("embedding backward: tables of > 2^24 rows, %llu rows in all or %lld ids "
+              "unsupported", (unsigned long long)total, (long long)n);
     return DCNR_UNSUPPORTED_SHAPE;
   }
-  const EmbTabs et = make_tabs(e);
-  hipLaunchKernelGGL(emb_keys_kernel, dim3((unsigned)cdiv(n, ENT)), dim3(ENT), 0, s, et, e.n_tab,
-                     user, item, cat, B, sb.keys, sb.vals);
-  DCNR_LAUNCH_CHECK();
-  size_t need = 0;
-  DCNR_HIP(rocprim::radix_sort_pairs(nullptr, need, sb.keys, sb.keys_s, sb.vals, sb.vals_s,
-                                     (size_t)n, 0, key_bits(e), s));
-  if (need > sb.tmp_bytes) {
-    set_error("embedding backward: sort scratch %zu > reserved %zu", need, sb.tmp_bytes);
+  if ((size_t)p.total_bk * p.C * 4 > sb.tmp_bytes) {
+    set_error("embedding backward: sort scratch too small");
     return DCNR_WORKSPACE_TOO_SMALL;
   }
-  size_t have = sb.tmp_bytes;
-  DCNR_HIP(rocprim::radix_sort_pairs(sb.tmp, have, sb.keys, sb.keys_s, sb.vals, sb.vals_s,
-                                     (size_t)n, 0, key_bits(e), s));
+  uint32_t* hist = (uint32_t*)sb.tmp;
+  static size_t attr_bk = 0, attr_low = 0;   // dynamic LDS above the 64 KiB default
+  const size_t lds_bk = (size_t)SC_W * p.max_bk * 4, lds_low = (size_t)4 * p.max_low * 4;
+  if (lds_bk > 65536 && lds_bk > attr_bk) {
+    DCNR_HIP(hipFuncSetAttribute((const void*)emb_scatter_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bk));
+    attr_bk = lds_bk;
+  }
+  if (lds_low + ENT * 4 > 65536 && lds_low > attr_low) {
+    DCNR_HIP(hipFuncSetAttribute((const void*)emb_bucket_sort_kernel,
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_low));
+    attr_low = lds_low;
+  }
+  const dim3 gc((unsigned)p.C, (unsigned)e.n_tab);
+  hipLaunchKernelGGL(emb_ids_kernel, dim3((unsigned)cdiv(B, ENT)), dim3(ENT), 0, s, p.st,
+                     e.n_tab, user, item, cat, B, sb.ids);
+  DCNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(emb_hist_kernel, gc, dim3(ENT), (size_t)p.max_bk * 4, s, p.st, sb.ids, B,
+                     p.C, hist);
+  DCNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(emb_scan_kernel, dim3((unsigned)e.n_tab), dim3(SCAN_T), 0, s, p.st, B, p.C,
+                     hist);
+  DCNR_LAUNCH_CHECK();
+  hipLaunchKernelGGL(emb_scatter_kernel, dim3((unsigned)(8 * cdiv(e.n_tab, 8) * p.C)), dim3(SC_T),
+                     lds_bk, s, p.st, e.n_tab, sb.ids, B, p.C, hist, sb.keys, sb.vals,
+                     sb.keys_s, sb.vals_s);
+  DCNR_LAUNCH_CHECK();
+  if (p.l2.n > 0) {
+    hipLaunchKernelGGL(emb_bucket_sort_kernel, dim3((unsigned)p.l2.first[p.l2.n]), dim3(ENT),
+                       lds_low, s, p.st, p.l2, B, p.C, hist, sb.keys, sb.vals, sb.keys_s,
+                       sb.vals_s);
+    DCNR_LAUNCH_CHECK();
+  }
   return DCNR_OK;
 }
 
