@@ -238,12 +238,14 @@ struct Layout {
   // per-block backward buffers: all alias G/dt2/du/da/a1 unless
   // DCNR_FLAG_KEEP_INTERMEDIATES gives each block its own
   void* duk[MAX_RES]; void* dt2k[MAX_RES]; void* dak[MAX_RES]; void* dt1k[MAX_RES];
-  float* dx0; float* dx0t;   // dx0t: total dx0 of the tables' columns, table-major
-  float* slab; int64_t slab_elems; float* cpart; size_t cpart_elems;
+  float* dx0;                 // deep part of dL/dx0, [B][Dq] (Dq = Dp rounded up to 32)
+  float* slab; int64_t slab_elems;
+  float* sc;                  // forward -> backward cross scalars [B][2L+1]
+  float* xcoef; float* xalpha;  // [B][L+1] each (cross_bwd.hip)
+  void* cscratch; size_t cscratch_bytes;
   // 1-bit keep masks for the backward GEMM epilogues (bf16, Hp % 32 == 0):
   // mask_a1[j] = [a1_j != 0], mask_h[j] = [h_j > 0] (j >= 1)
   uint8_t* mask_a1[MAX_RES]; uint8_t* mask_h[MAX_RES + 1];
-  float* cred2; size_t cred2_elems;             // cross partial second stage
   EmbSortBufs emb;                              // deterministic embedding backward
   double* bce_part;
   size_t total;
@@ -252,6 +254,9 @@ struct Layout {
 // the backward GEMM epilogues read 1-bit keep masks (bf16 path, mask rows of
 // whole 32-bit words) instead of the bf16 activations
 bool masks_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && d.Hp % 32 == 0; }
+// leading dimension of the deep dx0: 32-float (128-B) rows so that each
+// embedding table's segment of a row is line-aligned for embed_bwd.hip
+int dq_of(const Dims& d) { return (int)rup(d.Dp, 32); }
 bool keep_of(const dcnr_model_desc* desc) { return (desc->flags & DCNR_FLAG_KEEP_INTERMEDIATES) != 0; }
 
 Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = false) {
@@ -310,18 +315,18 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
     L.dt2 = b.take(act);
     L.du = b.take(act);
     L.da = b.take(act);
-    L.dx0 = (float*)b.take((size_t)B * d.Dp * 4);
-    L.dx0t = (float*)b.take((size_t)B * d.Dp * 4);   // table-major, tables' columns only
+    L.dx0 = (float*)b.take((size_t)B * dq_of(d) * 4);
     // split-K slabs: the fp32 path adapts its splits to 64; the bf16 kernel's
     // split count depends on the tile count (narrow H -> more splits)
     L.slab_elems = std::max<int64_t>({(int64_t)64 * d.Hp * std::max(d.Hp, d.Dp),
                                       (int64_t)gemm_dw_splits(d.Hp, d.Hp, B) * d.Hp * d.Hp,
                                       (int64_t)gemm_dw_splits(d.Hp, d.Dp, B) * d.Hp * d.Dp});
     L.slab = (float*)b.take((size_t)L.slab_elems * 4);
-    L.cpart_elems = cross_bwd_part_elems(d.D, d.L);
-    L.cpart = (float*)b.take(L.cpart_elems * 4);
-    L.cred2_elems = cross_red2_elems(d.D, d.L);
-    L.cred2 = (float*)b.take(L.cred2_elems * 4);
+    L.sc = (float*)b.take((size_t)B * (2 * d.L + 1) * 4);
+    L.xcoef = (float*)b.take((size_t)B * (d.L + 1) * 4);
+    L.xalpha = (float*)b.take((size_t)B * (d.L + 1) * 4);
+    L.cscratch_bytes = cross_bwd_scratch_bytes(d.D, d.L, B);
+    L.cscratch = b.take(L.cscratch_bytes);
     {
       const int64_t n = (int64_t)(2 + d.K) * B;
       L.emb.ids = (uint32_t*)b.take((size_t)n * 4);
@@ -745,7 +750,8 @@ dcnr_status dcnr_workspace_offset(const dcnr_model_desc* desc, int64_t B, int mo
     case DCNR_WS_G: if (train) p = L.G; break;
     case DCNR_WS_DX0: if (train) p = L.dx0; break;
     case DCNR_WS_ZC: p = L.zc; break;
-    case DCNR_WS_DX0_TOTAL: if (train) p = L.dx0t; break;
+    case DCNR_WS_XCOEF: if (train) p = L.xcoef; break;
+    case DCNR_WS_SC: if (train) p = L.sc; break;
   }
   *offset = p ? (int64_t)((const char*)p - base) : -1;
   return DCNR_OK;
@@ -811,7 +817,7 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   GatherDesc g = make_gather(d, P, desc->n_num);
   CrossParams cp = make_cross(d, P);
   {
-    const GcOut o{nullptr, L.x0, L.zc, 0, d.Dp};
+    const GcOut o{nullptr, L.x0, L.zc, 0, d.Dp, train ? L.sc : nullptr};
     TRYB(DCNR_K_GATHER_CROSS, (double)B * (gather_row_b(d, desc->n_num) + (double)d.Dp * d.es + 4.0),
          gather_cross_out(g, cp, user_ids, item_ids, cat_features, num_features, B, o,
                           d.prec == DCNR_PREC_BF16, L.err, check, s));
@@ -1011,30 +1017,32 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   {
     GemmArgs g;
     memset(&g, 0, sizeof(g));
-    g.A = L.G; g.lda = Hp; g.B = L.W0t; g.ldb = Hp; g.C = L.dx0; g.ldc = d.Dp; g.out_f32 = 1;
+    g.A = L.G; g.lda = Hp; g.B = L.W0t; g.ldb = Hp; g.C = L.dx0; g.ldc = dq_of(d); g.out_f32 = 1;
     g.M = B; g.N = d.Dp; g.K = Hp; g.k_per_split = Hp;
     TRYB(DCNR_K_GEMM_DX, act_b(d, B) + 4.0 * B * d.Dp + w_b(d, d.Dp), gemm_nn(d.prec, EPI_STORE, g, 1, s));
   }
-  // ---- cross stack + head bias + total dx0 rows; embedding backward part 2
-  CrossBwdParams cb;
-  memset(&cb, 0, sizeof(cb));
-  cb.cp = make_cross(d, P);
-  for (int l = 0; l < d.L; ++l) { cb.dw[l] = Gr.cw[l]; cb.db[l] = Gr.cb[l]; }
-  cb.dwf_cross = Gr.wf + H;
-  cb.dbf = Gr.bf;
-  for (int t = 0; t < 2 + d.K; ++t) cb.emb_grad[t] = Gr.tab[t];
-  cb.dx0_tot = L.dx0t;
-  CrossBwdScratch cws{L.cpart, L.cpart_elems, L.cred2, L.cred2_elems, L.red_cnt, CNT_SLOTS};
-  // re-gather + dx0 read + total dx0 write + dz read
+  // ---- cross network + head bias (low-rank form, from the forward's
+  // per-sample scalars and the stored x0; cross_bwd.hip)
+  CrossGrads cg;
+  memset(&cg, 0, sizeof(cg));
+  for (int l = 0; l < d.L; ++l) { cg.dw[l] = Gr.cw[l]; cg.db[l] = Gr.cb[l]; }
+  cg.dwf_cross = Gr.wf + H;
+  cg.dbf = Gr.bf;
+  const CrossParams cpx = make_cross(d, P);
+  TRYB(DCNR_K_CROSS_BWD, (double)B * (4.0 * (2 * d.L + 1) + 4.0 + 8.0 * (d.L + 1)) +
+                             (double)B * d.Dp * d.es,
+       cross_backward(cpx, d.D, L.sc, dz, L.x0, d.prec == DCNR_PREC_BF16, d.Dp, B, cg, L.xcoef,
+                      L.xalpha, L.cscratch, L.cscratch_bytes, accumulate, s));
+  // ---- embedding backward part 2: sorted (table row, sample) pairs -> per row
+  // sum of the deep dx0 segments + sum of the cross coefficients
   double ew = 0;
   for (int t = 0; t < 2 + d.K; ++t) ew += d.widths[t];
-  TRYB(DCNR_K_CROSS_BWD, (double)B * (gather_row_b(d, desc->n_num) + 4.0 * d.Dp + 4.0 + 4.0 * ew),
-       cross_bwd_scatter(g, cb, user_ids, item_ids, cat_features, num_features, dz, B, L.dx0, d.Dp,
-                        cws, accumulate, s));
-  // sorted (table row, sample) pairs + the dx0 entries they name -> grad rows
+  eb.nv = d.L + 1;
+  for (int l = 0; l < d.L; ++l) eb.V[l] = cpx.w[l];
+  eb.V[d.L] = cpx.wf_cross;
   TRY(sj.join(s));
-  TRYB(DCNR_K_EMB_SUM, (double)B * (4.0 * ew + 8.0 * g.n_tab),
-       emb_segment_sum(eb, L.emb, B, L.dx0t, accumulate, s));
+  TRYB(DCNR_K_EMB_SUM, (double)B * (4.0 * ew + (8.0 + 4.0 * (d.L + 1)) * g.n_tab),
+       emb_segment_sum(eb, L.emb, B, L.dx0, dq_of(d), L.xcoef, accumulate, s));
   return DCNR_OK;
 }
 

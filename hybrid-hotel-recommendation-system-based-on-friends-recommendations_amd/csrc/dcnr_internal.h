@@ -392,42 +392,37 @@ struct GcOut {
   void* x0;       // [B][ld_x0] fp32 or bf16, or null
   float* zc;      // [B] w_f[H:] . x_L, or null
   int ld_cross, ld_x0;
+  float* sc;      // [B][2L+1] per-sample cross scalars for the backward, or null:
+                  // s_l = x_l . w_l (l < L), u_m = x_0 . w_m (m < L), u_f = x_0 . w_f[H:]
 };
 dcnr_status gather_cross_out(const GatherDesc& g, const CrossParams& cp, const int64_t* user,
                              const int64_t* item, const int64_t* cat, const float* num, int64_t B,
                              const GcOut& o, int x0_bf16, int* err, int check, hipStream_t s);
 
-struct CrossBwdParams {
-  CrossParams cp;
-  float* dw[8]; float* db[8];      // grads (final)
-  float* dwf_cross;                // grad final_linear.weight + H
-  float* dbf;                      // grad final_linear.bias
-  float* emb_grad[MAX_TABLES];     // dense embedding grads (atomic scatter-add) ...
-  float* dx0_tot;                  // ... or, if set, the total dx0 of the table columns
-                                   // stored here table-major (table t: [B][w_t] at
-                                   // B * off_t) for embed_bwd.hip
+// low-rank cross backward (cross_bwd.hip)
+struct CrossGrads {
+  float* dw[8]; float* db[8];      // cross_network.{l}.w.weight / .b grads [D]
+  float* dwf_cross;                // grad final_linear.weight + H  [D]
+  float* dbf;                      // grad final_linear.bias        [1]
 };
-struct CrossBwdScratch {
-  float* part; size_t part_elems;  // per-block partials
-  float* red2; size_t red2_elems;  // [RED_G][stride] second-stage sums
-  int* counters; int n_counters;   // hand-off counters, zero at rest
-};
-constexpr int64_t BWD_BLOCKS = 2048;
-dcnr_status cross_bwd_scatter(const GatherDesc& g, const CrossBwdParams& p,
-                              const int64_t* user, const int64_t* item, const int64_t* cat,
-                              const float* num, const float* dz, int64_t B,
-                              const float* dx0_deep, int ld_dx, const CrossBwdScratch& ws,
-                              int accumulate, hipStream_t s);
+size_t cross_bwd_scratch_bytes(int D, int L, int64_t B);
+// sc: the forward's GcOut::sc; x0: the forward's stored x0 ([B][ldx], bf16 if
+// x0_bf16); coef, alpha: [B][L+1] outputs (coef = dx0_cross coefficients on
+// w_0..w_{L-1}, w_f[H:], read by emb_segment_sum)
+dcnr_status cross_backward(const CrossParams& cp, int D, const float* sc, const float* dz,
+                           const void* x0, int x0_bf16, int ldx, int64_t B, const CrossGrads& gr,
+                           float* coef, float* alpha, void* scratch, size_t scratch_bytes,
+                           int accumulate, hipStream_t s);
 
-size_t cross_bwd_part_elems(int D, int L);
 // deterministic embedding gradients (embed_bwd.hip)
 struct EmbBwdDesc {
   float* grad[MAX_TABLES];       // dense grads, [rows][width] each
   int64_t rows[MAX_TABLES];
   int width[MAX_TABLES];
-  int off[MAX_TABLES];           // first x0 column of the table; its dx0 block [B][w]
-                                 // starts at B * off in the table-major dx0_total
+  int off[MAX_TABLES];           // first x0 column of the table
   int n_tab;
+  const float* V[8];             // dx0_cross = sum_k coef[b][k] V[k] (w_0..w_{L-1}, w_f[H:])
+  int nv;                        // L + 1
 };
 struct EmbSortBufs {
   uint32_t *ids;                 // [n_tab * B] clamped ids, table-major
@@ -438,12 +433,13 @@ struct EmbSortBufs {
 size_t emb_sort_tmp_bytes(const int64_t* rows, int n_tab, int64_t B);
 dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* item,
                      const int64_t* cat, int64_t B, const EmbSortBufs& sb, hipStream_t s);
+// grad row r of table t = sum over its samples of dx0_deep[b][off_t:off_t+w_t]
+// + sum_k (sum over its samples of coef[b][k]) V[k][off_t:off_t+w_t]
 dcnr_status emb_segment_sum(const EmbBwdDesc& e, const EmbSortBufs& sb, int64_t B,
-                            const float* dx0_total, int accumulate, hipStream_t s);
+                            const float* dx0_deep, int ld, const float* coef, int accumulate,
+                            hipStream_t s);
 dcnr_status emb_side_stream(hipStream_t* out);
 
-size_t cross_red2_elems(int D, int L);
-int cross_red_groups(int D, int L);
 
 // Column reductions: partial sums per row-chunk, part[nchunks][NK][N] (f32),
 // reduced in fixed order into sums[3][N] (f64; components >= NK zeroed) with

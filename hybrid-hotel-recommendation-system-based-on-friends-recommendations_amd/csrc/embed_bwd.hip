@@ -24,11 +24,11 @@
 //      lists: a device-scope atomic per long run (12000 at the bench size)
 //      serialised at memory and cost ~100 us.
 //
-// Step 3 reads dx0_total (written by the cross backward: cross part + deep
-// part of each table's columns, table-major so that an entry's w_t floats are
-// one aligned segment -- in the row-major [B][Dp] dx0 three in four 128-B
-// segments straddled two lines) once per entry: 4*w_t + 8 bytes per
-// (sample, table) + one row write per distinct id.
+// Step 3 reads, per (sample, table) entry, the table's segment of the deep
+// dx0 (rows of Dq = 32-float multiples, so a 32-wide segment is one aligned
+// 128-B line) and the sample's L+1 cross coefficients (cross_bwd.hip), and
+// writes row = deep sum + sum_k coefficient sum_k V_k once per distinct id:
+// 4*w_t + 4*(L+1) + 8 bytes per entry.
 #include "dcnr_internal.h"
 
 #include <cstring>
@@ -47,6 +47,7 @@ struct EmbTabs {
   int64_t rows[MAX_TABLES];
   int width[MAX_TABLES];
   int off[MAX_TABLES];
+  const float* V[8];   // dx0_cross basis (w_0..w_{L-1}, w_f[H:]), indexed by x0 column
 };
 
 EmbTabs make_tabs(const EmbBwdDesc& e) {
@@ -61,6 +62,7 @@ EmbTabs make_tabs(const EmbBwdDesc& e) {
     t.off[i] = e.off[i];
     base += (uint32_t)e.rows[i];
   }
+  for (int k = 0; k < e.nv && k < 8; ++k) t.V[k] = e.V[k];
   return t;
 }
 
@@ -394,6 +396,12 @@ __global__ __launch_bounds__(ENT) void emb_bucket_sort_kernel(SortTabs st, L2Map
 template <int VEC> struct Vec;
 template <> struct Vec<1> {
   typedef float T;
+  // a + c * v rounded twice (never contracted to an fma: the test restates it)
+  static __device__ __forceinline__ T axpy(T a, float c, T v) {
+#pragma clang fp contract(off)
+    const T m = c * v;
+    return a + m;
+  }
   static __device__ __forceinline__ T ld(const float* p) { return *p; }
   static __device__ __forceinline__ void st(float* p, T v) { *p = v; }
   static __device__ __forceinline__ T zero() { return 0.f; }
@@ -401,6 +409,11 @@ template <> struct Vec<1> {
 };
 template <> struct Vec<4> {
   typedef f32x4 T;
+  static __device__ __forceinline__ T axpy(T a, float c, T v) {
+#pragma clang fp contract(off)
+    const T m = c * v;
+    return a + m;
+  }
   static __device__ __forceinline__ T ld(const float* p) { return *reinterpret_cast<const T*>(p); }
   static __device__ __forceinline__ void st(float* p, T v) { *reinterpret_cast<T*>(p) = v; }
   static __device__ __forceinline__ T zero() { return T{0.f, 0.f, 0.f, 0.f}; }
@@ -410,19 +423,22 @@ template <> struct Vec<4> {
 };
 
 // One thread per sorted position; the head of a run of <= LIM entries sums
-// it in ascending sample order.  Latency, not bandwidth, bounds this kernel
-// (a few KB per wave, scattered rows), so no load waits on another it does
-// not depend on: the run's keys and samples are loaded together, and its dx0
-// rows EG entries at a time (UNR column groups of VEC per pass).
-template <int VEC>
+// it in ascending sample order: the deep dx0 segments and the NV cross
+// coefficients, then row = deep + sum_k csum_k V_k.  Latency, not bandwidth,
+// bounds this kernel (a few KB per wave, scattered rows), so no load waits
+// on another it does not depend on: the run's keys and samples are loaded
+// together, and its dx0 rows EG entries at a time (UNR column groups of VEC
+// per pass).
+template <int VEC, int NV>
 __global__ __launch_bounds__(ENT) void emb_runs_short_kernel(EmbTabs et, int nt, int64_t B,
                                                              const uint32_t* ks,
                                                              const uint32_t* vs,
-                                                             const float* dx0, int accumulate) {
+                                                             const float* dx0, int ld,
+                                                             const float* coef, int accumulate) {
   typedef Vec<VEC> V;
   typedef typename V::T T;
   constexpr int UNR = 16 / VEC;   // 16 columns per pass
-  constexpr int EG = 4;           // entries whose loads are in flight together
+  constexpr int EG = 2;           // entries whose loads are in flight together
   const int64_t i = (int64_t)blockIdx.x * ENT + threadIdx.x;
   if (i >= (int64_t)nt * B) return;
   const int t = (int)(i / B);
@@ -439,8 +455,26 @@ __global__ __launch_bounds__(ENT) void emb_runs_short_kernel(EmbTabs et, int nt,
   uint32_t smp[LIM];
 #pragma unroll
   for (int q = 0; q < LIM; ++q) smp[q] = q < len ? vs[i + q] : 0u;
+  // cross coefficients, summed in entry order
+  float csum[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) csum[v] = 0.f;
+#pragma unroll
+  for (int q0 = 0; q0 < LIM; q0 += EG) {
+    if (q0 >= len) break;
+    float cf[EG][NV];
+#pragma unroll
+    for (int q = 0; q < EG; ++q)
+#pragma unroll
+      for (int v = 0; v < NV; ++v) cf[q][v] = q0 + q < len ? coef[(int64_t)smp[q0 + q] * NV + v] : 0.f;
+#pragma unroll
+    for (int q = 0; q < EG; ++q)
+      if (q0 + q < len)
+#pragma unroll
+        for (int v = 0; v < NV; ++v) csum[v] += cf[q][v];
+  }
   const int w = et.width[t];
-  const float* src = dx0 + B * et.off[t];   // table t's [B][w] block
+  const float* src = dx0 + et.off[t];
   float* dst = et.grad[t] + (int64_t)(k - et.base[t]) * w;
   for (int c = 0; c < w; c += UNR * VEC) {
     T acc[UNR];
@@ -452,7 +486,7 @@ __global__ __launch_bounds__(ENT) void emb_runs_short_kernel(EmbTabs et, int nt,
       T x[EG][UNR];
 #pragma unroll
       for (int q = 0; q < EG; ++q) {
-        const float* row = src + (int64_t)smp[q0 + q] * w + c;
+        const float* row = src + (int64_t)smp[q0 + q] * ld + c;
 #pragma unroll
         for (int u = 0; u < UNR; ++u)
           x[q][u] = (q0 + q < len && c + u * VEC < w) ? V::ld(row + u * VEC) : V::zero();
@@ -466,8 +500,12 @@ __global__ __launch_bounds__(ENT) void emb_runs_short_kernel(EmbTabs et, int nt,
 #pragma unroll
     for (int u = 0; u < UNR; ++u)
       if (c + u * VEC < w) {
+        const int col = et.off[t] + c + u * VEC;
+        T r = acc[u];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) r = V::axpy(r, csum[v], V::ld(et.V[v] + col));
         float* p = dst + c + u * VEC;
-        V::st(p, accumulate ? V::ld(p) + acc[u] : acc[u]);
+        V::st(p, accumulate ? V::ld(p) + r : r);
       }
   }
 }
@@ -476,14 +514,19 @@ __global__ __launch_bounds__(ENT) void emb_runs_short_kernel(EmbTabs et, int nt,
 // p+L's key and sample (coalesced loads, the next block's issued before this
 // block's dx0 rows), the column groups of VEC sit across lanes and the
 // block's entries across the remaining S = 64/Gb lane slots (slot s takes
-// entries s, s+S, ... of every block, summing them in ascending order),
-// slots added in ascending order at the end.  The wave owning the run's
-// head position (64 positions per wave) reduces it.
-template <int VEC>
+// entries s, s+S, ... of every block, summing their deep segments and cross
+// coefficients in ascending order), slots added in ascending order, then
+// row = deep + sum_k csum_k V_k.  The wave owning the run's head position
+// (64 positions per wave) reduces it.  SPLIT (every column block has
+// Gb >= NV groups): lane (slot, cg < NV) sums coefficient cg of its slot's
+// entries, instead of every lane summing all NV (fewer loads and registers;
+// same order, same result).
+template <int VEC, int NV, bool SPLIT>
 __global__ __launch_bounds__(ENT) void emb_runs_long_kernel(EmbTabs et, int64_t B, int64_t n,
                                                             const uint32_t* ks,
                                                             const uint32_t* vs,
-                                                            const float* dx0, int accumulate) {
+                                                            const float* dx0, int ld,
+                                                            const float* coef, int accumulate) {
   typedef Vec<VEC> V;
   typedef typename V::T T;
   constexpr int QMAX = 8;   // entries per slot per block held in flight (S >= 8)
@@ -506,7 +549,7 @@ __global__ __launch_bounds__(ENT) void emb_runs_long_kernel(EmbTabs et, int64_t 
     const int t = (int)(i / B);
     const int64_t t1 = (int64_t)(t + 1) * B;
     const int w = et.width[t], G = w / VEC;
-    const float* src = dx0 + B * et.off[t];   // table t's [B][w] block
+    const float* src = dx0 + et.off[t];
     float* dst = et.grad[t] + (int64_t)(k - et.base[t]) * w;
     for (int cb = 0; cb < G; cb += WAVE) {
       const int Gb = G - cb < WAVE ? G - cb : WAVE;
@@ -514,6 +557,9 @@ __global__ __launch_bounds__(ENT) void emb_runs_long_kernel(EmbTabs et, int64_t 
       const int col = (cb + cg) * VEC;
       const bool act = slot < S;
       T acc = V::zero();
+      float csum[SPLIT ? 1 : NV];
+#pragma unroll
+      for (int v = 0; v < (SPLIT ? 1 : NV); ++v) csum[v] = 0.f;
       int64_t p = i;
       uint32_t kn = p + lane < t1 ? ks[p + lane] : ~0u;
       uint32_t sn = p + lane < t1 ? vs[p + lane] : 0u;
@@ -525,41 +571,72 @@ __global__ __launch_bounds__(ENT) void emb_runs_long_kernel(EmbTabs et, int64_t 
           kn = pn + lane < t1 ? ks[pn + lane] : ~0u;
           sn = pn + lane < t1 ? vs[pn + lane] : 0u;
         }
-        T x[QMAX];
+        for (int q0 = 0; S * q0 < WAVE; q0 += QMAX) {   // uniform trip count
+          T x[QMAX];
+          float cf[QMAX][SPLIT ? 1 : NV];
 #pragma unroll
-        for (int q = 0; q < QMAX; ++q) {
-          const int j = slot + S * q;
-          const int b = __shfl(smp, j & 63);
-          x[q] = (act && j < nb) ? V::ld(src + (int64_t)b * w + col) : V::zero();
-        }
+          for (int q = 0; q < QMAX; ++q) {
+            const int j = slot + S * (q0 + q);
+            const int b = __shfl(smp, j & 63);
+            const bool ok = act && j < nb;
+            x[q] = ok ? V::ld(src + (int64_t)b * ld + col) : V::zero();
+            if constexpr (SPLIT)
+              cf[q][0] = ok && cg < NV ? coef[(int64_t)b * NV + cg] : 0.f;
+            else
 #pragma unroll
-        for (int q = 0; q < QMAX; ++q)
-          if (act && slot + S * q < nb) acc += x[q];
-        for (int q = QMAX; S * q < WAVE; ++q) {   // S < 8 only; uniform trip count
-          const int j = slot + S * q;
-          const int b = __shfl(smp, j & 63);
-          if (act && j < nb) acc += V::ld(src + (int64_t)b * w + col);
+              for (int v = 0; v < NV; ++v) cf[q][v] = ok ? coef[(int64_t)b * NV + v] : 0.f;
+          }
+#pragma unroll
+          for (int q = 0; q < QMAX; ++q)
+            if (act && slot + S * (q0 + q) < nb) {
+              acc += x[q];
+#pragma unroll
+              for (int v = 0; v < (SPLIT ? 1 : NV); ++v) csum[v] += cf[q][v];
+            }
         }
         if (nb < WAVE) break;
         p = pn;
       }
       T tot = acc;
+      constexpr int NC = SPLIT ? 1 : NV;
+      float ctot[NV];
+#pragma unroll
+      for (int v = 0; v < NC; ++v) ctot[v] = csum[v];
       for (int s = 1; s < S; ++s) {   // wave-uniform trip count
-        const T v = V::shfl(acc, (s * Gb + cg) & 63);
-        if (slot == 0) tot += v;
+        const int src_l = (s * Gb + cg) & 63;
+        const T o = V::shfl(acc, src_l);
+        float oc[NC];
+#pragma unroll
+        for (int v = 0; v < NC; ++v) oc[v] = __shfl(csum[v], src_l);
+        if (slot == 0) {
+          tot += o;
+#pragma unroll
+          for (int v = 0; v < NC; ++v) ctot[v] += oc[v];
+        }
+      }
+      if constexpr (SPLIT) {   // coefficient v's total sits in lane v (slot 0, cg v)
+        const float mine = ctot[0];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) ctot[v] = __shfl(mine, v);
       }
       if (slot == 0) {
+        const int xc = et.off[t] + col;
+        T r = tot;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) r = V::axpy(r, ctot[v], V::ld(et.V[v] + xc));
         float* q = dst + col;
-        V::st(q, accumulate ? V::ld(q) + tot : tot);
+        V::st(q, accumulate ? V::ld(q) + r : r);
       }
     }
   }
 }
 
-bool vec4_ok(const EmbBwdDesc& e, const float* dx0) {
-  if ((uintptr_t)dx0 & 15) return false;
+bool vec4_ok(const EmbBwdDesc& e, const float* dx0, int ld) {
+  if (((uintptr_t)dx0 & 15) || ld % 4) return false;
   for (int t = 0; t < e.n_tab; ++t)
     if (e.width[t] % 4 || e.off[t] % 4 || ((uintptr_t)e.grad[t] & 15)) return false;
+  for (int k = 0; k < e.nv; ++k)
+    if ((uintptr_t)e.V[k] & 15) return false;
   return true;
 }
 
@@ -622,25 +699,55 @@ dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* it
   return DCNR_OK;
 }
 
+namespace {
+
+template <int VEC, int NV>
+void launch_sums(const EmbTabs& et, int nt, int64_t B, const EmbSortBufs& sb, const float* dx0,
+                 int ld, const float* coef, int accumulate, hipStream_t s) {
+  const int64_t n = (int64_t)nt * B;
+  const dim3 gs((unsigned)cdiv(n, ENT));
+  hipLaunchKernelGGL((emb_runs_short_kernel<VEC, NV>), gs, dim3(ENT), 0, s, et, nt, B, sb.keys_s,
+                     sb.vals_s, dx0, ld, coef, accumulate);
+  bool split = true;   // every column block of every table has >= NV groups
+  for (int t = 0; t < nt; ++t) {
+    const int G = et.width[t] / VEC, last = G % WAVE;
+    if ((G < WAVE && G < NV) || (G >= WAVE && last != 0 && last < NV)) split = false;
+  }
+  if (split)
+    hipLaunchKernelGGL((emb_runs_long_kernel<VEC, NV, true>), gs, dim3(ENT), 0, s, et, B, n,
+                       sb.keys_s, sb.vals_s, dx0, ld, coef, accumulate);
+  else
+    hipLaunchKernelGGL((emb_runs_long_kernel<VEC, NV, false>), gs, dim3(ENT), 0, s, et, B, n,
+                       sb.keys_s, sb.vals_s, dx0, ld, coef, accumulate);
+}
+
+template <int VEC>
+void launch_sums_nv(int nv, const EmbTabs& et, int nt, int64_t B, const EmbSortBufs& sb,
+                    const float* dx0, int ld, const float* coef, int accumulate, hipStream_t s) {
+  switch (nv) {
+#define CASE(k) \
+  case k: launch_sums<VEC, k>(et, nt, B, sb, dx0, ld, coef, accumulate, s); break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+  }
+}
+
+}  // namespace
+
 dcnr_status emb_segment_sum(const EmbBwdDesc& e, const EmbSortBufs& sb, int64_t B,
-                            const float* dx0, int accumulate, hipStream_t s) {
+                            const float* dx0, int ld, const float* coef, int accumulate,
+                            hipStream_t s) {
   const int64_t n = (int64_t)e.n_tab * B;
   if (n <= 0) return DCNR_OK;
-  const EmbTabs et = make_tabs(e);
-  const dim3 gs((unsigned)cdiv(n, ENT));
-  if (vec4_ok(e, dx0)) {
-    hipLaunchKernelGGL(emb_runs_short_kernel<4>, gs, dim3(ENT), 0, s, et, e.n_tab, B, sb.keys_s,
-                       sb.vals_s, dx0, accumulate);
-    DCNR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(emb_runs_long_kernel<4>, gs, dim3(ENT), 0, s, et, B, n, sb.keys_s,
-                       sb.vals_s, dx0, accumulate);
-  } else {
-    hipLaunchKernelGGL(emb_runs_short_kernel<1>, gs, dim3(ENT), 0, s, et, e.n_tab, B, sb.keys_s,
-                       sb.vals_s, dx0, accumulate);
-    DCNR_LAUNCH_CHECK();
-    hipLaunchKernelGGL(emb_runs_long_kernel<1>, gs, dim3(ENT), 0, s, et, B, n, sb.keys_s,
-                       sb.vals_s, dx0, accumulate);
+  if (e.nv < 1 || e.nv > 8) {
+    set_error("embedding backward: %d cross basis vectors unsupported", e.nv);
+    return DCNR_UNSUPPORTED_SHAPE;
   }
+  const EmbTabs et = make_tabs(e);
+  if (vec4_ok(e, dx0, ld))
+    launch_sums_nv<4>(e.nv, et, e.n_tab, B, sb, dx0, ld, coef, accumulate, s);
+  else
+    launch_sums_nv<1>(e.nv, et, e.n_tab, B, sb, dx0, ld, coef, accumulate, s);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }

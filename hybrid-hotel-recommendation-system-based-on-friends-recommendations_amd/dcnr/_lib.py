@@ -24,7 +24,7 @@ FLAG_CHECK_INDICES = 1
 FLAG_KEEP_INTERMEDIATES = 2
 # dcnr_ws_tensor (include/dcnr.h)
 WS_KINDS = ["x0", "h", "t1", "t2", "a1", "mask_a1", "mask_h", "bn_mean", "bn_invstd", "bn_scale",
-            "bn_shift", "du", "dt2", "da", "dt1", "G", "dx0", "zc", "dx0_total"]
+            "bn_shift", "du", "dt2", "da", "dt1", "G", "dx0", "zc", "xcoef", "sc"]
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.c_void_p)

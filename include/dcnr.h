@@ -128,12 +128,12 @@ dcnr_status dcnr_workspace_size(const dcnr_model_desc* desc, int64_t B, int mode
 /* Where a stored tensor lives in the workspace of (desc, B, mode), for tests
  * that check each stage against a recomputation from the kernels' own stored
  * inputs.  Row-major with leading dimension Hp = hidden rounded up to 8
- * (Dp for x0 / dx0); element type bf16 in bf16 mode, else fp32 (masks: 1 bit
- * per element, Hp/8 bytes per row; BN vectors, zc, dx0: fp32).  dx0 is the
- * deep tower's part of d loss/d x0; dx0_total (fp32) is deep + cross part of
- * the embedding tables' columns only, TABLE-MAJOR: table t's [B][w_t] block
- * starts at float B * off_t (off_t = its first x0 column) -- the rows the
- * embedding gradients sum.  `index` is
+ * (Dp for x0, Dq = Dp rounded up to 32 for dx0); element type bf16 in bf16
+ * mode, else fp32 (masks: 1 bit per element, Hp/8 bytes per row; BN vectors,
+ * zc, dx0, xcoef, sc: fp32).  dx0 is the deep tower's part of d loss/d x0;
+ * the cross network's part is sum_k xcoef[b][k] V_k with V = (w_0 .. w_{L-1},
+ * w_f[H:]), xcoef [B][L+1]; sc [B][2L+1] holds the forward's per-sample cross
+ * scalars (x_l . w_l for l < L, x_0 . w_m for m < L, x_0 . w_f[H:]).  `index` is
  * the block j (h: 0..n_res; bn_*: 2j for bn1, 2j+1 for bn2).  *offset = -1
  * when that tensor is not materialised in this configuration. */
 typedef enum {
@@ -141,7 +141,7 @@ typedef enum {
   DCNR_WS_MASK_A1 = 5, DCNR_WS_MASK_H = 6, DCNR_WS_BN_MEAN = 7, DCNR_WS_BN_INVSTD = 8,
   DCNR_WS_BN_SCALE = 9, DCNR_WS_BN_SHIFT = 10, DCNR_WS_DU = 11, DCNR_WS_DT2 = 12,
   DCNR_WS_DA = 13, DCNR_WS_DT1 = 14, DCNR_WS_G = 15, DCNR_WS_DX0 = 16, DCNR_WS_ZC = 17,
-  DCNR_WS_DX0_TOTAL = 18, DCNR_WS_KINDS = 19
+  DCNR_WS_XCOEF = 18, DCNR_WS_SC = 19, DCNR_WS_KINDS = 20
 } dcnr_ws_tensor;
 dcnr_status dcnr_workspace_offset(const dcnr_model_desc* desc, int64_t B, int mode, int kind,
                                   int index, int64_t* offset);

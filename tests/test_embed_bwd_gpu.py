@@ -2,14 +2,15 @@
 embedding gradients of loss.backward() (reference train.py:156-158, 225;
 nn.Embedding with sparse=False, i.e. embedding_dense_backward).
 
-grad_t[r] = sum of dx0_total[b, off_t:off_t+w_t] over the samples b with
-id_t[b] == r.  The library sums each row in a FIXED order: runs of <= 16
+grad_t[r] = sum of dx0[b, off_t:off_t+w_t] over the samples b with id_t[b] == r,
+dx0 = deep part + sum_k coef[b][k] V_k (the low-rank cross part).  The library sums each row in a FIXED order: runs of <= 16
 samples sequentially in ascending b; longer runs one wave per row, walked in
 blocks of 64 entries, slot s of S lane slots taking entries s, s+S, ... of
 every block in ascending order, slots added in ascending order.  ``emulate_table`` restates that order in numpy fp32, so the
-gradients are checked BIT-EXACT against it, from the kernels' own dx0_total
-(table-major: table t's [B][w_t] block at float offset B * off_t).  The fp64 recomputation of dx0_total itself
-is pinned by tests/test_stages_gpu.py.
+gradients are checked BIT-EXACT against it, from the kernels' own deep dx0
+and cross coefficients (row = deep sum + sum_k coef sum_k V_k, V = (w_0 ..
+w_{L-1}, w_f[H:]), each term rounded twice).  The fp64 recomputation of the deep dx0 and of
+the cross coefficients is pinned by tests/test_stages_gpu.py.
 
 Skewed ids exercise both paths: a user id taken by 40 % of the batch, a
 Zipf-like item column, a categorical column with one value (a run of B) and
@@ -27,22 +28,34 @@ SHORT = 16   # embed_bwd.hip LIM
 BLK = 64     # embed_bwd.hip emb_runs_long_kernel block of entries
 
 
-def emulate_table(ids, X, rows, vec):
-    """fp32 gradient of one table in the library's summation order."""
+def emulate_table(ids, X, Cf, Vt, rows, vec):
+    """fp32 gradient of one table in the library's summation order: X the
+    table's deep dx0 segments [B][w], Cf the cross coefficients [B][nv], Vt
+    the basis restricted to the table's columns [nv][w]."""
     B, w = X.shape
+    nv = Cf.shape[1]
     order = np.argsort(ids, kind="stable")
     ks = ids[order]
     heads = np.flatnonzero(np.r_[True, ks[1:] != ks[:-1]])
     ends = np.r_[heads[1:], B]
     lens = ends - heads
     g = np.zeros((rows, w), np.float32)
+
+    def combine(deep, cs):   # row = deep + sum_k cs_k V_k, two roundings per term
+        out = deep.astype(np.float32)
+        for k in range(nv):
+            out = (out + (np.float32(cs[..., k:k + 1]) * Vt[k]).astype(np.float32)).astype(np.float32)
+        return out
+
     short = lens <= SHORT
     hs, ls = heads[short], lens[short]
     acc = np.zeros((len(hs), w), np.float32)
+    csum = np.zeros((len(hs), nv), np.float32)
     for k in range(SHORT):
         sel = ls > k
         acc[sel] += X[order[hs[sel] + k]]
-    g[ks[hs]] = acc
+        csum[sel] += Cf[order[hs[sel] + k]]
+    g[ks[hs]] = combine(acc, csum)
     G = w // vec
 
     def seq(a):   # sequential fp32 sum over axis 0 (0 if empty)
@@ -50,6 +63,7 @@ def emulate_table(ids, X, rows, vec):
 
     for h, e in zip(heads[~short], ends[~short]):
         ent = X[order[h:e]]
+        cfe = Cf[order[h:e]]
         m = e - h
         out = np.zeros(w, np.float32)
         for cb in range(0, G, 64):
@@ -57,14 +71,70 @@ def emulate_table(ids, X, rows, vec):
             S = 64 // gb
             cols = slice(cb * vec, (cb + gb) * vec)
             sub = ent[:, cols]
-            tot = None
+            tot = ctot = None
             for s in range(S):   # slot s: entries s, s+S, ... of every BLK-entry block
                 idx = [p + j for p in range(0, m, BLK) for j in range(s, BLK, S) if p + j < m]
-                t = seq(sub[idx])
+                t, ct = seq(sub[idx]), seq(cfe[idx])
                 tot = t if tot is None else tot + t
-            out[cols] = tot
+                ctot = ct if ctot is None else ctot + ct
+            out[cols] = _combine_cols(tot, ctot, Vt[:, cols])
         g[ks[h]] = out
     return g
+
+
+def _combine_cols(deep, cs, Vc):
+    out = deep.astype(np.float32)
+    for k in range(Vc.shape[0]):
+        out = (out + (np.float32(cs[k]) * Vc[k]).astype(np.float32)).astype(np.float32)
+    return out
+
+
+def _tables(m, batch_np, cfg):
+    """[(grad name, ids, first x0 column, width)]"""
+    u, i, c = batch_np
+    names = ["user_embedding.weight", "item_embedding.weight"]
+    names += [f"cat_embeddings.{k}.weight" for k in range(c.shape[1])]
+    ids = [u, i] + [c[:, k] for k in range(c.shape[1])]
+    out, col = [], 0
+    for nm, idv in zip(names, ids):
+        w = m.state_dict()[nm].shape[1]
+        out.append((nm, idv, col, w))
+        col += w
+    return out
+
+
+def _check_tables(m, cfg, B, ws, grads, batch_np, vec_expected=None):
+    from dcnr import _lib
+    gd = dict(zip([k for k, _ in m.named_parameters()], grads))
+    sd = m.state_dict()
+    D = m._dims["input_dim"]
+    Dp = (D + 7) // 8 * 8
+    Dq = (Dp + 31) // 32 * 32
+    L = cfg["params"]["n_cross_layers"]
+    H = cfg["params"]["hidden_dim"]
+    off = m.workspace_offset(B, _lib.TRAIN, "dx0", 0)
+    X = ws[off:off + B * Dq * 4].view(torch.float32).view(B, Dq)[:, :D].cpu().numpy()
+    off = m.workspace_offset(B, _lib.TRAIN, "xcoef", 0)
+    Cf = ws[off:off + B * (L + 1) * 4].view(torch.float32).view(B, L + 1).cpu().numpy()
+    Vfull = np.stack([sd[f"cross_network.{l}.w.weight"][0].cpu().numpy() for l in range(L)]
+                     + [sd["final_linear.weight"][0, H:].cpu().numpy()]).astype(np.float32)
+    tabs = _tables(m, batch_np, cfg)
+    vec = 4 if all(w % 4 == 0 for _, _, _, w in tabs) and Dq % 4 == 0 else 1
+    if vec_expected is not None:
+        assert vec == vec_expected
+    long_runs = 0
+    for name, ids, col, w in tabs:
+        rows = sd[name].shape[0]
+        ref = emulate_table(ids, X[:, col:col + w], Cf, Vfull[:, col:col + w], rows, vec)
+        got = gd[name].cpu().numpy()
+        if not np.array_equal(got, ref):
+            bad = np.flatnonzero(np.any(got != ref, axis=1))
+            cnt = np.bincount(ids, minlength=rows)
+            raise AssertionError((name, np.abs(got - ref).max(), len(bad), bad[:5].tolist(),
+                                  cnt[bad[:5]].tolist(), got[bad[0]][:4].tolist(),
+                                  ref[bad[0]][:4].tolist()))
+        long_runs += int((np.bincount(ids, minlength=rows) > SHORT).sum())
+    return long_runs
 
 
 def _cfg():
@@ -116,41 +186,20 @@ def _fwd_bwd(m, batch, seed, grads=None, accumulate=False):
 @pytest.mark.parametrize("precision", ["bf16", "fp32"])
 def test_embedding_grads_bit_exact_skewed(dev, precision):
     """Every table's gradient equals the fixed-order fp32 emulation from the
-    kernels' own dx0_total, bit for bit; rows no sample references are 0."""
-    from dcnr import _lib
+    kernels' own deep dx0 and cross coefficients, bit for bit; rows no sample
+    references are 0."""
     cfg = _cfg()
     B = 65536
     m = _model(cfg, dev, precision)
     batch = _skewed_batch(cfg, B, dev)
     grads, ws = _fwd_bwd(m, batch, seed=77)
-    names = [k for k, _ in m.named_parameters()]
-    gd = dict(zip(names, grads))
-    D = m._dims["input_dim"]
-    Dp = (D + 7) // 8 * 8
-    off = m.workspace_offset(B, _lib.TRAIN, "dx0_total", 0)
-    assert off >= 0
-    X = ws[off:off + B * Dp * 4].view(torch.float32).cpu().numpy()   # table-major blocks
-    u, i, c = (t.cpu().numpy() for t in batch[:3])
-    tabs = [("user_embedding.weight", u), ("item_embedding.weight", i)]
-    tabs += [(f"cat_embeddings.{k}.weight", c[:, k]) for k in range(c.shape[1])]
-    widths = [m.state_dict()[name].shape[1] for name, _ in tabs]
-    vec = 4 if all(w % 4 == 0 for w in widths) and D % 4 == 0 else 1
-    col = 0
-    long_runs = 0
-    for (name, ids), w in zip(tabs, widths):
-        rows = m.state_dict()[name].shape[0]
-        ref = emulate_table(ids, X[B * col:B * (col + w)].reshape(B, w), rows, vec)
-        got = gd[name].cpu().numpy()
-        assert np.array_equal(got, ref), (name, np.abs(got - ref).max())
-        long_runs += int((np.bincount(ids, minlength=rows) > SHORT).sum())
-        col += w
+    long_runs = _check_tables(m, cfg, B, ws, grads, [t.cpu().numpy() for t in batch[:3]], 4)
     assert long_runs > 2000   # both kernels ran
 
 
 def test_embedding_grads_bit_exact_odd_widths(dev):
-    """CFG_ODD (table widths 24, 2, 5, 2: the scalar-column kernels), every
-    run long (B >> rows): bit-exact against the emulation."""
-    from dcnr import _lib
+    """CFG_ODD (table widths 24, 2, 5, 2: the scalar-column kernels; 4 cross
+    layers), every run long (B >> rows): bit-exact against the emulation."""
     cfg = gc.CFG_ODD
     B = 4096
     m = _model(cfg, dev, "fp32")
@@ -159,19 +208,7 @@ def test_embedding_grads_bit_exact_odd_widths(dev):
     batch = (t(u, torch.int64), t(i, torch.int64), t(c, torch.int64), t(n, torch.float32),
              t(y, torch.float32))
     grads, ws = _fwd_bwd(m, batch, seed=5)
-    gd = dict(zip([k for k, _ in m.named_parameters()], grads))
-    D = m._dims["input_dim"]
-    Dp = (D + 7) // 8 * 8
-    off = m.workspace_offset(B, _lib.TRAIN, "dx0_total", 0)
-    X = ws[off:off + B * Dp * 4].view(torch.float32).cpu().numpy()   # table-major blocks
-    tabs = [("user_embedding.weight", u), ("item_embedding.weight", i)]
-    tabs += [(f"cat_embeddings.{k}.weight", c[:, k]) for k in range(c.shape[1])]
-    col = 0
-    for name, ids in tabs:
-        rows, w = m.state_dict()[name].shape
-        ref = emulate_table(ids, X[B * col:B * (col + w)].reshape(B, w), rows, 1)
-        assert np.array_equal(gd[name].cpu().numpy(), ref), name
-        col += w
+    _check_tables(m, cfg, B, ws, grads, [u, i, c], 1)
 
 
 def test_full_size_backward_bit_identical(dev):

@@ -16,12 +16,15 @@ and compared.  The workspace keeps every block's backward buffers
     h_{j+1}     relu(t2 * scale + shift + h_j)                     <= BF16_ULPS ulp
     masks       1-bit [a1 != 0], [h_j > 0] images                  exact
     logits      h_R . w_f[:H] + zc + b_f                           rel 1e-5
+    sc          s_l, x_0 . w_m, x_0 . w_f[H:] (cross scalars)      rel 1e-5
   backward (loss.backward(), train.py:225)
     du_{R-1}    dz w_f[:H] * [h_R > 0]                             <= BF16_ULPS ulp
     dt2, dt1    BN backward apply (coefficients from fp64 sums)     <= BF16_ULPS ulp
     da          (dt2 W2) / (1-p) * [a1 != 0]                        <= BF16_ULPS ulp
     du_{j-1}    (dt1 W1 + du_j) * [h_j > 0];  G = dt1_0 W1 + du_0  <= BF16_ULPS ulp
     dW, db, dgamma, dbeta, dW_f, cross, embedding grads (fp32 sums)  rel 2e-4
+    dx0_cross   sum_k xcoef_k V_k (low-rank cross backward)         rel 2e-4
+    (the cross weight grads' x_0 part is summed over the stored bf16 x0)
 
 A bf16 value within BF16_ULPS units in the last place (plus ACC_EPS times
 the magnitude of the summed terms): the kernels and this recomputation
@@ -80,17 +83,6 @@ def check_bf16(name, got, ref, stats, scale):
     stats.append((name, flips, float(d.max())))
     assert nb == 0, (name, nb, float(d.max()), got[bad][:5].tolist(), ref[bad][:5].tolist())
     assert flips <= FLIP_FRAC, (name, flips)
-
-
-def _table_cols(sd, K):
-    """[(first, end) x0 column of each table]: user, item, cat 0..K-1."""
-    names = ["user_embedding.weight", "item_embedding.weight"]
-    names += [f"cat_embeddings.{k}.weight" for k in range(K)]
-    out, a = [], 0
-    for n in names:
-        out.append((a, a + sd[n].shape[1]))
-        a += sd[n].shape[1]
-    return out
 
 
 def check_rel(name, got, ref, tol=REL):
@@ -216,6 +208,14 @@ def test_bf16_step_stage_by_stage(dev, full):
         ss.append(s_)
         x = x + x * s_[:, None] + sd0[f"cross_network.{l}.b"].double()
     check_rel("zc", zc, x @ wf[H:].double(), 1e-5)
+    # the cross backward's saved scalars: s_l, u_m = x_0 . w_m, u_f = x_0 . w_f[H:]
+    Lc = cfg["params"]["n_cross_layers"]
+    scs = T("sc", cols=2 * Lc + 1, dtype=f32)
+    us = [x0f.double() @ sd0[f"cross_network.{m}.w.weight"][0].double() for m in range(Lc)]
+    for l in range(Lc):
+        check_rel(f"s[{l}]", scs[:, l], ss[l], 1e-5)
+        check_rel(f"u[{l}]", scs[:, Lc + l], us[l], 1e-5)
+    check_rel("u_f", scs[:, 2 * Lc], x0f.double() @ wf[H:].double(), 1e-5)
 
     # ---- backward ------------------------------------------------------
     def bn_back(dr, t, bi, gam_key):
@@ -265,25 +265,33 @@ def test_bf16_step_stage_by_stage(dev, full):
             check_bf16("G", G[:, :H], Gj[:, :H], stats, Gs)
     check_rel("db0", gd["initial_deep_layer.bias"], G[:, :H].double().sum(0))
     check_rel("dW0", gd["initial_deep_layer.weight"], G[:, :H].double().T @ x0.double())
-    dx0 = T("dx0", cols=Dp, dtype=f32)[:, :D]
+    Dq = (Dp + 31) // 32 * 32
+    dx0 = T("dx0", cols=Dq, dtype=f32)[:, :D]
     check_rel("dx0", dx0, G[:, :H].double() @ W0.double())
-    # cross backward (fp64 from the fp32 gathered rows) + embedding scatter of dx0
+    # cross backward (fp64 from the fp32 gathered rows).  The weight gradients'
+    # x_0 part is summed over the STORED x0 (bf16 here, like dW0's): x_l enters
+    # them as x_l + a_l (x0 - x0f), a_l = prod_{j<l} (1 + s_j)
+    dxs = x0.double() - x0f.double()
+    a_l = [torch.ones(B, dtype=torch.float64, device=dev)]
+    for l in range(Lc):
+        a_l.append(a_l[-1] * (1.0 + ss[l]))
     dx = dz.double()[:, None] * wf[H:].double()
-    check_rel("dW_f[H:]", gd["final_linear.weight"][0, H:], x.T @ dz.double())
+    check_rel("dW_f[H:]", gd["final_linear.weight"][0, H:],
+              (x + a_l[Lc][:, None] * dxs).T @ dz.double())
     check_rel("db_f", gd["final_linear.bias"], dz.double().sum().reshape(1))
     for l in reversed(range(cfg["params"]["n_cross_layers"])):
         xl, sl = xs[l], ss[l]
         wl = sd0[f"cross_network.{l}.w.weight"][0].double()
         check_rel(f"cross_b[{l}]", gd[f"cross_network.{l}.b"], dx.sum(0))
         gx = (dx * xl).sum(1)
-        check_rel(f"cross_w[{l}]", gd[f"cross_network.{l}.w.weight"][0], (gx[:, None] * xl).sum(0))
+        check_rel(f"cross_w[{l}]", gd[f"cross_network.{l}.w.weight"][0],
+                  (gx[:, None] * (xl + a_l[l][:, None] * dxs)).sum(0))
         dx = dx * (1.0 + sl)[:, None] + gx[:, None] * wl[None, :]
+    # dx0_cross = sum_k xcoef[b][k] V_k, V = (w_0 .. w_{L-1}, w_f[H:])
+    xco = T("xcoef", cols=Lc + 1, dtype=f32).double()
+    Vs = [sd0[f"cross_network.{m}.w.weight"][0].double() for m in range(Lc)] + [wf[H:].double()]
+    check_rel("dx0_cross", sum(xco[:, k:k + 1] * Vs[k][None] for k in range(Lc + 1)), dx)
     dxe = dx0.double() + dx
-    # dx0_total: the tables' columns of dx0 + dx_cross, table-major ([B][w_t] per table)
-    flat = T("dx0_total", cols=Dp, dtype=f32).reshape(-1)
-    Dt = D - cfg["n_num"]
-    tot = torch.cat([flat[B * a:B * b].view(B, b - a) for a, b in _table_cols(sd0, K)], 1)
-    check_rel("dx0_total", tot, dxe[:, :Dt])
     off = 0
     tabs = [("user_embedding.weight", u), ("item_embedding.weight", i)]
     tabs += [(f"cat_embeddings.{k}.weight", c[:, k]) for k in range(K)]
