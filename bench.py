@@ -54,7 +54,7 @@ CFG2_B = 65536
 CFG2_BYTES = 14 * 8 + 14 * 32 * 4 + 8 * 4 + D * 4
 PEAK_BF16 = 2.5e15     # MI355X dense bf16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM = 8.0e12
-SINGLE_KERNEL_CLASSES = ("gemm_dw", "cross_bwd", "adam", "gather_cross")
+SINGLE_KERNEL_CLASSES = ("gemm_dw", "adam", "gather_cross")
 CLASS_KERNELS = {
     "gather_cross": "gather_cross_v4_kernel (train forward)",
     "gemm_fwd": "gemm_ws_kernel (deep-tower Linear forward)",
@@ -62,8 +62,8 @@ CLASS_KERNELS = {
     "gemm_dw": "gemm_dw_kernel (deep-tower weight gradient)",
     "rowwise": "rowcol_kernel (BN apply / statistics passes)",
     "reduce": "reduce / split-K combine kernels",
-    "cross_bwd": "cross_bwd_v4_kernel (cross backward, total dx0 rows)",
-    "emb_sort": "emb_keys_kernel + rocPRIM radix sort of the ids (side stream, overlapped)",
+    "cross_bwd": "cross_coef / x0_alpha / cross_final kernels (low-rank cross backward)",
+    "emb_sort": "emb_ids/hist/scan/scatter/bucket_sort kernels (stable id sort)",
     "emb_sum": "emb_runs_short/long_kernel (fixed-order embedding-gradient sums)",
     "head": "row_dot / logits / bce kernels",
     "adam": "adam_kernel (fused AdamW)",

@@ -89,43 +89,16 @@ namespace {
     if (st_ != DCNR_OK) return st_;          \
   } while (0)
 
-// The id sort of the embedding backward runs on the call's stream unless
-// DCNR_EMB_SORT_SIDE=1 puts it on a side stream overlapped with the deep-tower
-// backward (measured slower: its blocks hold CU slots the GEMMs wait for).
-bool emb_sort_on_side() {
-  static const bool on = [] {
-    const char* e = getenv("DCNR_EMB_SORT_SIDE");
-    return e && e[0] == '1';
-  }();
-  return on;
+// dcnr_grad_ready_fn of the model desc, if any
+dcnr_status grads_ready(const dcnr_model_desc* desc, int group, hipStream_t s) {
+  if (!desc->grad_ready) return DCNR_OK;
+  const int rc = desc->grad_ready(desc->grad_ready_ctx, group, (void*)s);
+  if (rc != 0) {
+    set_error("grad_ready hook failed (%d) for gradient group %d", rc, group);
+    return DCNR_HIP_ERROR;
+  }
+  return DCNR_OK;
 }
-
-// Fork/join of the embedding-backward side stream within one call.
-struct SideJoin {
-  hipStream_t side = nullptr;
-  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-  dcnr_status fork(hipStream_t s, bool use_side) {
-    if (!use_side) { side = s; return DCNR_OK; }
-    TRY(emb_side_stream(&side));
-    DCNR_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
-    DCNR_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
-    DCNR_HIP(hipEventRecord(fork_ev, s));
-    DCNR_HIP(hipStreamWaitEvent(side, fork_ev, 0));
-    return DCNR_OK;
-  }
-  dcnr_status record() {
-    if (join_ev) DCNR_HIP(hipEventRecord(join_ev, side));
-    return DCNR_OK;
-  }
-  dcnr_status join(hipStream_t s) {
-    if (join_ev) DCNR_HIP(hipStreamWaitEvent(s, join_ev, 0));
-    return DCNR_OK;
-  }
-  ~SideJoin() {
-    if (fork_ev) (void)hipEventDestroy(fork_ev);
-    if (join_ev) (void)hipEventDestroy(join_ev);
-  }
-};
 
 constexpr int MAX_CAT = 64;
 constexpr int MAX_RES = 8;
@@ -920,8 +893,10 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     TRYB(DCNR_K_PACK, zb, fill_zero_multi(2 + d.K, zp, zn, s));
   }
 
-  // embedding backward, part 1: sort the ids (they are all it reads) on the
-  // side stream while the deep-tower backward runs on `s`
+  // embedding backward, part 1: sort the (table row, sample) pairs (they
+  // depend on the ids alone).  Measured: on a side stream overlapped with the
+  // deep-tower backward the sort's blocks held CU slots the GEMMs waited for
+  // and the step got slower than running it here.
   GatherDesc g = make_gather(d, P, desc->n_num);
   EmbBwdDesc eb;
   memset(&eb, 0, sizeof(eb));
@@ -929,14 +904,20 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   for (int t = 0; t < g.n_tab; ++t) {
     eb.grad[t] = Gr.tab[t]; eb.rows[t] = g.rows[t]; eb.width[t] = g.width[t]; eb.off[t] = g.off[t];
   }
-  SideJoin sj;
-  TRY(sj.fork(s, emb_sort_on_side()));
-  {
-    hipStream_t s = sj.side;   // TRYB times the side stream
-    TRYB(DCNR_K_EMB_SORT, 2.0 * 8.0 * g.n_tab * B + 8.0 * B * (2 + d.K) + 4.0 * B * 2,
-         emb_sort(eb, user_ids, item_ids, cat_features, B, L.emb, s));
-  }
-  TRY(sj.record());
+  TRYB(DCNR_K_EMB_SORT, 2.0 * 8.0 * g.n_tab * B + 8.0 * B * (2 + d.K) + 4.0 * B * 2,
+       emb_sort(eb, user_ids, item_ids, cat_features, B, L.emb, s));
+  // ---- cross network + head bias (low-rank form, from the forward's
+  // per-sample scalars, dz and the stored x0 alone; cross_bwd.hip)
+  CrossGrads cg;
+  memset(&cg, 0, sizeof(cg));
+  for (int l = 0; l < d.L; ++l) { cg.dw[l] = Gr.cw[l]; cg.db[l] = Gr.cb[l]; }
+  cg.dwf_cross = Gr.wf + H;
+  cg.dbf = Gr.bf;
+  const CrossParams cpx = make_cross(d, P);
+  TRYB(DCNR_K_CROSS_BWD, (double)B * (4.0 * (2 * d.L + 1) + 4.0 + 8.0 * (d.L + 1)) +
+                             (double)B * d.Dp * d.es,
+       cross_backward(cpx, d.D, L.sc, dz, L.x0, d.prec == DCNR_PREC_BF16, d.Dp, B, cg, L.xcoef,
+                      L.xalpha, L.cscratch, L.cscratch_bytes, accumulate, s));
 
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   const bool fuse = epi_stats_ok(d);   // BN partials from the dX GEMM epilogues
@@ -1014,6 +995,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   TRYB(DCNR_K_ROWWISE, act_b(d, B), col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
   TRY(bias_reduce(d, L, nc, Gr.b0, accumulate, s));
   TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s));
+  TRY(grads_ready(desc, DCNR_GRADS_DENSE, s));   // every non-embedding gradient is enqueued
   {
     GemmArgs g;
     memset(&g, 0, sizeof(g));
@@ -1021,18 +1003,6 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     g.M = B; g.N = d.Dp; g.K = Hp; g.k_per_split = Hp;
     TRYB(DCNR_K_GEMM_DX, act_b(d, B) + 4.0 * B * d.Dp + w_b(d, d.Dp), gemm_nn(d.prec, EPI_STORE, g, 1, s));
   }
-  // ---- cross network + head bias (low-rank form, from the forward's
-  // per-sample scalars and the stored x0; cross_bwd.hip)
-  CrossGrads cg;
-  memset(&cg, 0, sizeof(cg));
-  for (int l = 0; l < d.L; ++l) { cg.dw[l] = Gr.cw[l]; cg.db[l] = Gr.cb[l]; }
-  cg.dwf_cross = Gr.wf + H;
-  cg.dbf = Gr.bf;
-  const CrossParams cpx = make_cross(d, P);
-  TRYB(DCNR_K_CROSS_BWD, (double)B * (4.0 * (2 * d.L + 1) + 4.0 + 8.0 * (d.L + 1)) +
-                             (double)B * d.Dp * d.es,
-       cross_backward(cpx, d.D, L.sc, dz, L.x0, d.prec == DCNR_PREC_BF16, d.Dp, B, cg, L.xcoef,
-                      L.xalpha, L.cscratch, L.cscratch_bytes, accumulate, s));
   // ---- embedding backward part 2: sorted (table row, sample) pairs -> per row
   // sum of the deep dx0 segments + sum of the cross coefficients
   double ew = 0;
@@ -1040,9 +1010,9 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   eb.nv = d.L + 1;
   for (int l = 0; l < d.L; ++l) eb.V[l] = cpx.w[l];
   eb.V[d.L] = cpx.wf_cross;
-  TRY(sj.join(s));
   TRYB(DCNR_K_EMB_SUM, (double)B * (4.0 * ew + (8.0 + 4.0 * (d.L + 1)) * g.n_tab),
        emb_segment_sum(eb, L.emb, B, L.dx0, dq_of(d), L.xcoef, accumulate, s));
+  TRY(grads_ready(desc, DCNR_GRADS_EMBEDDING, s));
   return DCNR_OK;
 }
 

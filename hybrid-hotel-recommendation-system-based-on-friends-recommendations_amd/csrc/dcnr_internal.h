@@ -438,7 +438,6 @@ dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* it
 dcnr_status emb_segment_sum(const EmbBwdDesc& e, const EmbSortBufs& sb, int64_t B,
                             const float* dx0_deep, int ld, const float* coef, int accumulate,
                             hipStream_t s);
-dcnr_status emb_side_stream(hipStream_t* out);
 
 
 // Column reductions: partial sums per row-chunk, part[nchunks][NK][N] (f32),

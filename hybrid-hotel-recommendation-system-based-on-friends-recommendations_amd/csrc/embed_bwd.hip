@@ -12,10 +12,9 @@
 //      pairs (below: bucket counts per chunk, a scan, a stable scatter, then
 //      per-bucket sorts on the low id bits); after it table t occupies
 //      [t*B, (t+1)*B) of the sorted arrays (key = base_t + id) and each run
-//      of equal keys lists its samples in ascending b.  It reads only the
-//      ids; DCNR_EMB_SORT_SIDE=1 runs it on a side stream overlapped with
-//      the deep-tower backward.  (rocPRIM's radix_sort_pairs did the same in
-//      ~107 us at the bench size: three look-back-bound 8-bit passes.)
+//      of equal keys lists its samples in ascending b.  (rocPRIM's
+//      radix_sort_pairs did the same in ~107 us at the bench size: three
+//      look-back-bound 8-bit passes.)
 //   3. emb_runs_short_kernel: the thread at a run's head sums runs of <= LIM
 //      entries sequentially and writes the row; emb_runs_long_kernel: the
 //      wave whose 64 positions hold the head of a longer run (popular ids,
@@ -32,7 +31,6 @@
 #include "dcnr_internal.h"
 
 #include <cstring>
-#include <mutex>
 #include <algorithm>
 
 namespace dcnr {
@@ -749,22 +747,6 @@ dcnr_status emb_segment_sum(const EmbBwdDesc& e, const EmbSortBufs& sb, int64_t 
   else
     launch_sums_nv<1>(e.nv, et, e.n_tab, B, sb, dx0, ld, coef, accumulate, s);
   DCNR_LAUNCH_CHECK();
-  return DCNR_OK;
-}
-
-// Side stream for the id sort, one per device, created on first use.
-dcnr_status emb_side_stream(hipStream_t* out) {
-  static std::mutex mu;
-  static hipStream_t streams[64] = {};
-  int dev = 0;
-  DCNR_HIP(hipGetDevice(&dev));
-  if (dev < 0 || dev >= 64) {
-    set_error("embedding backward: device %d out of range", dev);
-    return DCNR_BAD_ARG;
-  }
-  std::lock_guard<std::mutex> lk(mu);
-  if (!streams[dev]) DCNR_HIP(hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking));
-  *out = streams[dev];
   return DCNR_OK;
 }
 

@@ -28,6 +28,9 @@ WS_KINDS = ["x0", "h", "t1", "t2", "a1", "mask_a1", "mask_h", "bn_mean", "bn_inv
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.c_void_p)
+# dcnr_grad_ready_fn(ctx, group, stream); groups below
+GRAD_READY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p)
+GRADS_DENSE, GRADS_EMBEDDING = 0, 1
 
 
 class ModelDesc(ctypes.Structure):
@@ -46,6 +49,8 @@ class ModelDesc(ctypes.Structure):
         ("flags", ctypes.c_uint32),
         ("bn_allreduce", ALLREDUCE_FN),
         ("bn_allreduce_ctx", ctypes.c_void_p),
+        ("grad_ready", GRAD_READY_FN),
+        ("grad_ready_ctx", ctypes.c_void_p),
     ]
 
 
@@ -141,7 +146,7 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.dcnr_abi_version() != 1:
+        if lib.dcnr_abi_version() != 2:
             raise LibraryMissing("libdcnr ABI version mismatch")
         if path is None:
             _lib = lib

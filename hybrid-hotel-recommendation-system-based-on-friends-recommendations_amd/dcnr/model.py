@@ -172,6 +172,7 @@ class DCN_RecSys(nn.Module):
         self.keep_intermediates = False   # tests: per-block backward buffers (stage checks)
         self.bn_allreduce = None   # set by dcnr.parallel for SyncBN
         self._sync_bn_hook = None
+        self.grad_ready = None     # set by FusedTrainer (data-parallel exchange overlap)
         self._active_ws = None
         self._flat = None
 
@@ -194,6 +195,8 @@ class DCN_RecSys(nn.Module):
             (_lib.FLAG_KEEP_INTERMEDIATES if getattr(self, 'keep_intermediates', False) else 0)
         if self.bn_allreduce is not None:
             desc.bn_allreduce = self.bn_allreduce
+        if getattr(self, 'grad_ready', None) is not None:
+            desc.grad_ready = self.grad_ready
         return desc
 
     # Host-side dispatch cost matters for small serving batches: building
@@ -211,6 +214,7 @@ class DCN_RecSys(nn.Module):
         st.pop('_ptr_cache', None)
         st['_index_watch'] = IndexErrorWatch()
         st.pop('_gc_flag', None)
+        st['grad_ready'] = None   # bound to a trainer; ctypes callbacks do not copy
         return st
 
     def check_index_errors(self):
@@ -376,22 +380,31 @@ class DCN_RecSys(nn.Module):
         """Move every parameter into one contiguous fp32 buffer (views keep the
         state_dict API) and give each a ``.grad`` view into one flat gradient
         buffer: lets the fused optimizer and the DP exchange run as single
-        launches.  The total length is padded to a multiple of ``pad_to``
-        (the optimizer shards split it evenly).  Returns (flat_params, flat_grads)."""
+        launches.  Two segments, each padded to a multiple of ``pad_to`` (the
+        optimizer shards split them evenly): the embedding tables
+        [0, flat_emb_end) and the dense parameters after them -- the two
+        gradient groups dcnr_backward completes one after the other.
+        Returns (flat_params, flat_grads)."""
         params = self.param_tensors()
         dev = params[0].device
+        n_emb = 2 + len(self._dims['cat_dims'])   # the tables lead named_parameters()
         sizes = [((p.numel() + 63) // 64) * 64 for p in params]
-        total = ((sum(sizes) + pad_to - 1) // pad_to) * pad_to
+        rnd = lambda x: ((x + pad_to - 1) // pad_to) * pad_to   # noqa: E731
+        emb_end = rnd(sum(sizes[:n_emb]))   # the dense segment starts on a shard boundary
+        total = emb_end + rnd(sum(sizes[n_emb:]))
         flat = torch.zeros(total, dtype=torch.float32, device=dev)
         gflat = torch.zeros(total, dtype=torch.float32, device=dev)
         off = 0
-        for p, sz in zip(params, sizes):
+        for k, (p, sz) in enumerate(zip(params, sizes)):
+            if k == n_emb:
+                off = emb_end
             n = p.numel()
             flat[off:off + n].copy_(p.detach().reshape(-1))
             p.data = flat[off:off + n].view_as(p)
             p.grad = gflat[off:off + n].view_as(p)
             off += sz
         self._flat = (flat, gflat)
+        self.flat_emb_end = emb_end
         return flat, gflat
 
 

@@ -5,18 +5,25 @@ optimizer.step) as native calls over flat parameter/gradient/moment buffers:
     dcnr_forward(train) -> dcnr_bce_with_logits -> dcnr_backward
       -> data-parallel exchange + dcnr_adam_step (dense semantics):
          world == 1: one launch over every parameter
-         world > 1, shard_optimizer (default): reduce-scatter of the flat
-           gradient (RCCL), AdamW on this rank's 1/world shard of the flat
-           parameters with its 1/world of the moments, all-gather of the
-           updated parameters -- the all-reduce's bytes, 1/world of the
-           optimizer's HBM traffic and moment memory (ZeRO-1 style)
-         world > 1, shard_optimizer=False: all-reduce, then every rank
-           updates everything
-         world > 1, exchange="sparse": the user table's gradient goes through
-           the owner-bucketed sparse exchange (dcnr.parallel.
-           sparse_rows_allreduce: only the rows the ranks' batches touched),
-           the rest of the flat gradient through one all-reduce, then every
-           rank updates everything
+         world > 1: the flat buffers have two segments (model.flatten_): the
+           embedding tables (~95 % of the bytes) and the dense parameters.
+           dcnr_backward completes the dense group first (its
+           DCNR_GRADS_DENSE hook fires before the dx0 GEMM and the whole
+           embedding backward), and the hook starts the dense segment's
+           all-reduce right there, so it runs under the embedding backward.
+           Then the embedding segment:
+           shard_optimizer (default): reduce-scatter (RCCL), AdamW on this
+             rank's 1/world shard with its 1/world of the moments,
+             all-gather of the updated parameters -- the all-reduce's bytes,
+             1/world of the optimizer's HBM traffic and moment memory
+             (ZeRO-1 style); the dense segment is updated whole on every rank
+           shard_optimizer=False: all-reduce, every rank updates everything
+           exchange="sparse": the user table's gradient goes through the
+             owner-bucketed sparse exchange (dcnr.parallel.
+             sparse_rows_allreduce: only the rows the ranks' batches
+             touched; it synchronises the host for its message sizes), the
+             other tables through an all-reduce, every rank updates
+             everything
 
 Numerically the same update as ``torch.optim.AdamW``/``Adam`` on the
 reference's dense gradients (every embedding row's moments decay every step).
@@ -52,10 +59,18 @@ class FusedTrainer:
             shard_optimizer = False
         self.shard = (self.world > 1) if shard_optimizer is None else bool(shard_optimizer)
         self.flat, self.gflat = model.flatten_(pad_to=64 * self.world)
-        n = self.flat.numel() // (self.world if self.shard else 1)
-        self.m = torch.zeros(n, dtype=torch.float32, device=self.flat.device)
+        self.E = model.flat_emb_end                      # embedding segment [0, E)
+        N = self.flat.numel()
+        self.Es = self.E // self.world if self.shard else self.E   # this rank's embedding moments
+        self.m = torch.zeros(self.Es + N - self.E, dtype=torch.float32, device=self.flat.device)
         self.v = torch.zeros_like(self.m)
-        self.gshard = torch.empty_like(self.m) if self.shard else None
+        self.gshard = torch.empty(self.Es, dtype=torch.float32,
+                                  device=self.flat.device) if self.shard else None
+        self._dense_work = None
+        self._hook_error = None
+        if self.world > 1:   # start the dense segment's all-reduce from inside the backward
+            self._grad_ready_cb = _lib.GRAD_READY_FN(self._on_grads_ready)
+            model.grad_ready = self._grad_ready_cb
         self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
         self.decoupled = optimizer_name == 'AdamW'
         self.step_count = 0
@@ -77,10 +92,29 @@ class FusedTrainer:
         logits, self._ws = run_forward(model, True, seed, user, item, cat, num, self._ws)
         # grad_scale 1/world: the SUM all-reduce then yields the global mean gradient
         loss, dz = bce_with_logits(logits, y, True, 1.0 / self.world)
-        run_backward(model, user, item, cat, num, dz, self._ws, self._grads, seed,
-                     accumulate=False)
+        self._dense_work = None
+        try:
+            run_backward(model, user, item, cat, num, dz, self._ws, self._grads, seed,
+                         accumulate=False)
+        except RuntimeError as e:
+            if self._hook_error is not None:
+                err, self._hook_error = self._hook_error, None
+                raise RuntimeError("gradient exchange hook failed") from err
+            raise
         self.exchange_and_update(user_ids=user)
         return (loss, logits) if return_logits else loss
+
+    def _on_grads_ready(self, ctx, group, stream):
+        """dcnr_grad_ready_fn: the dense gradients are enqueued -> start their
+        all-reduce now (ordered after the stream's work so far)."""
+        try:
+            if group == _lib.GRADS_DENSE:
+                self._dense_work = dist.all_reduce(self.gflat[self.E:], op=dist.ReduceOp.SUM,
+                                                   group=self.pg, async_op=True)
+            return 0
+        except Exception as e:   # noqa: BLE001 -- reported after the C call returns
+            self._hook_error = e
+            return 1
 
     def check_indices(self):
         """Wait for every step's id check; raises IndexError if any failed
@@ -94,29 +128,39 @@ class FusedTrainer:
         ``user_ids``: this rank's batch user ids (the sparse exchange)."""
         adam = adam or self._adam
         self.step_count += 1
-        if self.world > 1 and self.exchange == "sparse":
+        E, Es, world = self.E, self.Es, self.world
+        if world == 1:
+            adam(self.flat, self.gflat, self.m, self.v, self.step_count)
+            return
+        dense = self._dense_work   # started by the backward's hook, or now
+        if dense is None:
+            dense = dist.all_reduce(self.gflat[E:], op=dist.ReduceOp.SUM, group=self.pg,
+                                    async_op=True)
+        self._dense_work = None
+        if self.exchange == "sparse":
             from .parallel import sparse_rows_allreduce
             uw = self.model.user_embedding.weight
             nu = ((uw.numel() + 63) // 64) * 64     # its padded segment at offset 0
             assert uw.data_ptr() == self.flat.data_ptr()
             self.last_exchange = sparse_rows_allreduce(uw.grad, user_ids, self.pg)
-            dist.all_reduce(self.gflat[nu:], op=dist.ReduceOp.SUM, group=self.pg)
-            adam(self.flat, self.gflat, self.m, self.v, self.step_count)
-            return
-        if self.world > 1 and self.shard:
-            n = self.m.numel()
-            dist.reduce_scatter_tensor(self.gshard, self.gflat, op=dist.ReduceOp.SUM,
+            dist.all_reduce(self.gflat[nu:E], op=dist.ReduceOp.SUM, group=self.pg)
+            adam(self.flat[:E], self.gflat[:E], self.m[:E], self.v[:E], self.step_count)
+        elif self.shard:
+            dist.reduce_scatter_tensor(self.gshard, self.gflat[:E], op=dist.ReduceOp.SUM,
                                        group=self.pg)
-            pshard = self.flat[self.rank * n:(self.rank + 1) * n]
-            adam(pshard, self.gshard, self.m, self.v, self.step_count)
-            dist.all_gather_into_tensor(self.flat, pshard, group=self.pg)
-            return
-        if self.world > 1:
-            dist.all_reduce(self.gflat, op=dist.ReduceOp.SUM, group=self.pg)
-        adam(self.flat, self.gflat, self.m, self.v, self.step_count)
+            pshard = self.flat[self.rank * Es:(self.rank + 1) * Es]
+            adam(pshard, self.gshard, self.m[:Es], self.v[:Es], self.step_count)
+            dist.all_gather_into_tensor(self.flat[:E], pshard, group=self.pg)
+        else:
+            dist.all_reduce(self.gflat[:E], op=dist.ReduceOp.SUM, group=self.pg)
+            adam(self.flat[:E], self.gflat[:E], self.m[:E], self.v[:E], self.step_count)
+        dense.wait()
+        adam(self.flat[E:], self.gflat[E:], self.m[Es:], self.v[Es:], self.step_count)
 
     def optimizer_step(self):
         """Adam/AdamW over the local flat gradient (no exchange)."""
+        if self.shard:
+            raise RuntimeError("optimizer_step: the moments are sharded; use exchange_and_update")
         self.step_count += 1
         self._adam(self.flat, self.gflat, self.m, self.v, self.step_count)
 

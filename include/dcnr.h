@@ -68,7 +68,7 @@
 extern "C" {
 #endif
 
-#define DCNR_ABI_VERSION 1
+#define DCNR_ABI_VERSION 2
 
 typedef void* dcnr_stream_t; /* hipStream_t */
 
@@ -98,6 +98,19 @@ typedef enum { DCNR_EVAL = 0, DCNR_TRAIN = 1 } dcnr_mode;
  * BN (each rank normalises with its own batch statistics). */
 typedef int (*dcnr_allreduce_fn)(void* ctx, double* device_buf, int64_t count, dcnr_stream_t stream);
 
+/* Optional data-parallel hook of dcnr_backward: called (from the calling
+ * thread, while the call enqueues its work) as soon as every kernel that
+ * writes a group of gradients has been enqueued on `stream`:
+ *   DCNR_GRADS_DENSE      initial_deep_layer .. final_linear (every
+ *                         parameter after the embedding tables)
+ *   DCNR_GRADS_EMBEDDING  user, item and categorical tables (last)
+ * A caller starts that group's exchange from here (ordered after the
+ * stream's work so far), so the dense group's exchange runs under the
+ * embedding backward.  Nonzero return = failure (dcnr_backward fails). */
+#define DCNR_GRADS_DENSE 0
+#define DCNR_GRADS_EMBEDDING 1
+typedef int (*dcnr_grad_ready_fn)(void* ctx, int32_t group, dcnr_stream_t stream);
+
 typedef struct {
   int64_t n_users;          /* user_embedding rows      (train.py:136) */
   int64_t n_items;          /* item_embedding rows      (train.py:137) */
@@ -113,6 +126,8 @@ typedef struct {
   uint32_t flags;           /* DCNR_FLAG_* */
   dcnr_allreduce_fn bn_allreduce; /* SyncBN hook or NULL */
   void* bn_allreduce_ctx;
+  dcnr_grad_ready_fn grad_ready;  /* gradient-group hook or NULL (ABI 2) */
+  void* grad_ready_ctx;
 } dcnr_model_desc;
 
 int dcnr_abi_version(void);
@@ -177,9 +192,9 @@ dcnr_status dcnr_gather_cross(const dcnr_model_desc* desc, void* const* params,
  * overwrites (embedding grads are zeroed, then every referenced row gets the
  * sum of its samples' dx0 rows, i.e. embedding_dense_backward semantics);
  * accumulate = 1 adds into grads.  Deterministic: the embedding sums run in
- * ascending sample order after a stable sort of the ids (on a library-owned
- * side stream, joined back into `stream` before the call's last kernel), so
- * two calls on the same inputs give bit-identical gradients. */
+ * a fixed order after a stable sort of the ids, and every other reduction is
+ * fixed-order too, so two calls on the same inputs give bit-identical
+ * gradients. */
 dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void* const* grads,
                           const int64_t* user_ids, const int64_t* item_ids,
                           const int64_t* cat_features, const float* num_features, int64_t B,
@@ -297,7 +312,7 @@ typedef enum {
   DCNR_K_KNN = 9,          /* cosine top-k                                  */
   DCNR_K_PACK = 10,        /* weight packing / zero fills                  */
   DCNR_K_SERVE = 11,       /* candidate union, ranking batch, sort, MMR     */
-  DCNR_K_EMB_SORT = 12,    /* embedding-backward id sort (side stream)      */
+  DCNR_K_EMB_SORT = 12,    /* embedding-backward stable id sort             */
   DCNR_K_EMB_SUM = 13,     /* embedding-backward per-row segmented sums     */
   DCNR_K_COUNT = 14
 } dcnr_kernel_class;

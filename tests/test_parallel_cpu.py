@@ -197,8 +197,9 @@ def _exchange_worker(rank, world, port):
                                 dict(emb_dim=8, hidden_dim=16, n_cross_layers=1, n_res_blocks=1,
                                      dropout=0.0))
             tr = dcnr.FusedTrainer(m, lr=1e-2, weight_decay=1e-2, shard_optimizer=shard)
-            assert tr.flat.numel() % (64 * world) == 0
-            assert tr.m.numel() == tr.flat.numel() // (world if shard else 1)
+            assert tr.flat.numel() % (64 * world) == 0 and tr.E % (64 * world) == 0
+            # the embedding segment's moments are sharded, the dense segment's whole
+            assert tr.m.numel() == tr.E // (world if shard else 1) + tr.flat.numel() - tr.E
             ref_p = tr.flat.clone()
             ref_m = torch.zeros_like(ref_p)
             ref_v = torch.zeros_like(ref_p)
