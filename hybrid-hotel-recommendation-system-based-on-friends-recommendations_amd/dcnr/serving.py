@@ -35,6 +35,7 @@ from .knn import NearestNeighbors
 
 ml_artifacts: Dict[str, Any] = {}
 
+SV_MAX = 4096   # csrc/serving.hip: candidates per union / rank / MMR call
 
 def _dev_table(emb, device):
     """(table fp32 [n, d] on device, inverse row norms [n]) cached per source array."""
@@ -61,10 +62,14 @@ def row_inv_norms(t: torch.Tensor) -> torch.Tensor:
 def mmr_positions(table: torch.Tensor, inv: torch.Tensor, rows: torch.Tensor,
                   scores: torch.Tensor, lambda_param: float, top_k: int = 20) -> torch.Tensor:
     """Device MMR over candidates in ranked order: returns int64 positions
-    (into the ranked list) of the re-ranked items (dcnr_mmr_rerank)."""
+    (into the ranked list) of the re-ranked items (dcnr_mmr_rerank).  At most
+    SV_MAX candidates (one workgroup's LDS holds every candidate's running
+    max-similarity); more raise ValueError."""
     lib = _lib.load()
     dev = table.device
     n = rows.numel()
+    if n > SV_MAX:
+        raise ValueError(f"mmr_positions: {n} candidates exceed the device MMR's {SV_MAX}")
     out = torch.empty(max(1, top_k), dtype=torch.int64, device=dev)
     cnt = torch.zeros(1, dtype=torch.int32, device=dev)
     if n == 0:
@@ -145,12 +150,20 @@ class RankingPipeline:
             return pos
         k = self.n_neighbors
         _, idx = self.index.kneighbors_device(self.index._table[pos], k)
-        out = torch.empty(Q * k, dtype=torch.int64, device=self.device)
-        cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
-        _lib.check(lib.dcnr_candidate_union(pos.data_ptr(), Q, idx.data_ptr(), k, out.data_ptr(),
-                                            cnt.data_ptr(), _lib.stream_ptr(self.device)),
-                   "dcnr_candidate_union")
-        return out[:int(cnt.item())]
+        qc = max(1, SV_MAX // k)     # the union kernel's one-workgroup capacity
+        outs = []
+        for q0 in range(0, Q, qc):   # > SV_MAX entries: per-chunk unions, then merged
+            p_, i_ = pos[q0:q0 + qc].contiguous(), idx[q0:q0 + qc].contiguous()
+            out = torch.empty(p_.numel() * k, dtype=torch.int64, device=self.device)
+            cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
+            _lib.check(lib.dcnr_candidate_union(p_.data_ptr(), p_.numel(), i_.data_ptr(), k,
+                                                out.data_ptr(), cnt.data_ptr(),
+                                                _lib.stream_ptr(self.device)),
+                       "dcnr_candidate_union")
+            outs.append(out[:int(cnt.item())])
+        if len(outs) == 1:
+            return outs[0]
+        return torch.unique(torch.cat(outs))   # ascending distinct rows, as one call gives
 
     def ranking_batch(self, user_row: int, item_rows: torch.Tensor):
         """preprocess_for_ranking (main.py:215-230) on the device."""
@@ -179,9 +192,13 @@ class RankingPipeline:
         return self.model(*self.ranking_batch(user_row, item_rows)).reshape(-1)
 
     def rank(self, scores: torch.Tensor) -> torch.Tensor:
-        """Positions in descending score order, ties by position (main.py:325)."""
+        """Positions in descending score order, ties by position (main.py:325).
+        Above SV_MAX candidates (the LDS sort's capacity) a stable device sort
+        of -score gives the same order."""
         lib = _lib.load()
         n = scores.numel()
+        if n > SV_MAX:
+            return torch.sort(-scores.to(self.device, torch.float32), stable=True).indices
         order = torch.empty(n, dtype=torch.int64, device=self.device)
         if n:
             s = scores.to(torch.float32).contiguous()

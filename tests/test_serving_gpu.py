@@ -34,8 +34,9 @@ def test_mmr_vs_reference_golden(dev):
     assert serving.rerank_with_mmr([], 0.5) == []
 
 
-@pytest.mark.parametrize("n", [1, 7, 300, 4096])
+@pytest.mark.parametrize("n", [1, 7, 300, 4096, 4097, 20000])
 def test_rank_by_score_stable(dev, n):
+    """n <= SV_MAX: the LDS bitonic kernel; above: the stable device sort."""
     from dcnr.serving import RankingPipeline
     rng = np.random.default_rng(n)
     s = rng.integers(-20, 20, n).astype(np.float32) / 4   # many exact ties
@@ -75,6 +76,24 @@ def test_candidate_union_and_batch(dev):
     # /similar_items: kneighbors(n+1)[1:]
     sim = pipe.similar_items(int(pos[0]), 10).cpu().numpy()
     assert sim.tolist() == idx[0, 1:].tolist()
+
+
+def test_candidate_union_above_capacity(dev):
+    """Q*k above SV_MAX (a user with 500 positive hotels, k=11): per-chunk
+    unions merged give exactly the one-shot union; MMR above SV_MAX raises."""
+    from dcnr.serving import SV_MAX, mmr_positions
+    cfg, m, pipe, item_cat, item_num = make_pipeline(dev)
+    emb = m.item_embedding.weight.detach().cpu().numpy()
+    rng = np.random.default_rng(4)
+    pos = rng.choice(cfg["n_items"], 500, replace=False)
+    assert pos.size * pipe.n_neighbors > SV_MAX
+    cand = pipe.candidates(pos).cpu().numpy()
+    _, idx = orc.cosine_kneighbors(emb, emb[pos], 11)
+    assert cand.tolist() == orc.candidate_union(pos, idx).tolist()
+    rows = torch.arange(SV_MAX + 1, device=dev) % cfg["n_items"]
+    with pytest.raises(ValueError):
+        mmr_positions(pipe.index._table, pipe.index._inv, rows,
+                      torch.zeros(SV_MAX + 1, device=dev), 0.5, 5)
 
 
 @pytest.mark.parametrize("lam", [1.0, 0.7, 0.3])
