@@ -173,11 +173,11 @@ __global__ __launch_bounds__(CT) void cross_scalar_reduce_kernel(const float* pa
 // Wave w takes rows w*RW .. w*RW+RW-1 of the block (8 in flight), lane L the
 // 8 columns 8L..8L+7 (one 16-B bf16 / two 16-B fp32 loads per row), 512
 // columns per pass; the waves' sums are added in wave order through LDS.
-template <typename T>
+template <typename T, int V>
 __global__ __launch_bounds__(XA_T) void x0_alpha_kernel(const T* x0, int ldx, int D,
-                                                        const float* alpha, int V, int64_t B,
+                                                        const float* alpha, int64_t B,
                                                         float* part) {
-  constexpr int KM = 8, RW = XA_ROWS / XA_W, U = 8;
+  constexpr int KM = V, RW = XA_ROWS / XA_W, U = 8;
   __shared__ float red[KM][8 * WAVE];
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int64_t r0 = (int64_t)blockIdx.x * XA_ROWS + (int64_t)w * RW;
@@ -351,12 +351,19 @@ dcnr_status cross_backward(const CrossParams& cp, int D, const float* sc, const 
     set_error("cross backward: x0 rows must be 16-B aligned (ld %d)", ldx);
     return DCNR_UNSUPPORTED_SHAPE;
   }
-  if (x0_bf16)
-    hipLaunchKernelGGL(x0_alpha_kernel<bf16>, dim3((unsigned)nx), dim3(XA_T), 0, s,
-                       (const bf16*)x0, ldx, D, alpha, V, B, xpart);
-  else
-    hipLaunchKernelGGL(x0_alpha_kernel<float>, dim3((unsigned)nx), dim3(XA_T), 0, s,
-                       (const float*)x0, ldx, D, alpha, V, B, xpart);
+  switch (V) {
+#define CASE(v)                                                                           \
+  case v:                                                                                 \
+    if (x0_bf16)                                                                          \
+      hipLaunchKernelGGL((x0_alpha_kernel<bf16, v>), dim3((unsigned)nx), dim3(XA_T), 0, s, \
+                         (const bf16*)x0, ldx, D, alpha, B, xpart);                        \
+    else                                                                                  \
+      hipLaunchKernelGGL((x0_alpha_kernel<float, v>), dim3((unsigned)nx), dim3(XA_T), 0, s, \
+                         (const float*)x0, ldx, D, alpha, B, xpart);                       \
+    break;
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
+#undef CASE
+  }
   DCNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(x0_alpha_reduce_kernel, dim3((unsigned)cdiv(V * D, 64)), dim3(64 * RG), 0,
                      s, xpart, nx, V * D, x0a);
