@@ -89,6 +89,48 @@ namespace {
     if (st_ != DCNR_OK) return st_;          \
   } while (0)
 
+// One side stream per device (created on first use, never destroyed) for the
+// backward's work that does not depend on the deep tower; fork/join events
+// per call.
+dcnr_status side_stream(hipStream_t* out) {
+  static std::mutex mu;
+  static hipStream_t streams[64] = {};
+  int dev = 0;
+  DCNR_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) {
+    set_error("side stream: device %d out of range", dev);
+    return DCNR_BAD_ARG;
+  }
+  std::lock_guard<std::mutex> lk(mu);
+  if (!streams[dev]) DCNR_HIP(hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking));
+  *out = streams[dev];
+  return DCNR_OK;
+}
+struct SideJoin {
+  hipStream_t side = nullptr;
+  hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+  dcnr_status fork(hipStream_t s) {
+    TRY(side_stream(&side));
+    DCNR_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
+    DCNR_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
+    DCNR_HIP(hipEventRecord(fork_ev, s));
+    DCNR_HIP(hipStreamWaitEvent(side, fork_ev, 0));
+    return DCNR_OK;
+  }
+  dcnr_status record() {
+    DCNR_HIP(hipEventRecord(join_ev, side));
+    return DCNR_OK;
+  }
+  dcnr_status join(hipStream_t s) {
+    DCNR_HIP(hipStreamWaitEvent(s, join_ev, 0));
+    return DCNR_OK;
+  }
+  ~SideJoin() {
+    if (fork_ev) (void)hipEventDestroy(fork_ev);
+    if (join_ev) (void)hipEventDestroy(join_ev);
+  }
+};
+
 // dcnr_grad_ready_fn of the model desc, if any
 dcnr_status grads_ready(const dcnr_model_desc* desc, int group, hipStream_t s) {
   if (!desc->grad_ready) return DCNR_OK;
@@ -904,6 +946,14 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   for (int t = 0; t < g.n_tab; ++t) {
     eb.grad[t] = Gr.tab[t]; eb.rows[t] = g.rows[t]; eb.width[t] = g.width[t]; eb.off[t] = g.off[t];
   }
+  // The id sort and the cross backward depend on the ids, dz and the
+  // forward's outputs alone: they run on a side stream under the deep-tower
+  // backward and join before the dense-gradient hook.
+  SideJoin sj;
+  TRY(sj.fork(s));
+  const CrossParams cpx = make_cross(d, P);
+  {
+  hipStream_t s = sj.side;   // TRYB launches and times on the side stream
   TRYB(DCNR_K_EMB_SORT, 2.0 * 8.0 * g.n_tab * B + 8.0 * B * (2 + d.K) + 4.0 * B * 2,
        emb_sort(eb, user_ids, item_ids, cat_features, B, L.emb, s));
   // ---- cross network + head bias (low-rank form, from the forward's
@@ -913,11 +963,12 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   for (int l = 0; l < d.L; ++l) { cg.dw[l] = Gr.cw[l]; cg.db[l] = Gr.cb[l]; }
   cg.dwf_cross = Gr.wf + H;
   cg.dbf = Gr.bf;
-  const CrossParams cpx = make_cross(d, P);
   TRYB(DCNR_K_CROSS_BWD, (double)B * (4.0 * (2 * d.L + 1) + 4.0 + 8.0 * (d.L + 1)) +
                              (double)B * d.Dp * d.es,
        cross_backward(cpx, d.D, L.sc, dz, L.x0, d.prec == DCNR_PREC_BF16, d.Dp, B, cg, L.xcoef,
                       L.xalpha, L.cscratch, L.cscratch_bytes, accumulate, s));
+  }
+  TRY(sj.record());
 
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   const bool fuse = epi_stats_ok(d);   // BN partials from the dX GEMM epilogues
@@ -995,6 +1046,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   TRYB(DCNR_K_ROWWISE, act_b(d, B), col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
   TRY(bias_reduce(d, L, nc, Gr.b0, accumulate, s));
   TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s));
+  TRY(sj.join(s));   // the side stream's cross gradients, coefficients and sorted ids
   TRY(grads_ready(desc, DCNR_GRADS_DENSE, s));   // every non-embedding gradient is enqueued
   {
     GemmArgs g;
