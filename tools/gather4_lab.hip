@@ -139,73 +139,6 @@ int main() {
     for (int64_t i = 0; i < B; ++i) zw = std::max(zw, (double)std::fabs(za[i] - zb[i]) / std::max(1.f, std::fabs(zb[i])));
     printf("cfg3 check: x0 bf16 mismatches %ld, zc max rel diff %.2e\n", nx, zw);
   }
-  // ---- 3. backward: cross recompute + backward + embedding-grad scatter, new vs old
-  {
-    const int64_t B = 131072;
-    dcnr::CrossBwdParams p;
-    std::memset(&p, 0, sizeof(p));
-    p.cp = cp;
-    float* gb; CK(hipMalloc(&gb, 2 * ((2 * L + 1) * D + 64) * 4));
-    float* gb2 = gb + (2 * L + 1) * D + 64;
-    std::vector<float*> gt(14), gt2(14);
-    for (int t = 0; t < g.n_tab; ++t) {
-      CK(hipMalloc(&gt[t], rows[t] * E * 4)); CK(hipMalloc(&gt2[t], rows[t] * E * 4));
-    }
-    auto setp = [&](float* base, std::vector<float*>& tabs) {
-      for (int l = 0; l < L; ++l) { p.dw[l] = base + l * D; p.db[l] = base + (L + l) * D; }
-      p.dwf_cross = base + 2 * L * D; p.dbf = base + (2 * L + 1) * D;
-      for (int t = 0; t < 14; ++t) p.emb_grad[t] = tabs[t];
-    };
-    float *dx0, *dzv; CK(hipMalloc(&dx0, B * ldx * 4)); CK(hipMalloc(&dzv, B * 4));
-    std::vector<float> hdx(B * ldx);
-    for (auto& v : hdx) v = 0.01f * U(rng);
-    {
-      CK(hipMemcpy(dx0, hdx.data(), B * ldx * 4, hipMemcpyHostToDevice));
-      std::vector<float> hz(B);
-      for (auto& v : hz) v = 1e-3f * U(rng);
-      CK(hipMemcpy(dzv, hz.data(), B * 4, hipMemcpyHostToDevice));
-    }
-    dcnr::CrossBwdScratch ws;
-    ws.part_elems = dcnr::cross_bwd_part_elems(D, L); CK(hipMalloc(&ws.part, ws.part_elems * 4));
-    ws.red2_elems = dcnr::cross_red2_elems(D, L); CK(hipMalloc(&ws.red2, ws.red2_elems * 4));
-    ws.n_counters = 512; CK(hipMalloc(&ws.counters, 512 * 4)); CK(hipMemset(ws.counters, 0, 2048));
-    auto zero = [&](std::vector<float*>& tabs) {
-      for (int t = 0; t < 14; ++t) (void)hipMemsetAsync(tabs[t], 0, rows[t] * E * 4, 0);
-    };
-    setp(gb, gt);
-    auto bwd_new = [&] { dcnr::cross_bwd_scatter(g, p, u, it, c, num, dzv, B, dx0, ldx, ws, 0, 0); };
-    double us_new = time_us(bwd_new, 20);
-    setp(gb2, gt2);
-    auto bwd_old = [&] {
-      const int64_t nb = dcnr::bwd_blocks(B);
-      dcnr::dispatch_bwd_L<8>(L, g, p, u, it, c, num, dzv, B, dx0, ldx, ws.part, nb, 0);
-      hipLaunchKernelGGL(dcnr::cross_reduce_kernel, dim3((unsigned)dcnr::cross_red_groups(D, L), dcnr::RED_G),
-                         dim3(dcnr::NT), 0, 0, ws.part, (int)nb, D, L, p, ws.red2, ws.counters, 0);
-    };
-    double us_old = time_us(bwd_old, 20);
-    printf("cross_bwd          B=%ld  v4 %7.1f us   old %7.1f us  (incl. partial reduce)\n", (long)B,
-           us_new, us_old);
-    // one clean run of each, then compare
-    CK(hipMemcpy(dx0, hdx.data(), B * ldx * 4, hipMemcpyHostToDevice));
-    setp(gb, gt); zero(gt); bwd_new();
-    CK(hipMemcpy(dx0, hdx.data(), B * ldx * 4, hipMemcpyHostToDevice));
-    setp(gb2, gt2); zero(gt2); bwd_old();
-    CK(hipDeviceSynchronize());
-    std::vector<float> a((2 * L + 1) * D + 1), bb((2 * L + 1) * D + 1);
-    CK(hipMemcpy(a.data(), gb, a.size() * 4, hipMemcpyDeviceToHost));
-    CK(hipMemcpy(bb.data(), gb2, bb.size() * 4, hipMemcpyDeviceToHost));
-    double wd = 0, nd = 0;
-    for (size_t k = 0; k < a.size(); ++k) { wd += (a[k] - bb[k]) * (double)(a[k] - bb[k]); nd += (double)bb[k] * bb[k]; }
-    printf("bwd check: dense grads norm-rel diff %.2e\n", std::sqrt(wd / nd));
-    double we = 0, ne = 0;
-    for (int t : {0, 2, 13}) {
-      std::vector<float> x(rows[t] * E), y(rows[t] * E);
-      CK(hipMemcpy(x.data(), gt[t], x.size() * 4, hipMemcpyDeviceToHost));
-      CK(hipMemcpy(y.data(), gt2[t], y.size() * 4, hipMemcpyDeviceToHost));
-      for (size_t k = 0; k < x.size(); ++k) { we += (x[k] - y[k]) * (double)(x[k] - y[k]); ne += (double)y[k] * y[k]; }
-    }
-    printf("bwd check: emb grads (user, cat0) norm-rel diff %.2e\n", std::sqrt(we / ne));
-  }
   CK(hipDeviceSynchronize());
   printf("status %s\n", hipGetErrorString(hipGetLastError()));
   return 0;

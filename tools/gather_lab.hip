@@ -66,33 +66,6 @@ int main(int argc, char** argv) {
   const double us = ms * 1e3 / iters;
   printf("gather mode %d  B=%ld  %.1f us  %.2f TB/s of 2852 B/sample\n", GC_LAB_MODE, (long)B, us,
          2852.0 * B / us / 1e6);
-  // backward: cross + embedding scatter (user/item atomics, cat tables privatised)
-  dcnr::CrossBwdParams p;
-  std::memset(&p, 0, sizeof(p));
-  p.cp = cp;
-  float* gb; (void)hipMalloc(&gb, (2 * L + 1) * D * 4 + 64);
-  for (int l = 0; l < L; ++l) { p.dw[l] = gb + l * D; p.db[l] = gb + (L + l) * D; }
-  p.dwf_cross = gb + 2 * L * D; p.dbf = gb + (2 * L + 1) * D;
-  for (int t = 0; t < g.n_tab; ++t) {
-    float* gt; (void)hipMalloc(&gt, rows[t] * E * 4); (void)hipMemset(gt, 0, rows[t] * E * 4);
-    p.emb_grad[t] = gt;
-  }
-  float *dx0, *dzv; (void)hipMalloc(&dx0, B * ldx * 4); (void)hipMalloc(&dzv, B * 4);
-  (void)hipMemset(dx0, 0, B * ldx * 4); (void)hipMemset(dzv, 0, B * 4);
-  dcnr::CrossBwdScratch ws;
-  ws.part_elems = dcnr::cross_bwd_part_elems(D, L); (void)hipMalloc(&ws.part, ws.part_elems * 4);
-  ws.red2_elems = dcnr::cross_red2_elems(D, L); (void)hipMalloc(&ws.red2, ws.red2_elems * 4);
-  ws.n_counters = 512; (void)hipMalloc(&ws.counters, 512 * 4); (void)hipMemset(ws.counters, 0, 2048);
-  auto bwd = [&] {
-    dcnr::cross_bwd_scatter(g, p, u, it, c, num, dzv, B, dx0, ldx, ws, 0, 0);
-  };
-  for (int i = 0; i < 2; ++i) bwd();
-  (void)hipEventRecord(e0, 0);
-  for (int i = 0; i < iters; ++i) bwd();
-  (void)hipEventRecord(e1, 0);
-  (void)hipEventSynchronize(e1);
-  (void)hipEventElapsedTime(&ms, e0, e1);
-  printf("cross_bwd mode %d  %.1f us\n", GC_LAB_MODE, ms * 1e3 / iters);
   (void)hipDeviceSynchronize();
   printf("status %s\n", hipGetErrorString(hipGetLastError()));
   return 0;
