@@ -67,10 +67,17 @@ __device__ __forceinline__ void ldc(const float* p, float (&o)[V]) {
 // Generic row x column-group driver.  Each thread owns V consecutive columns
 // (c0 = cg*V) and walks rows rsub, rsub+rpp, ... of its block's chunk, U rows
 // per step (all loads first).  NK > 0: per-column partial sums per chunk.
+// rows in flight per thread: UNROLL, or 2 for the bf16 BN apply / backward
+// ops (several operands + per-column constants per row: at 4 rows they take
+// 99-172 VGPRs, 2-4 waves/SIMD).  Same-box A/B (gpurun_out/r02r, r02s): the
+// rowwise class 1.315 -> 1.226 ms/step, the step 4.21 -> 4.18 ms.
+template <class Op> struct RowUnroll { static constexpr int v = UNROLL; };
+
 template <typename T, int NK, class Op>
 __global__ __launch_bounds__(NT) void rowcol_kernel(Op op, int64_t B, int N, int rows_per_chunk,
                                                     float* part) {
   constexpr int V = VE<T>;
+  constexpr int UNROLL = RowUnroll<Op>::v;
   constexpr int NKA = NK > 0 ? NK : 1;
   const int tcols = (N + V - 1) / V;
   const int rpp = NT / tcols;
@@ -370,6 +377,13 @@ template <typename T> struct Bwd1ApplyOp {
     stv<T>(dt + r * ld + c, q.a);
   }
 };
+
+template <typename T, bool G> struct RowUnroll<Bwd2StatsOp<T, G>> { static constexpr int v = 2; };
+template <typename T> struct RowUnroll<BnAddReluHeadOp<T>> { static constexpr int v = 2; };
+template <typename T> struct RowUnroll<Bwd1ApplyOp<T>> { static constexpr int v = 2; };
+template <typename T> struct RowUnroll<Bwd2ApplyOp<T>> { static constexpr int v = 2; };
+template <typename T> struct RowUnroll<BnAddReluOp<T>> { static constexpr int v = 2; };
+template <typename T> struct RowUnroll<BnReluDropOp<T>> { static constexpr int v = 2; };
 
 // ------------------------------------------------------------ small kernels
 __global__ void bn_finalize_kernel(const double* sums, int N, int Nr, int train, BnFinal f) {
