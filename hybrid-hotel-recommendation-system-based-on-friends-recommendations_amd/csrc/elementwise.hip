@@ -477,26 +477,50 @@ __global__ void splitk_reduce_kernel(const float* slab, int splits, int64_t stri
   out[i] = accumulate ? out[i] + s : s;
 }
 
+// fp32 weights -> padded T copies [rows_p][ld] (8 columns = one 16-B (bf16)
+// or two 16-B (fp32) stores per thread) and, for the backward, transposes
+// [cols_p][ld_t] through 64x64 LDS tiles (coalesced reads and writes).
 template <typename T>
-__global__ void pack_kernel(PackBatch pb) {
+__global__ __launch_bounds__(NT) void pack_kernel(PackBatch pb) {
   const PackDesc& d = pb.d[blockIdx.y];
   T* dst = (T*)d.dst;
-  int64_t tot = (int64_t)d.rows_p * d.ld;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    int r = (int)(i / d.ld), c = (int)(i % d.ld);
-    float v = (r < d.rows && c < d.cols) ? d.src[(int64_t)r * d.cols + c] : 0.f;
-    St<T>::st(dst + i, v);
-  }
-  if (d.dst_t) {
-    T* dt = (T*)d.dst_t;
-    int64_t tot2 = (int64_t)d.cols_p * d.ld_t;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < tot2;
-         i += (int64_t)gridDim.x * blockDim.x) {
-      int c = (int)(i / d.ld_t), r = (int)(i % d.ld_t);
-      float v = (r < d.rows && c < d.cols) ? d.src[(int64_t)r * d.cols + c] : 0.f;
-      St<T>::st(dt + i, v);
+  const int cg = d.ld >> 3;
+  const int tot = d.rows_p * cg;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < tot; i += gridDim.x * NT) {
+    const int r = i / cg, c0 = (i - r * cg) * 8;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int c = c0 + k;
+      v[k] = (r < d.rows && c < d.cols) ? d.src[(int64_t)r * d.cols + c] : 0.f;
     }
+    T* p = dst + (int64_t)r * d.ld + c0;
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 h;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h[k] = (bf16)v[k];
+      *reinterpret_cast<bf16x8*>(p) = h;
+    } else {
+      *reinterpret_cast<f32x4*>(p) = f32x4{v[0], v[1], v[2], v[3]};
+      *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
+    }
+  }
+  if (!d.dst_t) return;
+  __shared__ float tile[64][65];
+  T* dt = (T*)d.dst_t;
+  const int tr = (d.ld_t + 63) / 64, tc = (d.cols_p + 63) / 64;
+  for (int t = blockIdx.x; t < tr * tc; t += gridDim.x) {
+    const int r0 = (t / tc) * 64, c0 = (t % tc) * 64;
+    for (int k = threadIdx.x; k < 64 * 64; k += NT) {
+      const int rr = k >> 6, cc = k & 63, r = r0 + rr, c = c0 + cc;
+      tile[rr][cc] = (r < d.rows && c < d.cols) ? d.src[(int64_t)r * d.cols + c] : 0.f;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < 64 * 64; k += NT) {
+      const int cc = k >> 6, rr = k & 63, r = r0 + rr, c = c0 + cc;
+      if (c < d.cols_p && r < d.ld_t) St<T>::st(dt + (int64_t)c * d.ld_t + r, tile[rr][cc]);
+    }
+    __syncthreads();
   }
 }
 
@@ -663,6 +687,11 @@ dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, 
 // ================================================================== API
 dcnr_status pack_weights(int precision, const PackBatch& pb, hipStream_t s) {
   if (pb.n == 0) return DCNR_OK;
+  for (int i = 0; i < pb.n; ++i)
+    if (pb.d[i].ld % 8) {
+      set_error("pack: leading dimension %d not a multiple of 8", pb.d[i].ld);
+      return DCNR_UNSUPPORTED_SHAPE;
+    }
   dim3 grid(64, pb.n);
   if (precision == DCNR_PREC_BF16) hipLaunchKernelGGL(pack_kernel<bf16>, grid, dim3(NT), 0, s, pb);
   else hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(NT), 0, s, pb);
