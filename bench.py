@@ -323,8 +323,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-serving", action="store_true", help="skip the configs[4] top-k leg")
     ap.add_argument("--exchange", default="dense", choices=["dense", "sparse"],
-                    help="N>1 gradient exchange: dense = reduce-scatter/all-gather of the flat "
-                         "gradient (sharded AdamW); sparse = owner-bucketed user-table rows + "
+                    help="N>1 gradient exchange: dense = the dense parameters' all-reduce "
+                         "started inside the backward + reduce-scatter / sharded AdamW / "
+                         "all-gather of the tables; sparse = owner-bucketed user-table rows + "
                          "all-reduce of the rest")
     args = ap.parse_args()
 
@@ -490,7 +491,8 @@ def main():
                        "deep": "3 cross + 4 x 512 residual", "parallelism": f"dp{world}",
                        "exchange": "none" if world == 1 else (
                            "sparse user rows + all-reduce" if args.exchange == "sparse"
-                           else "reduce-scatter + sharded AdamW + all-gather")},
+                           else "dense params: all-reduce started in the backward (overlapped); "
+                                "tables: reduce-scatter + sharded AdamW + all-gather")},
             "scored_pairs_per_sec": pairs_per_s,
             "final_loss": final_loss,
             "roofline": roof,
