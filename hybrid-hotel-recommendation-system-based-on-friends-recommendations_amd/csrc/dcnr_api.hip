@@ -349,7 +349,7 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
       L.emb.vals = (uint32_t*)b.take((size_t)n * 4);
       L.emb.keys_s = (uint32_t*)b.take((size_t)n * 4);
       L.emb.vals_s = (uint32_t*)b.take((size_t)n * 4);
-      L.emb.tmp_bytes = emb_sort_tmp_bytes(d.rows, 2 + d.K, B);
+      L.emb.tmp_bytes = emb_sort_tmp_bytes(d.rows, d.widths, 2 + d.K, B);
       L.emb.tmp = b.take(L.emb.tmp_bytes);
     }
     for (int j = 0; j < d.R; ++j) {

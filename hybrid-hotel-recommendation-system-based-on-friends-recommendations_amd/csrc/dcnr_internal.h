@@ -428,9 +428,9 @@ struct EmbSortBufs {
   uint32_t *ids;                 // [n_tab * B] clamped ids, table-major
   uint32_t *keys, *vals;         // [n_tab * B] level-1 sorted (tables of > 1024 rows)
   uint32_t *keys_s, *vals_s;     // sorted
-  void* tmp; size_t tmp_bytes;   // per-(bucket, chunk) counts / offsets of the sort
+  void* tmp; size_t tmp_bytes;   // sort counts / offsets, then the huge-run pieces
 };
-size_t emb_sort_tmp_bytes(const int64_t* rows, int n_tab, int64_t B);
+size_t emb_sort_tmp_bytes(const int64_t* rows, const int* width, int n_tab, int64_t B);
 dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* item,
                      const int64_t* cat, int64_t B, const EmbSortBufs& sb, hipStream_t s);
 // grad row r of table t = sum over its samples of dx0_deep[b][off_t:off_t+w_t]

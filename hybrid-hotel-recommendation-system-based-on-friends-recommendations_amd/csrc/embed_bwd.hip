@@ -19,8 +19,11 @@
 //      entries sequentially and writes the row; emb_runs_long_kernel: the
 //      wave whose 64 positions hold the head of a longer run (popular ids,
 //      small categorical tables) reduces it (entries strided over lane
-//      slots, slots combined in fixed lane order).  No global counters or
-//      lists: a device-scope atomic per long run (12000 at the bench size)
+//      slots, slots combined in fixed lane order).  Runs of more than HSEG
+//      entries are cut at the global HSEG-position grid: one wave per
+//      segment sums its pieces (long kernel), the wave of the segment where
+//      the run starts adds them in order (short kernel).  No global counters
+//      or lists: a device-scope atomic per long run (12000 at the bench size)
 //      serialised at memory and cost ~100 us.
 //
 // Step 3 reads, per (sample, table) entry, the table's segment of the deep
@@ -420,6 +423,10 @@ template <> struct Vec<4> {
   }
 };
 
+template <int NV>
+__device__ void emb_huge_final(const EmbTabs& et, int64_t B, int64_t n, int64_t g,
+                               const float* hp, int hps, int accumulate, int lane);
+
 // One thread per sorted position; the head of a run of <= LIM entries sums
 // it in ascending sample order: the deep dx0 segments and the NV cross
 // coefficients, then row = deep + sum_k csum_k V_k.  Latency, not bandwidth,
@@ -432,13 +439,21 @@ __global__ __launch_bounds__(ENT) void emb_runs_short_kernel(EmbTabs et, int nt,
                                                              const uint32_t* ks,
                                                              const uint32_t* vs,
                                                              const float* dx0, int ld,
-                                                             const float* coef, int accumulate) {
+                                                             const float* coef,
+                                                             const float* hp, int hps,
+                                                             int64_t nseg, int accumulate) {
   typedef Vec<VEC> V;
   typedef typename V::T T;
   constexpr int UNR = 16 / VEC;   // 16 columns per pass
   constexpr int EG = 2;           // entries whose loads are in flight together
   const int64_t i = (int64_t)blockIdx.x * ENT + threadIdx.x;
-  if (i >= (int64_t)nt * B) return;
+  const int64_t n = (int64_t)nt * B, nbh = (n + ENT - 1) / ENT;   // head-position blocks
+  if ((int64_t)blockIdx.x >= nbh) {   // huge-run finalisation waves
+    const int64_t g = ((int64_t)blockIdx.x - nbh) * (ENT / WAVE) + (threadIdx.x >> 6);
+    if (g < nseg) emb_huge_final<NV>(et, B, n, g, hp, hps, accumulate, threadIdx.x & 63);
+    return;
+  }
+  if (i >= n) return;
   const int t = (int)(i / B);
   const int64_t t0 = (int64_t)t * B, t1 = t0 + B;
   const uint32_t k = ks[i];
@@ -508,37 +523,229 @@ __global__ __launch_bounds__(ENT) void emb_runs_short_kernel(EmbTabs et, int nt,
   }
 }
 
-// One wave per long run, walked WAVE entries at a time: lane L holds entry
-// p+L's key and sample (coalesced loads, the next block's issued before this
-// block's dx0 rows), the column groups of VEC sit across lanes and the
-// block's entries across the remaining S = 64/Gb lane slots (slot s takes
-// entries s, s+S, ... of every block, summing their deep segments and cross
-// coefficients in ascending order), slots added in ascending order, then
-// row = deep + sum_k csum_k V_k.  The wave owning the run's head position
-// (64 positions per wave) reduces it.  SPLIT (every column block has
-// Gb >= NV groups): lane (slot, cg < NV) sums coefficient cg of its slot's
-// entries, instead of every lane summing all NV (fewer loads and registers;
-// same order, same result).
+// Sums over the entries [lo, hi) of run k (table t), walked WAVE entries at
+// a time from lo: lane L holds entry p+L's key and sample (coalesced loads,
+// the next block's issued before this block's dx0 rows), the column groups
+// of VEC (column block cb) sit across lanes and the block's entries across
+// the remaining S = 64/Gb lane slots (slot s takes entries s, s+S, ... of
+// every block, summing their deep segments and cross coefficients in
+// ascending order), slots added in ascending order.  Returns, in the slot-0
+// lanes, the deep sum of their columns (tot) and in every lane the NV
+// coefficient sums (ctot).  SPLIT (Gb >= NV): lane (slot, cg < NV) sums
+// coefficient cg of its slot's entries instead of every lane summing all NV.
+template <int VEC, int NV, bool SPLIT>
+__device__ __forceinline__ void piece_sums(const EmbTabs& et, int t, uint32_t k, int64_t lo,
+                                           int64_t hi, const uint32_t* ks, const uint32_t* vs,
+                                           const float* dx0, int ld, const float* coef, int cb,
+                                           int lane, typename Vec<VEC>::T& tot,
+                                           float (&ctot)[NV]) {
+  typedef Vec<VEC> V;
+  typedef typename V::T T;
+  constexpr int QMAX = 8;   // entries per slot per block held in flight (S >= 8)
+  const int G = et.width[t] / VEC;
+  const float* src = dx0 + et.off[t];
+  const int Gb = G - cb < WAVE ? G - cb : WAVE;
+  const int S = WAVE / Gb, slot = lane / Gb, cg = lane - slot * Gb;
+  const int col = (cb + cg) * VEC;
+  const bool act = slot < S;
+  T acc = V::zero();
+  float csum[SPLIT ? 1 : NV];
+#pragma unroll
+  for (int v = 0; v < (SPLIT ? 1 : NV); ++v) csum[v] = 0.f;
+  int64_t p = lo;
+  uint32_t kn = p + lane < hi ? ks[p + lane] : ~0u;
+  uint32_t sn = p + lane < hi ? vs[p + lane] : 0u;
+  for (;;) {
+    const int nb = __popcll(__ballot(kn == k));   // the piece's entries in this block: a prefix
+    const int smp = (int)sn;
+    const int64_t pn = p + WAVE;
+    if (nb == WAVE) {   // the piece may go on: fetch the next block now
+      kn = pn + lane < hi ? ks[pn + lane] : ~0u;
+      sn = pn + lane < hi ? vs[pn + lane] : 0u;
+    }
+    for (int q0 = 0; S * q0 < WAVE; q0 += QMAX) {   // uniform trip count
+      T x[QMAX];
+      float cf[QMAX][SPLIT ? 1 : NV];
+#pragma unroll
+      for (int q = 0; q < QMAX; ++q) {
+        const int j = slot + S * (q0 + q);
+        const int b = __shfl(smp, j & 63);
+        const bool ok = act && j < nb;
+        x[q] = ok ? V::ld(src + (int64_t)b * ld + col) : V::zero();
+        if constexpr (SPLIT)
+          cf[q][0] = ok && cg < NV ? coef[(int64_t)b * NV + cg] : 0.f;
+        else
+#pragma unroll
+          for (int v = 0; v < NV; ++v) cf[q][v] = ok ? coef[(int64_t)b * NV + v] : 0.f;
+      }
+#pragma unroll
+      for (int q = 0; q < QMAX; ++q)
+        if (act && slot + S * (q0 + q) < nb) {
+          acc += x[q];
+#pragma unroll
+          for (int v = 0; v < (SPLIT ? 1 : NV); ++v) csum[v] += cf[q][v];
+        }
+    }
+    if (nb < WAVE) break;
+    p = pn;
+  }
+  tot = acc;
+  constexpr int NC = SPLIT ? 1 : NV;
+#pragma unroll
+  for (int v = 0; v < NC; ++v) ctot[v] = csum[v];
+  for (int s = 1; s < S; ++s) {   // wave-uniform trip count
+    const int src_l = (s * Gb + cg) & 63;
+    const T o = V::shfl(acc, src_l);
+    float oc[NC];
+#pragma unroll
+    for (int v = 0; v < NC; ++v) oc[v] = __shfl(csum[v], src_l);
+    if (slot == 0) {
+      tot += o;
+#pragma unroll
+      for (int v = 0; v < NC; ++v) ctot[v] += oc[v];
+    }
+  }
+  if constexpr (SPLIT) {   // coefficient v's total sits in lane v (slot 0, cg v)
+    const float mine = ctot[0];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) ctot[v] = __shfl(mine, v);
+  } else {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) ctot[v] = __shfl(ctot[v], 0);
+  }
+}
+
+// Huge runs (> HSEG entries, e.g. one id taking a large share of the batch)
+// are cut at the global HSEG-position segment boundaries: the wave of segment
+// g writes the partial sums of the (at most two) huge-run pieces inside it
+// to hp[g][slot] = {key, run start, run end, NV coefficient sums, w deep
+// sums}; the wave of the segment where a huge run starts adds its pieces in
+// segment order (emb_huge_final, run by the short kernel's extra waves).
+constexpr int HSEG = 2048;
+
+__device__ __forceinline__ int64_t lower_key(const uint32_t* ks, int64_t lo, int64_t hi, uint32_t k) {
+  while (lo < hi) {   // first position in [lo, hi) with key >= k
+    const int64_t mid = (lo + hi) >> 1;
+    if (ks[mid] < k) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+template <int VEC, int NV, bool SPLIT>
+__device__ void emb_huge_partial(const EmbTabs& et, int64_t B, int64_t n, int64_t g,
+                                 const uint32_t* ks, const uint32_t* vs, const float* dx0,
+                                 int ld, const float* coef, float* hp, int hps, int lane) {
+  typedef typename Vec<VEC>::T T;
+  const int64_t s0 = g * HSEG, s1 = min(n, s0 + HSEG);
+  for (int slot = 0; slot < 2; ++slot) {
+    float* out = hp + (g * 2 + slot) * (int64_t)hps;
+    uint32_t* hdr = reinterpret_cast<uint32_t*>(out);
+    const int64_t p = slot == 0 ? s0 : s1 - 1;
+    const uint32_t k = ks[p];
+    const int t = (int)(p / B);
+    const int64_t t0 = (int64_t)t * B, t1 = t0 + B;
+    bool cand = !(slot == 1 && k == ks[s0]);   // the same run as slot 0
+    // a run longer than HSEG through p reaches p - HSEG/2 or p + HSEG/2
+    if (cand) {
+      const bool l = p - HSEG / 2 >= t0 && ks[p - HSEG / 2] == k;
+      const bool r = p + HSEG / 2 < t1 && ks[p + HSEG / 2] == k;
+      cand = l || r;
+    }
+    int64_t rs = 0, re = 0;
+    if (cand) {
+      rs = lower_key(ks, t0, p, k);
+      re = lower_key(ks, p + 1, t1, k + 1);
+      cand = re - rs > HSEG;
+    }
+    if (!cand) {
+      if (lane == 0) hdr[0] = ~0u;
+      continue;
+    }
+    const int64_t lo = max(rs, s0), hi = min(re, s1);
+    const int G = et.width[t] / VEC;
+    for (int cb = 0; cb < G; cb += WAVE) {
+      T tot;
+      float ctot[NV];
+      piece_sums<VEC, NV, SPLIT>(et, t, k, lo, hi, ks, vs, dx0, ld, coef, cb, lane, tot, ctot);
+      const int Gb = G - cb < WAVE ? G - cb : WAVE;
+      if (lane < Gb) Vec<VEC>::st(out + 3 + 8 + (cb + lane) * VEC, tot);
+      if (cb == 0 && lane < NV) out[3 + lane] = ctot[lane];
+    }
+    if (lane == 0) { hdr[0] = k; hdr[1] = (uint32_t)rs; hdr[2] = (uint32_t)re; }
+  }
+}
+
+// the wave of segment g finalises every huge run that starts inside it
+template <int NV>
+__device__ void emb_huge_final(const EmbTabs& et, int64_t B, int64_t n, int64_t g,
+                               const float* hp, int hps, int accumulate, int lane) {
+  for (int slot = 0; slot < 2; ++slot) {
+    const float* in = hp + (g * 2 + slot) * (int64_t)hps;
+    const uint32_t* hdr = reinterpret_cast<const uint32_t*>(in);
+    const uint32_t k = hdr[0];
+    if (k == ~0u) continue;
+    const int64_t rs = hdr[1], re = hdr[2];
+    if (rs < g * HSEG) continue;   // starts in an earlier segment
+    const int t = (int)(rs / B);
+    const int w = et.width[t];
+    const int64_t g1 = (re - 1) / HSEG;
+    float* dst = et.grad[t] + (int64_t)(k - et.base[t]) * w;
+    float csum = 0.f;   // lane v < NV: coefficient v
+    for (int c0 = 0; c0 < w; c0 += WAVE) {
+      const int c = c0 + lane;
+      float acc = 0.f;
+      for (int64_t gg = g; gg <= g1; ++gg) {   // pieces in segment order
+        const float* pc = hp + (gg * 2) * (int64_t)hps;
+        if (reinterpret_cast<const uint32_t*>(pc)[0] != k) pc += hps;   // its slot 1
+        if (c < w) acc += pc[3 + 8 + c];
+        if (c0 == 0 && lane < NV) csum += pc[3 + lane];
+      }
+      float cs[NV];
+#pragma unroll
+      for (int v = 0; v < NV; ++v) cs[v] = __shfl(csum, v);
+      if (c < w) {
+        float r = acc;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) r = Vec<1>::axpy(r, cs[v], et.V[v][et.off[t] + c]);
+        dst[c] = accumulate ? dst[c] + r : r;
+      }
+    }
+  }
+}
+
+// One wave per long run (LIM < length <= HSEG); the wave owning the run's
+// head position (64 positions per wave) reduces it with piece_sums and writes
+// row = deep + sum_k csum_k V_k.  Blocks past the head-position range are the
+// huge-run partial waves (one per HSEG segment).
 template <int VEC, int NV, bool SPLIT>
 __global__ __launch_bounds__(ENT) void emb_runs_long_kernel(EmbTabs et, int64_t B, int64_t n,
                                                             const uint32_t* ks,
                                                             const uint32_t* vs,
                                                             const float* dx0, int ld,
-                                                            const float* coef, int accumulate) {
+                                                            const float* coef, float* hp,
+                                                            int hps, int64_t nseg,
+                                                            int accumulate) {
   typedef Vec<VEC> V;
   typedef typename V::T T;
-  constexpr int QMAX = 8;   // entries per slot per block held in flight (S >= 8)
   const int lane = threadIdx.x & 63;
-  // this wave's 64 positions: which start a run longer than LIM
-  const int64_t base = ((int64_t)blockIdx.x * (ENT / WAVE) + (threadIdx.x >> 6)) * WAVE;
+  const int64_t wave = (int64_t)blockIdx.x * (ENT / WAVE) + (threadIdx.x >> 6);
+  const int64_t nwh = (n + WAVE - 1) / WAVE;   // head-position waves
+  if (wave >= nwh) {
+    if (wave - nwh < nseg)
+      emb_huge_partial<VEC, NV, SPLIT>(et, B, n, wave - nwh, ks, vs, dx0, ld, coef, hp, hps, lane);
+    return;
+  }
+  // this wave's 64 positions: which start a run longer than LIM (not huge)
+  const int64_t base = wave * WAVE;
   bool head = false;
   {
     const int64_t i = base + lane;
     if (i < n) {
       const int t = (int)(i / B);
-      const int64_t t0 = (int64_t)t * B;
+      const int64_t t0 = (int64_t)t * B, t1 = t0 + B;
       const uint32_t k = ks[i];
-      head = (i == t0 || ks[i - 1] != k) && i + LIM < t0 + B && ks[i + LIM] == k;
+      head = (i == t0 || ks[i - 1] != k) && i + LIM < t1 && ks[i + LIM] == k &&
+             !(i + HSEG < t1 && ks[i + HSEG] == k);
     }
   }
   for (uint64_t hm = __ballot(head); hm; hm &= hm - 1) {
@@ -547,77 +754,14 @@ __global__ __launch_bounds__(ENT) void emb_runs_long_kernel(EmbTabs et, int64_t 
     const int t = (int)(i / B);
     const int64_t t1 = (int64_t)(t + 1) * B;
     const int w = et.width[t], G = w / VEC;
-    const float* src = dx0 + et.off[t];
     float* dst = et.grad[t] + (int64_t)(k - et.base[t]) * w;
     for (int cb = 0; cb < G; cb += WAVE) {
-      const int Gb = G - cb < WAVE ? G - cb : WAVE;
-      const int S = WAVE / Gb, slot = lane / Gb, cg = lane - slot * Gb;
-      const int col = (cb + cg) * VEC;
-      const bool act = slot < S;
-      T acc = V::zero();
-      float csum[SPLIT ? 1 : NV];
-#pragma unroll
-      for (int v = 0; v < (SPLIT ? 1 : NV); ++v) csum[v] = 0.f;
-      int64_t p = i;
-      uint32_t kn = p + lane < t1 ? ks[p + lane] : ~0u;
-      uint32_t sn = p + lane < t1 ? vs[p + lane] : 0u;
-      for (;;) {
-        const int nb = __popcll(__ballot(kn == k));   // the run's entries in this block: a prefix
-        const int smp = (int)sn;
-        const int64_t pn = p + WAVE;
-        if (nb == WAVE) {   // the run may go on: fetch the next block now
-          kn = pn + lane < t1 ? ks[pn + lane] : ~0u;
-          sn = pn + lane < t1 ? vs[pn + lane] : 0u;
-        }
-        for (int q0 = 0; S * q0 < WAVE; q0 += QMAX) {   // uniform trip count
-          T x[QMAX];
-          float cf[QMAX][SPLIT ? 1 : NV];
-#pragma unroll
-          for (int q = 0; q < QMAX; ++q) {
-            const int j = slot + S * (q0 + q);
-            const int b = __shfl(smp, j & 63);
-            const bool ok = act && j < nb;
-            x[q] = ok ? V::ld(src + (int64_t)b * ld + col) : V::zero();
-            if constexpr (SPLIT)
-              cf[q][0] = ok && cg < NV ? coef[(int64_t)b * NV + cg] : 0.f;
-            else
-#pragma unroll
-              for (int v = 0; v < NV; ++v) cf[q][v] = ok ? coef[(int64_t)b * NV + v] : 0.f;
-          }
-#pragma unroll
-          for (int q = 0; q < QMAX; ++q)
-            if (act && slot + S * (q0 + q) < nb) {
-              acc += x[q];
-#pragma unroll
-              for (int v = 0; v < (SPLIT ? 1 : NV); ++v) csum[v] += cf[q][v];
-            }
-        }
-        if (nb < WAVE) break;
-        p = pn;
-      }
-      T tot = acc;
-      constexpr int NC = SPLIT ? 1 : NV;
+      T tot;
       float ctot[NV];
-#pragma unroll
-      for (int v = 0; v < NC; ++v) ctot[v] = csum[v];
-      for (int s = 1; s < S; ++s) {   // wave-uniform trip count
-        const int src_l = (s * Gb + cg) & 63;
-        const T o = V::shfl(acc, src_l);
-        float oc[NC];
-#pragma unroll
-        for (int v = 0; v < NC; ++v) oc[v] = __shfl(csum[v], src_l);
-        if (slot == 0) {
-          tot += o;
-#pragma unroll
-          for (int v = 0; v < NC; ++v) ctot[v] += oc[v];
-        }
-      }
-      if constexpr (SPLIT) {   // coefficient v's total sits in lane v (slot 0, cg v)
-        const float mine = ctot[0];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) ctot[v] = __shfl(mine, v);
-      }
-      if (slot == 0) {
+      piece_sums<VEC, NV, SPLIT>(et, t, k, i, t1, ks, vs, dx0, ld, coef, cb, lane, tot, ctot);
+      const int Gb = G - cb < WAVE ? G - cb : WAVE;
+      if (lane < Gb) {   // slot-0 lanes
+        const int col = (cb + lane) * VEC;
         const int xc = et.off[t] + col;
         T r = tot;
 #pragma unroll
@@ -640,9 +784,22 @@ bool vec4_ok(const EmbBwdDesc& e, const float* dx0, int ld) {
 
 }  // namespace
 
-size_t emb_sort_tmp_bytes(const int64_t* rows, int nt, int64_t B) {
+namespace {
+// huge-run piece slots: {key, run start, run end, 8 coefficients, widest row}
+int huge_stride(const int* width, int nt) {
+  int w = 0;
+  for (int t = 0; t < nt; ++t) w = std::max(w, width[t]);
+  return (3 + 8 + w + 3) & ~3;
+}
+int64_t huge_segs(int nt, int64_t B) { return cdiv((int64_t)nt * B, (int64_t)HSEG); }
+}  // namespace
+
+size_t emb_sort_tmp_bytes(const int64_t* rows, const int* width, int nt, int64_t B) {
   const SortPlan p = make_plan(rows, nt, B);
-  return (size_t)p.total_bk * (size_t)std::max(p.C, 1) * 4;
+  // the sort's counts are dead once the sort is done: the sums reuse them
+  // for the huge-run pieces
+  return std::max((size_t)p.total_bk * (size_t)std::max(p.C, 1) * 4,
+                  (size_t)huge_segs(nt, B) * 2 * huge_stride(width, nt) * 4);
 }
 
 dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* item,
@@ -701,30 +858,35 @@ namespace {
 
 template <int VEC, int NV>
 void launch_sums(const EmbTabs& et, int nt, int64_t B, const EmbSortBufs& sb, const float* dx0,
-                 int ld, const float* coef, int accumulate, hipStream_t s) {
-  const int64_t n = (int64_t)nt * B;
-  const dim3 gs((unsigned)cdiv(n, ENT));
-  hipLaunchKernelGGL((emb_runs_short_kernel<VEC, NV>), gs, dim3(ENT), 0, s, et, nt, B, sb.keys_s,
-                     sb.vals_s, dx0, ld, coef, accumulate);
+                 int ld, const float* coef, int hps, int accumulate, hipStream_t s) {
+  const int64_t n = (int64_t)nt * B, nseg = huge_segs(nt, B);
+  float* hp = (float*)sb.tmp;
+  const int wpb = ENT / WAVE;
+  // head-position blocks, then one wave per HSEG segment: the long kernel's
+  // extra waves write the huge-run pieces, the short kernel's add them up
+  const dim3 gl((unsigned)(cdiv(n, (int64_t)ENT) + cdiv(nseg, (int64_t)wpb)));
   bool split = true;   // every column block of every table has >= NV groups
   for (int t = 0; t < nt; ++t) {
     const int G = et.width[t] / VEC, last = G % WAVE;
     if ((G < WAVE && G < NV) || (G >= WAVE && last != 0 && last < NV)) split = false;
   }
   if (split)
-    hipLaunchKernelGGL((emb_runs_long_kernel<VEC, NV, true>), gs, dim3(ENT), 0, s, et, B, n,
-                       sb.keys_s, sb.vals_s, dx0, ld, coef, accumulate);
+    hipLaunchKernelGGL((emb_runs_long_kernel<VEC, NV, true>), gl, dim3(ENT), 0, s, et, B, n,
+                       sb.keys_s, sb.vals_s, dx0, ld, coef, hp, hps, nseg, accumulate);
   else
-    hipLaunchKernelGGL((emb_runs_long_kernel<VEC, NV, false>), gs, dim3(ENT), 0, s, et, B, n,
-                       sb.keys_s, sb.vals_s, dx0, ld, coef, accumulate);
+    hipLaunchKernelGGL((emb_runs_long_kernel<VEC, NV, false>), gl, dim3(ENT), 0, s, et, B, n,
+                       sb.keys_s, sb.vals_s, dx0, ld, coef, hp, hps, nseg, accumulate);
+  hipLaunchKernelGGL((emb_runs_short_kernel<VEC, NV>), gl, dim3(ENT), 0, s, et, nt, B,
+                     sb.keys_s, sb.vals_s, dx0, ld, coef, hp, hps, nseg, accumulate);
 }
 
 template <int VEC>
 void launch_sums_nv(int nv, const EmbTabs& et, int nt, int64_t B, const EmbSortBufs& sb,
-                    const float* dx0, int ld, const float* coef, int accumulate, hipStream_t s) {
+                    const float* dx0, int ld, const float* coef, int hps, int accumulate,
+                    hipStream_t s) {
   switch (nv) {
 #define CASE(k) \
-  case k: launch_sums<VEC, k>(et, nt, B, sb, dx0, ld, coef, accumulate, s); break;
+  case k: launch_sums<VEC, k>(et, nt, B, sb, dx0, ld, coef, hps, accumulate, s); break;
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
 #undef CASE
   }
@@ -741,11 +903,16 @@ dcnr_status emb_segment_sum(const EmbBwdDesc& e, const EmbSortBufs& sb, int64_t 
     set_error("embedding backward: %d cross basis vectors unsupported", e.nv);
     return DCNR_UNSUPPORTED_SHAPE;
   }
+  const int hps = huge_stride(e.width, e.n_tab);
+  if ((size_t)huge_segs(e.n_tab, B) * 2 * hps * 4 > sb.tmp_bytes) {
+    set_error("embedding backward: sort scratch too small for the huge-run pieces");
+    return DCNR_WORKSPACE_TOO_SMALL;
+  }
   const EmbTabs et = make_tabs(e);
   if (vec4_ok(e, dx0, ld))
-    launch_sums_nv<4>(e.nv, et, e.n_tab, B, sb, dx0, ld, coef, accumulate, s);
+    launch_sums_nv<4>(e.nv, et, e.n_tab, B, sb, dx0, ld, coef, hps, accumulate, s);
   else
-    launch_sums_nv<1>(e.nv, et, e.n_tab, B, sb, dx0, ld, coef, accumulate, s);
+    launch_sums_nv<1>(e.nv, et, e.n_tab, B, sb, dx0, ld, coef, hps, accumulate, s);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }

@@ -6,7 +6,10 @@ grad_t[r] = sum of dx0[b, off_t:off_t+w_t] over the samples b with id_t[b] == r,
 dx0 = deep part + sum_k coef[b][k] V_k (the low-rank cross part).  The library sums each row in a FIXED order: runs of <= 16
 samples sequentially in ascending b; longer runs one wave per row, walked in
 blocks of 64 entries, slot s of S lane slots taking entries s, s+S, ... of
-every block in ascending order, slots added in ascending order.  ``emulate_table`` restates that order in numpy fp32, so the
+every block in ascending order, slots added in ascending order.  Runs of
+more than HSEG entries are cut at the multiples of HSEG of the global sorted
+position (table t's entries sit at t*B ..): each piece is summed as a long
+run, the pieces added in order.  ``emulate_table`` restates that order in numpy fp32, so the
 gradients are checked BIT-EXACT against it, from the kernels' own deep dx0
 and cross coefficients (row = deep sum + sum_k coef sum_k V_k, V = (w_0 ..
 w_{L-1}, w_f[H:]), each term rounded twice).  The fp64 recomputation of the deep dx0 and of
@@ -26,12 +29,14 @@ pytestmark = pytest.mark.gpu
 
 SHORT = 16   # embed_bwd.hip LIM
 BLK = 64     # embed_bwd.hip emb_runs_long_kernel block of entries
+HSEG = 2048  # embed_bwd.hip huge-run segment
 
 
-def emulate_table(ids, X, Cf, Vt, rows, vec):
+def emulate_table(ids, X, Cf, Vt, rows, vec, gbase=0):
     """fp32 gradient of one table in the library's summation order: X the
     table's deep dx0 segments [B][w], Cf the cross coefficients [B][nv], Vt
-    the basis restricted to the table's columns [nv][w]."""
+    the basis restricted to the table's columns [nv][w], gbase the global
+    sorted position of the table's first entry."""
     B, w = X.shape
     nv = Cf.shape[1]
     order = np.argsort(ids, kind="stable")
@@ -61,22 +66,36 @@ def emulate_table(ids, X, Cf, Vt, rows, vec):
     def seq(a):   # sequential fp32 sum over axis 0 (0 if empty)
         return np.cumsum(a, axis=0, dtype=np.float32)[-1] if len(a) else np.zeros(a.shape[1], np.float32)
 
+    def piece(ent, cfe, cols):   # one wave's slot-ordered sums of a block walk
+        m = len(ent)
+        gb = (cols.stop - cols.start) // vec
+        S = 64 // gb
+        sub = ent[:, cols]
+        tot = ctot = None
+        for s in range(S):   # slot s: entries s, s+S, ... of every BLK-entry block
+            idx = [p + j for p in range(0, m, BLK) for j in range(s, BLK, S) if p + j < m]
+            t, ct = seq(sub[idx]), seq(cfe[idx])
+            tot = t if tot is None else tot + t
+            ctot = ct if ctot is None else ctot + ct
+        return tot, ctot
+
     for h, e in zip(heads[~short], ends[~short]):
         ent = X[order[h:e]]
         cfe = Cf[order[h:e]]
         m = e - h
+        # huge runs: pieces cut at the global multiples of HSEG
+        cuts = [0]
+        if m > HSEG:
+            first = (gbase + h) // HSEG * HSEG + HSEG - (gbase + h)
+            cuts += list(range(first, m, HSEG))
+        cuts.append(m)
         out = np.zeros(w, np.float32)
         for cb in range(0, G, 64):
-            gb = min(64, G - cb)
-            S = 64 // gb
-            cols = slice(cb * vec, (cb + gb) * vec)
-            sub = ent[:, cols]
-            tot = ctot = None
-            for s in range(S):   # slot s: entries s, s+S, ... of every BLK-entry block
-                idx = [p + j for p in range(0, m, BLK) for j in range(s, BLK, S) if p + j < m]
-                t, ct = seq(sub[idx]), seq(cfe[idx])
-                tot = t if tot is None else tot + t
-                ctot = ct if ctot is None else ctot + ct
+            cols = slice(cb * vec, (cb + min(64, G - cb)) * vec)
+            parts = [piece(ent[a:b], cfe[a:b], cols) for a, b in zip(cuts[:-1], cuts[1:])]
+            tot, ctot = parts[0]
+            for t, ct in parts[1:]:
+                tot, ctot = tot + t, ctot + ct
             out[cols] = _combine_cols(tot, ctot, Vt[:, cols])
         g[ks[h]] = out
     return g
@@ -122,10 +141,10 @@ def _check_tables(m, cfg, B, ws, grads, batch_np, vec_expected=None):
     vec = 4 if all(w % 4 == 0 for _, _, _, w in tabs) and Dq % 4 == 0 else 1
     if vec_expected is not None:
         assert vec == vec_expected
-    long_runs = 0
-    for name, ids, col, w in tabs:
+    long_runs = huge_runs = 0
+    for t, (name, ids, col, w) in enumerate(tabs):
         rows = sd[name].shape[0]
-        ref = emulate_table(ids, X[:, col:col + w], Cf, Vfull[:, col:col + w], rows, vec)
+        ref = emulate_table(ids, X[:, col:col + w], Cf, Vfull[:, col:col + w], rows, vec, t * B)
         got = gd[name].cpu().numpy()
         if not np.array_equal(got, ref):
             bad = np.flatnonzero(np.any(got != ref, axis=1))
@@ -133,8 +152,10 @@ def _check_tables(m, cfg, B, ws, grads, batch_np, vec_expected=None):
             raise AssertionError((name, np.abs(got - ref).max(), len(bad), bad[:5].tolist(),
                                   cnt[bad[:5]].tolist(), got[bad[0]][:4].tolist(),
                                   ref[bad[0]][:4].tolist()))
-        long_runs += int((np.bincount(ids, minlength=rows) > SHORT).sum())
-    return long_runs
+        cnt = np.bincount(ids, minlength=rows)
+        long_runs += int((cnt > SHORT).sum())
+        huge_runs += int((cnt > HSEG).sum())
+    return long_runs, huge_runs
 
 
 def _cfg():
@@ -152,6 +173,13 @@ def _skewed_batch(cfg, B, dev, seed=3):
     c = np.stack([rng.integers(0, n, B) for n in cards], 1)
     c[:, 0] = 5
     c[:, 1] = rng.integers(0, 2, B)
+    # runs at the huge-run threshold: HSEG (long kernel), HSEG + 1 and
+    # 2 HSEG + 1 entries (pieces)
+    c[:, 2] = rng.integers(10, cards[2], B)
+    p = rng.permutation(B)
+    c[p[:HSEG], 2] = 3
+    c[p[HSEG:2 * HSEG + 1], 2] = 4
+    c[p[2 * HSEG + 1:4 * HSEG + 2], 2] = 6
     n = rng.random((B, cfg["n_num"]), dtype=np.float32)
     y = (rng.random(B) < 0.5).astype(np.float32)
     t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
@@ -183,18 +211,18 @@ def _fwd_bwd(m, batch, seed, grads=None, accumulate=False):
     return grads, ws
 
 
-@pytest.mark.parametrize("precision", ["bf16", "fp32"])
-def test_embedding_grads_bit_exact_skewed(dev, precision):
+@pytest.mark.parametrize("precision,B", [("bf16", 65536), ("fp32", 65536), ("bf16", 50003)])
+def test_embedding_grads_bit_exact_skewed(dev, precision, B):
     """Every table's gradient equals the fixed-order fp32 emulation from the
     kernels' own deep dx0 and cross coefficients, bit for bit; rows no sample
-    references are 0."""
+    references are 0.  B = 50003: tables start off the HSEG segment grid."""
     cfg = _cfg()
-    B = 65536
     m = _model(cfg, dev, precision)
     batch = _skewed_batch(cfg, B, dev)
     grads, ws = _fwd_bwd(m, batch, seed=77)
-    long_runs = _check_tables(m, cfg, B, ws, grads, [t.cpu().numpy() for t in batch[:3]], 4)
-    assert long_runs > 2000   # both kernels ran
+    long_runs, huge_runs = _check_tables(m, cfg, B, ws, grads,
+                                         [t.cpu().numpy() for t in batch[:3]], 4)
+    assert long_runs > 1000 and huge_runs >= 6   # all three paths ran
 
 
 def test_embedding_grads_bit_exact_odd_widths(dev):
