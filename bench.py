@@ -269,6 +269,40 @@ def bench_cfg5(dev, iters, cpu):
     return out
 
 
+def bench_cfg5_sharded(dev, iters, world):
+    """SURVEY 8(e) cfg5 at N > 1: the 1M x 64 index row-sharded over the ranks
+    (dcnr.ShardedNearestNeighbors: each rank scans 1M/world rows, all-gather
+    of the world*k candidates, dcnr_topk_merge), barrier-bracketed, max over
+    ranks; the same answer as the single index (tests/test_knn_sharded_gpu.py)."""
+    import dcnr
+    n, d = 1_000_000, 64
+    g = torch.Generator(device=dev).manual_seed(11)
+    tab = torch.randn((n, d), generator=g, device=dev)
+    nn = dcnr.ShardedNearestNeighbors(n_neighbors=11, device=dev).fit(tab)
+    del tab
+    out = {"workload": f"cosine top-11 over 1M x 64, rows sharded over {world} ranks "
+                       f"({nn.hi - nn.lo} rows on rank 0), all-gather + merge"}
+    for Q in (1, 32, 256):
+        q = torch.randn((Q, d), generator=g, device=dev)
+        for _ in range(2):
+            nn.kneighbors_device(q, 11)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            nn.kneighbors_device(q, 11)
+        torch.cuda.synchronize()
+        dist.barrier()
+        el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        t = float(el.item()) / iters
+        out[f"topk_q{Q}_us"] = t * 1e6
+        out[f"topk_q{Q}_queries_per_sec"] = Q / t
+    del nn
+    torch.cuda.empty_cache()
+    return out
+
+
 def bench_fp32(B, dev, pool, world, steps=5, warmup=2):
     """The fp32 parity mode (f32 MFMA GEMMs, fp32 activations: the path pinned
     element-wise to the reference's fixtures) at the same workload: train
@@ -429,6 +463,8 @@ def main():
     cfg2 = bench_cfg2(model, gen, dev, max(args.steps, 10), world)
     cfg5 = bench_cfg5(dev, 10, world == 1 and rank == 0 and not args.no_cpu_baseline) \
         if not args.no_serving else None
+    if cfg5 is not None and world > 1:
+        cfg5["sharded_index"] = bench_cfg5_sharded(dev, 10, world)
 
     if rank == 0:
         samples = world * B * args.steps

@@ -1201,6 +1201,18 @@ dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t
   return DCNR_OK;
 }
 
+dcnr_status dcnr_topk_merge(const float* dist, const int64_t* idx, int32_t lists, int64_t Q,
+                            int32_t k, int64_t* out_idx, float* out_dist, dcnr_stream_t stream) {
+  if (!dist || !idx || !out_idx || !out_dist || Q < 0) {
+    set_error("dcnr_topk_merge: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  TRYB(DCNR_K_KNN, (double)lists * Q * k * 12.0 + Q * k * 12.0,
+       topk_merge(dist, idx, lists, Q, k, out_idx, out_dist, s));
+  return DCNR_OK;
+}
+
 dcnr_status dcnr_linear_bf16(const void* X, int64_t ldx, int64_t M, int32_t K, const void* W,
                              int64_t ldw, int32_t N, const float* bias, void* C, int64_t ldc,
                              int out_f32, dcnr_stream_t stream) {

@@ -515,6 +515,9 @@ dcnr_status adam(int n, float* const* p, const float* const* g, float* const* m,
 // knn
 dcnr_status row_inv_norms(const float* t, int64_t N, int d, float* out, hipStream_t s);
 size_t topk_ws(int64_t N, int64_t Q, int k);
+// k best of lists k-lists [lists][Q][k] by (dist, row as unsigned)
+dcnr_status topk_merge(const float* dist, const int64_t* idx, int lists, int64_t Q, int k,
+                       int64_t* out_idx, float* out_dist, hipStream_t s);
 dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, const float* q,
                         int64_t Q, int k, int64_t* idx, float* dist, void* ws, size_t ws_bytes,
                         hipStream_t s);

@@ -727,6 +727,51 @@ __global__ __launch_bounds__(NT) void merge_kernel(const Cand* in, int nslices, 
   }
 }
 
+// Per query: the k best of `lists` k-lists [lists][Q][k] (dist, int64 row),
+// ascending by (dist, row as unsigned); padding entries (FLT_MAX, -1) sort
+// last.  One block per query, all lists*k <= TM_CAP candidates sorted in LDS.
+constexpr int TM_CAP = 2048;
+__global__ __launch_bounds__(NT) void topk_merge_kernel(const float* dist, const int64_t* idx,
+                                                        int lists, int64_t Q, int k,
+                                                        int64_t* out_idx, float* out_dist) {
+  __shared__ float cd[TM_CAP];
+  __shared__ uint64_t ci[TM_CAP];
+  const int64_t qq = blockIdx.x;
+  const int n = lists * k;
+  int n2 = 2;
+  while (n2 < n) n2 <<= 1;
+  for (int t = threadIdx.x; t < n2; t += NT) {
+    if (t < n) {
+      const int64_t src = ((int64_t)(t / k) * Q + qq) * k + t % k;
+      cd[t] = dist[src];
+      ci[t] = (uint64_t)idx[src];
+    } else {
+      cd[t] = FLT_MAX;
+      ci[t] = ~0ull;
+    }
+  }
+  __syncthreads();
+  for (int k2 = 2; k2 <= n2; k2 <<= 1) {
+    for (int j = k2 >> 1; j > 0; j >>= 1) {
+      for (int t = threadIdx.x; t < n2 / 2; t += NT) {
+        const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+        const int p = i + j;
+        const bool asc = (i & k2) == 0;
+        const float a = cd[i], b = cd[p];
+        const uint64_t ia = ci[i], ib = ci[p];
+        const bool bl = b < a || (b == a && ib < ia);
+        const bool al = a < b || (a == b && ia < ib);
+        if (asc ? bl : al) { cd[i] = b; cd[p] = a; ci[i] = ib; ci[p] = ia; }
+      }
+      __syncthreads();
+    }
+  }
+  for (int t = threadIdx.x; t < k; t += NT) {
+    out_idx[qq * k + t] = (int64_t)ci[t];
+    out_dist[qq * k + t] = cd[t];
+  }
+}
+
 __global__ void inv_norm_kernel(const float* t, int64_t N, int d, float* out) {
   const int lane = threadIdx.x & 63;
   const int64_t nw = (int64_t)gridDim.x * (blockDim.x / 64);
@@ -873,6 +918,19 @@ dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, cons
   DCNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(merge_kernel, dim3((unsigned)Q), dim3(NT), 0, s, cands, ns, k, idx, dist, 1,
                      nullptr);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status topk_merge(const float* dist, const int64_t* idx, int lists, int64_t Q, int k,
+                       int64_t* out_idx, float* out_dist, hipStream_t s) {
+  if (k < 1 || lists < 1 || (int64_t)lists * k > TM_CAP) {
+    set_error("topk_merge: %d lists of k=%d unsupported (lists * k <= %d)", lists, k, TM_CAP);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  if (Q <= 0) return DCNR_OK;
+  hipLaunchKernelGGL(topk_merge_kernel, dim3((unsigned)Q), dim3(NT), 0, s, dist, idx, lists, Q, k,
+                     out_idx, out_dist);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }

@@ -19,7 +19,7 @@ All compute runs in libdcnr.so (C ABI: include/dcnr.h) on the HIP device.
 """
 from .model import CrossLayer, DCN_RecSys, ResBlock  # noqa: F401
 from .ops import Adam, AdamW, BCEWithLogitsLoss, bce_with_logits  # noqa: F401
-from .knn import NearestNeighbors  # noqa: F401
+from .knn import NearestNeighbors, ShardedNearestNeighbors  # noqa: F401
 from .train import FusedTrainer  # noqa: F401
 from . import serving  # noqa: F401
 from .data import DeviceLoader  # noqa: F401

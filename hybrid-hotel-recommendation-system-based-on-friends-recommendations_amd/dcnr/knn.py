@@ -77,3 +77,88 @@ class NearestNeighbors:
         if return_distance:
             return dist.cpu().numpy(), idx_np
         return idx_np
+
+
+def index_shard(n: int, rank: int, world: int):
+    """Rows [lo, hi) of an n-row index held by ``rank``: balanced, covering
+    every row (unlike parallel.shard_range, which trims a batch)."""
+    if world < 1 or not (0 <= rank < world):
+        raise ValueError("bad rank/world")
+    return n * rank // world, n * (rank + 1) // world
+
+
+class ShardedNearestNeighbors:
+    """The cosine index row-sharded over a process group (SURVEY.md 8(e),
+    cfg5): rank r holds rows ``index_shard(N, r, world)`` of the table, scans
+    only those (``dcnr_cosine_topk``), and the ranks' k-lists -- global row
+    ids -- are all-gathered (world * Q * k candidates, one exchange step) and
+    merged on the device by ``dcnr_topk_merge``.  Every rank returns exactly
+    what ``NearestNeighbors`` over the whole table returns, ties included
+    (ascending (dist, row)); the per-row distance does not depend on which
+    rank computes it.  Same ``kneighbors`` contract as the single index
+    (main.py:200, 300); every rank must call with the same queries."""
+
+    def __init__(self, n_neighbors=5, metric='cosine', algorithm='brute', device='cuda',
+                 group=None):
+        import torch.distributed as dist
+        self._local = NearestNeighbors(n_neighbors, metric, algorithm, device)
+        self.n_neighbors = n_neighbors
+        self.device = self._local.device
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        self.lo = self.hi = 0
+        self.n_samples_fit_ = None
+
+    def fit(self, X, y=None):
+        """X: the whole table (every rank passes the same one; only the
+        rank's rows are copied to the device)."""
+        n = X.shape[0]
+        if n < self.world:
+            raise ValueError(f"{n} rows cannot be split over {self.world} ranks")
+        self.lo, self.hi = index_shard(n, self.rank, self.world)
+        self._local.fit(X[self.lo:self.hi])
+        self.n_samples_fit_ = n
+        self.n_features_in_ = X.shape[1]
+        return self
+
+    def kneighbors_device(self, q: torch.Tensor, k: int):
+        import torch.distributed as dist
+        if self.n_samples_fit_ is None:
+            raise RuntimeError("This ShardedNearestNeighbors instance is not fitted yet")
+        if k > self.n_samples_fit_:
+            raise ValueError(f"Expected n_neighbors <= n_samples_fit, but n_neighbors = {k}, "
+                             f"n_samples_fit = {self.n_samples_fit_}")
+        q = q.to(self.device, torch.float32).reshape(-1, self.n_features_in_).contiguous()
+        Q = q.shape[0]
+        kl = min(k, self.hi - self.lo)
+        d_loc, i_loc = self._local.kneighbors_device(q, kl)
+        dl = torch.full((Q, k), torch.finfo(torch.float32).max, dtype=torch.float32,
+                        device=self.device)
+        il = torch.full((Q, k), -1, dtype=torch.int64, device=self.device)
+        dl[:, :kl] = d_loc
+        il[:, :kl] = i_loc + self.lo
+        dg = [torch.empty_like(dl) for _ in range(self.world)]
+        ig = [torch.empty_like(il) for _ in range(self.world)]
+        dist.all_gather(dg, dl, group=self.group)
+        dist.all_gather(ig, il, group=self.group)
+        dall = torch.stack(dg).contiguous()
+        iall = torch.stack(ig).contiguous()
+        idx = torch.empty((Q, k), dtype=torch.int64, device=self.device)
+        dd = torch.empty((Q, k), dtype=torch.float32, device=self.device)
+        lib = _lib.load()
+        _lib.check(lib.dcnr_topk_merge(dall.data_ptr(), iall.data_ptr(), self.world, Q, k,
+                                       idx.data_ptr(), dd.data_ptr(),
+                                       _lib.stream_ptr(self.device)), "dcnr_topk_merge")
+        return dd, idx
+
+    def kneighbors(self, X=None, n_neighbors=None, return_distance=True):
+        k = self.n_neighbors if n_neighbors is None else int(n_neighbors)
+        if k <= 0:
+            raise ValueError(f"Expected n_neighbors > 0. Got {k}")
+        q = torch.as_tensor(np.asarray(X, dtype=np.float32)) if not torch.is_tensor(X) else X
+        dist_, idx = self.kneighbors_device(q, k)
+        idx_np = idx.cpu().numpy()
+        if return_distance:
+            return dist_.cpu().numpy(), idx_np
+        return idx_np

@@ -234,6 +234,15 @@ dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t
                              const float* queries, int64_t Q, int32_t k, int64_t* idx,
                              float* dist, void* ws, size_t ws_bytes, dcnr_stream_t stream);
 
+/* Merge of row-sharded top-k lists (the cfg5 index split over ranks, SURVEY
+ * 8(e)): dist fp32 / idx int64 [lists][Q][k] (global rows; padding entries
+ * (FLT_MAX, -1) sort last) -> the k best per query, ascending by (dist, row),
+ * the order dcnr_cosine_topk gives over the whole table.  lists * k <= 2048.
+ * Replaces nothing in the reference (one sklearn index per process,
+ * main.py:268-270); the single-index result is reproduced exactly. */
+dcnr_status dcnr_topk_merge(const float* dist, const int64_t* idx, int32_t lists, int64_t Q,
+                            int32_t k, int64_t* out_idx, float* out_dist, dcnr_stream_t stream);
+
 /* Batch assembly of a device-resident dataset (TensorDataset + DataLoader,
  * train.py:195-196): for each of n_arrays (<= 8) arrays of n_src rows of
  * row_bytes[a] bytes (a multiple of 4), dst[a] row i = src[a] row idx[i]

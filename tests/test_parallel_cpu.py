@@ -46,6 +46,17 @@ def test_shard_range():
         parallel.shard_range(4, 2, 2)
 
 
+def test_index_shard_covers_every_row():
+    from dcnr.knn import index_shard
+    for n, w in [(15, 2), (1_000_000, 8), (8, 8), (1_000_003, 7)]:
+        parts = [index_shard(n, r, w) for r in range(w)]
+        assert parts[0][0] == 0 and parts[-1][1] == n
+        assert all(a[1] == b[0] for a, b in zip(parts, parts[1:]))
+        assert max(h - l for l, h in parts) - min(h - l for l, h in parts) <= 1
+    with pytest.raises(ValueError):
+        index_shard(4, 2, 2)
+
+
 class _FakeModel:
     _active_ws = None
     bn_allreduce = None
