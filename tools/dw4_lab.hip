@@ -1,0 +1,228 @@
+// Kernel lab: gemm_dw with 4 waves per block, each wave a 128 x 128 output
+// tile (8 x 8 MFMA 16x16x32 tiles, 256 fp32 accumulators per lane, 1 wave
+// per SIMD with the 512-register budget) instead of 8 waves of 128 x 64:
+// a third fewer LDS fragment bytes per MAC (32 vs 21 MAC/B).  Same LDS-DMA
+// ring, swizzle and XCD split mapping as csrc/gemm_dw.hip; compared against
+// it on the same data.  PIPE=1: the next stage's fragments are read from LDS
+// before this stage's MFMAs (double-buffered fragments).
+#include "../hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd/csrc/gemm_dw.hip"
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+#ifndef PIPE
+#define PIPE 0
+#endif
+
+namespace dcnr {
+void set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vfprintf(stderr, fmt, ap);
+  va_end(ap);
+  fprintf(stderr, "\n");
+}
+
+namespace {
+constexpr int NT4 = 256;
+
+// one stage (32 rows of A and B, 256 columns each) by 4 waves: 8 DMAs per wave
+__device__ __forceinline__ void stage_load4(u32x4 ar, u32x4 br, int64_t lda, int64_t ldb,
+                                            int64_t kb, int64_t kend, int n0, int N, int c0, int K,
+                                            char* lds_stage, int wave, int lane) {
+  const int rsub = lane >> 5, p = lane & 31;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pair = wave * 4 + i;                 // 0..15: rows 2*pair, 2*pair+1
+    const int row = pair * 2 + rsub;
+    const int chunk = ((p >> 1) ^ (row & 7)) * 2 + (p & 1);
+    const int64_t b = kb + row;
+    const int na = n0 + chunk * 8, ka = c0 + chunk * 8;
+    const bool okr = b < kend;
+    const int offa = (okr && na < N) ? (int)((b * lda + na) * 2) : OOR;
+    const int offb = (okr && ka < K) ? (int)((b * ldb + ka) * 2) : OOR;
+    const uint32_t dsta = lds_addr(lds_stage) + pair * 1024;
+    dma16(ar, offa, dsta);
+    dma16(br, offb, dsta + OPB);
+  }
+}
+
+__global__ __launch_bounds__(NT4, 1) void gemm_dw4_kernel(DwArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tiles = g.tiles_n * g.tiles_k;
+  const int bid = blockIdx.x;
+  const int split = (bid % 8) + 8 * (bid / (8 * tiles));
+  const int t = (bid / 8) % tiles;
+  const int n0 = (t / g.tiles_k) * TNW, c0 = (t % g.tiles_k) * TKW;
+  const int64_t kbeg = (int64_t)split * g.k_per_split;
+  const int64_t kend = min(g.Btot, kbeg + g.k_per_split);
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wn = wave >> 1, wk = wave & 1;    // wave tile: n wn*128.., k wk*128..
+
+  const u32x4 ar = rsrc_words(g.A, g.Btot * g.lda * 2);
+  const u32x4 br = rsrc_words(g.B, g.Btot * g.ldb * 2);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nst = kend > kbeg ? (int)((kend - kbeg + BKW - 1) / BKW) : 0;
+#pragma unroll
+  for (int p = 0; p < NSTAGE - 1; ++p)
+    if (p < nst)
+      stage_load4(ar, br, g.lda, g.ldb, kbeg + (int64_t)p * BKW, kend, n0, g.N, c0, g.K,
+                  lds + p * STAGEB, wave, lane);
+#if PIPE
+  // fragments of stage st+1 are read from LDS while stage st's MFMAs run
+  bf16x8 af[8], bf[8];
+  if (nst > 0) {
+    if (nst > 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (nst > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = frag_t(lds, wn * 128 + i * 16, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bf[j] = frag_t(lds + OPB, wk * 128 + j * 16, 0, lane);
+  }
+  for (int st = 0; st < nst; ++st) {
+    bf16x8 an[8], bn[8];
+    if (st + 1 < nst) {
+      // stage st+1 landed (stages st+2, st+3 stay in flight); the barrier
+      // also retires every wave's reads of stage st (done last iteration),
+      // so its buffer takes stage st+4
+      if (st + 3 < nst) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (st + 2 < nst) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (st + NSTAGE < nst)
+        stage_load4(ar, br, g.lda, g.ldb, kbeg + (int64_t)(st + NSTAGE) * BKW, kend, n0, g.N,
+                    c0, g.K, lds + (st % NSTAGE) * STAGEB, wave, lane);
+      const char* ai = lds + ((st + 1) % NSTAGE) * STAGEB;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) an[i] = frag_t(ai, wn * 128 + i * 16, 0, lane);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) bn[j] = frag_t(ai + OPB, wk * 128 + j * 16, 0, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { af[i] = an[i]; bf[i] = bn[i]; }
+  }
+#else
+  for (int st = 0; st < nst; ++st) {
+    // 8 DMAs per wave per stage: the younger two stages' 16 stay in flight
+    if (st + 2 < nst) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    else if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (st + NSTAGE - 1 < nst)
+      stage_load4(ar, br, g.lda, g.ldb, kbeg + (int64_t)(st + NSTAGE - 1) * BKW, kend, n0, g.N,
+                  c0, g.K, lds + ((st + NSTAGE - 1) % NSTAGE) * STAGEB, wave, lane);
+    const char* ai = lds + (st % NSTAGE) * STAGEB;
+    const char* bi = ai + OPB;
+    bf16x8 af[8], bf[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) af[i] = frag_t(ai, wn * 128 + i * 16, 0, lane);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) bf[j] = frag_t(bi, wk * 128 + j * 16, 0, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+  }
+#endif
+
+  float* out = g.C + (int64_t)split * g.slab_stride;
+  const __amdgpu_buffer_rsrc_t cr = buf_rsrc(out, (int64_t)g.N * g.ldc * 4);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = c0 + wk * 128 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4 + r;
+        const bool ok = n < g.N && k < g.K;
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), cr,
+                                              ok ? (n * g.ldc + k) * 4 : OOR, 0, 0);
+      }
+    }
+}
+}  // namespace
+}  // namespace dcnr
+
+using namespace dcnr;
+
+static float time_it(void (*launch)(const DwArgs&), const DwArgs& a) {
+  for (int i = 0; i < 3; ++i) launch(a);
+  hipEvent_t e0, e1;
+  (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+  (void)hipEventRecord(e0, 0);
+  for (int i = 0; i < 20; ++i) launch(a);
+  (void)hipEventRecord(e1, 0);
+  (void)hipEventSynchronize(e1);
+  float ms;
+  (void)hipEventElapsedTime(&ms, e0, e1);
+  return ms * 1e3f / 20;
+}
+
+static void launch_ref(const DwArgs& a) { gemm_dw(a, 0); }
+static void launch_4(const DwArgs& a0) {
+  DwArgs a = a0;
+  a.tiles_n = (int)cdiv(a.N, TNW);
+  a.tiles_k = (int)cdiv(a.K, TKW);
+  hipLaunchKernelGGL(gemm_dw4_kernel, dim3(a.tiles_n * a.tiles_k * a.splits), dim3(NT4), LDS_DW, 0,
+                     a);
+}
+
+int main() {
+  const int64_t B = 131072;
+  const int N = 512, K = 512;
+  bf16 *A, *X;
+  float *slab, *slab2;
+  const int S = gemm_dw_splits(N, K, B);
+  (void)hipMalloc(&A, B * N * 2); (void)hipMalloc(&X, B * K * 2);
+  (void)hipMalloc(&slab, (size_t)S * N * K * 4);
+  (void)hipMalloc(&slab2, (size_t)S * N * K * 4);
+  {
+    std::vector<uint16_t> h(B * (size_t)std::max(N, K));
+    uint32_t st = 12345;
+    for (auto& v : h) {
+      st = st * 1664525u + 1013904223u;
+      const float f = (float)(st >> 8) / 8388608.f - 1.f;
+      v = (uint16_t)(__builtin_bit_cast(uint32_t, f) >> 16);
+    }
+    (void)hipMemcpy(A, h.data(), B * N * 2, hipMemcpyHostToDevice);
+    (void)hipMemcpy(X, h.data() + 3, B * K * 2, hipMemcpyHostToDevice);
+  }
+  (void)hipFuncSetAttribute((const void*)gemm_dw4_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DW);
+  DwArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.A = A; a.lda = N; a.B = X; a.ldb = K; a.C = slab; a.ldc = K; a.slab_stride = (int64_t)N * K;
+  a.Btot = B; a.k_per_split = (B + S - 1) / S; a.N = N; a.K = K; a.splits = S;
+  const float t_ref = time_it(launch_ref, a);
+  DwArgs b = a;
+  b.C = slab2;
+  const float t4 = time_it(launch_4, b);
+  (void)hipDeviceSynchronize();
+  std::vector<float> h1((size_t)S * N * K), h2((size_t)S * N * K);
+  (void)hipMemcpy(h1.data(), slab, h1.size() * 4, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(h2.data(), slab2, h2.size() * 4, hipMemcpyDeviceToHost);
+  size_t diff = 0;
+  for (size_t i = 0; i < h1.size(); ++i) diff += h1[i] != h2[i];
+  printf("S=%d  8-wave %.1f us (%.0f TF/s)   4-wave %.1f us (%.0f TF/s)   mismatches %zu  %s\n",
+         S, t_ref, 2.0 * B * N * K / t_ref / 1e6, t4, 2.0 * B * N * K / t4 / 1e6, diff,
+         hipGetErrorString(hipGetLastError()));
+  return 0;
+}
