@@ -81,6 +81,56 @@ def make_batch(gen, B, dev):
     return user, item, cat, num, y
 
 
+class ZipfIds:
+    """Ids with P(rank r) ~ r^-a over n rows (the secondary
+    Zipf(1.05) distribution), ranks mapped to rows by a fixed permutation so
+    the hot rows are scattered over the table."""
+
+    def __init__(self, n, dev, a=1.05, seed=3):
+        g = torch.Generator(device=dev).manual_seed(seed)
+        w = torch.arange(1, n + 1, device=dev, dtype=torch.float64).pow(-a)
+        self.cdf = torch.cumsum(w, 0) / w.sum()
+        self.perm = torch.randperm(n, generator=g, device=dev)
+        self.n = n
+
+    def __call__(self, shape, gen, dev):
+        u = torch.rand(shape, generator=gen, device=dev, dtype=torch.float64)
+        r = torch.searchsorted(self.cdf, u).clamp_(max=self.n - 1)
+        return self.perm[r]
+
+
+def bench_zipf(trainer, dev, B, world, steps=10, warmup=3):
+    """The train step on Zipf(1.05) ids for the user, item and categorical
+    columns (fresh batch per step, generated before the timed region)."""
+    gen = torch.Generator(device=dev).manual_seed(77 + (dist.get_rank() if world > 1 else 0))
+    zu, zi, zc = ZipfIds(CFG["n_users"], dev), ZipfIds(CFG["n_items"], dev), ZipfIds(1000, dev)
+    pool = []
+    for _ in range(warmup + steps):
+        pool.append((zu((B,), gen, dev), zi((B,), gen, dev), zc((B, 12), gen, dev),
+                     torch.rand((B, 8), generator=gen, device=dev),
+                     (torch.rand((B,), generator=gen, device=dev) < 0.5).float()))
+    top_user = float(torch.bincount(pool[0][0]).max()) / B
+    for k in range(warmup):
+        trainer.step(*pool[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        trainer.step(*pool[warmup + k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    el = float(el.item())
+    return {"distribution": "Zipf(1.05) over each table's rows (user, item, 12 categorical), "
+                            "ranks scattered by a fixed permutation",
+            "samples_per_sec": world * B * steps / el, "ms_per_step": el / steps * 1e3,
+            "steps": steps, "top_user_share": top_user}
+
+
 def cpu_threads():
     return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
 
@@ -459,6 +509,7 @@ def main():
     if world > 1:
         dist.all_reduce(ev, op=dist.ReduceOp.MAX)
     pairs_per_s = world * B * args.eval_steps / float(ev.item())
+    zipf = bench_zipf(trainer, dev, B, world)
     fp32 = None if args.no_fp32 else bench_fp32(B, dev, pool, world)
     cfg2 = bench_cfg2(model, gen, dev, max(args.steps, 10), world)
     cfg5 = bench_cfg5(dev, 10, world == 1 and rank == 0 and not args.no_cpu_baseline) \
@@ -538,6 +589,7 @@ def main():
                                 "frac_of_bf16_peak": deep_flop / (deep_ms / 1e3) / PEAK_BF16 if deep_ms else None,
                                 "step_tflops": deep_flop / (el / args.steps) / 1e12},
             "fp32_parity_mode": fp32,
+            "zipf_ids": zipf,
             "roofline_gather": {"bound": "hbm", "kernel": "gather_cross", "achieved": gather_gbs,
                                 "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                                 "frac": gather_gbs / (PEAK_HBM / 1e9),
