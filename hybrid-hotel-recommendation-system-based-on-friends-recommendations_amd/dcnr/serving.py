@@ -209,11 +209,18 @@ class RankingPipeline:
     @torch.no_grad()
     def recommend(self, user_row: int, positive_rows, lambda_param: float = 1.0,
                   top_k: int = 20, allowed: Optional[Iterable[int]] = None,
-                  excluded: Optional[Iterable[int]] = None):
+                  excluded: Optional[Iterable[int]] = None,
+                  fallback: Optional[Iterable[int]] = None, min_candidates: int = 20):
         """The scoring core of /recommendations (main.py:309-332) on hotel rows:
-        candidates -> [filters] -> ranking batch -> logits -> sort -> MMR when
-        lambda_param < 1.  Returns (ranked rows, their logits) on the device."""
+        candidates -> [fallback] -> [filters] -> ranking batch -> logits ->
+        sort -> MMR when lambda_param < 1.  ``fallback`` (the city's most
+        reviewed hotels) joins the candidates when fewer than
+        ``min_candidates`` were found (main.py:204-207).  Returns (ranked
+        rows, their logits) on the device."""
         cand = self.candidates(positive_rows)
+        if fallback is not None and cand.numel() < min_candidates:
+            extra = torch.as_tensor(list(fallback), dtype=torch.int64).to(self.device)
+            cand = torch.unique(torch.cat([cand, extra]))
         if allowed is not None or excluded is not None:   # host set filters (main.py:210-212)
             keep = set(cand.tolist())
             if allowed is not None:
@@ -221,6 +228,8 @@ class RankingPipeline:
             if excluded is not None:
                 keep -= set(int(e) for e in excluded)
             cand = torch.tensor(sorted(keep), dtype=torch.int64, device=self.device)
+        if cand.numel() == 0:   # "No suitable candidates found." (main.py:311-312)
+            return cand, torch.empty(0, dtype=torch.float32, device=self.device)
         scores = self.score(user_row, cand)
         order = self.rank(scores)
         ranked, rscores = cand[order], scores[order]
