@@ -406,6 +406,7 @@ def main():
     ap.add_argument("--eval-steps", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-serving", action="store_true", help="skip the configs[4] top-k leg")
+    ap.add_argument("--no-zipf", action="store_true", help="skip the Zipf(1.05)-id train line")
     ap.add_argument("--exchange", default="dense", choices=["dense", "sparse"],
                     help="N>1 gradient exchange: dense = the dense parameters' all-reduce "
                          "started inside the backward + reduce-scatter / sharded AdamW / "
@@ -509,7 +510,7 @@ def main():
     if world > 1:
         dist.all_reduce(ev, op=dist.ReduceOp.MAX)
     pairs_per_s = world * B * args.eval_steps / float(ev.item())
-    zipf = bench_zipf(trainer, dev, B, world)
+    zipf = None if args.no_zipf else bench_zipf(trainer, dev, B, world)
     fp32 = None if args.no_fp32 else bench_fp32(B, dev, pool, world)
     cfg2 = bench_cfg2(model, gen, dev, max(args.steps, 10), world)
     cfg5 = bench_cfg5(dev, 10, world == 1 and rank == 0 and not args.no_cpu_baseline) \

@@ -9,13 +9,13 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 400 python3 bench.py > $OUT/bench.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-serving --no-fp32 > $OUT/trace.log 2>&1 &&
+    python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-serving --no-fp32 --no-zipf > $OUT/trace.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $OUT/fetch -o run -- \
-    python3 bench.py --steps 3 --warmup 2 --eval-steps 1 --no-cpu-baseline --no-serving --no-fp32 > $OUT/fetch.log 2>&1 &&
+    python3 bench.py --steps 3 --warmup 2 --eval-steps 1 --no-cpu-baseline --no-serving --no-fp32 --no-zipf > $OUT/fetch.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $OUT/write -o run -- \
-    python3 bench.py --steps 3 --warmup 2 --eval-steps 1 --no-cpu-baseline --no-serving --no-fp32 > $OUT/write.log 2>&1 &&
+    python3 bench.py --steps 3 --warmup 2 --eval-steps 1 --no-cpu-baseline --no-serving --no-fp32 --no-zipf > $OUT/write.log 2>&1 &&
 python3 tools/stats_summary.py $OUT/trace/run_kernel_stats.csv \
-    "rocprofv3 --kernel-trace --stats of \`python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-serving --no-fp32\`" \
+    "rocprofv3 --kernel-trace --stats of \`python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-serving --no-fp32 --no-zipf\`" \
     > $OUT/kernel_summary.txt &&
 python3 tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \
     --json $OUT/pmc_traffic.json > $OUT/pmc_traffic.txt
