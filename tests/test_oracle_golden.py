@@ -118,3 +118,42 @@ def test_rank_and_union_oracle():
     assert orc.rank_by_score(s).tolist() == [1, 4, 0, 2, 3]   # stable on ties
     u = orc.candidate_union([5, 9], np.array([[5, 3, 9, -1], [9, 5, 7, 7]]))
     assert u.tolist() == [3, 5, 7, 9]
+
+
+def test_f7_reference_service_responses_oracle():
+    """F7: the oracle's serving chain (kNN -> union -> [fallback, filters] ->
+    fp64 forward -> stable sort -> MMR) on f7_common's caller-side rows gives
+    the reference service's ranked hotel ids and similar-item lists."""
+    import f7_common
+    f = f7_common.load()
+    sd = {k: v.double().numpy() for k, v in f.state.items()}
+    spec = orc.spec_from_params(f.n_users, f.n_items, f.cat_dims, f.n_num, f.params)
+    for req in f.expected["recommendations"]:
+        r = f7_common.request_rows(f, req)
+        pos = np.asarray(r["pos"], np.int64)
+        cand = np.zeros(0, np.int64)
+        if len(pos):
+            _, nn = orc.cosine_kneighbors(f.emb, f.emb[pos], 11)
+            cand = orc.candidate_union(pos, nn)
+        if len(cand) < 20:
+            cand = np.union1d(cand, np.asarray(r["fallback"], np.int64))
+        cand = np.asarray(sorted(set(cand.tolist()) & set(r["allowed"]) - set(r["excluded"])),
+                          np.int64)
+        got = []
+        if len(cand):
+            n = len(cand)
+            z, _ = orc.forward(sd, spec, np.full(n, r["user_row"], np.int64), cand,
+                               f.item_cat[cand], f.item_num[cand])
+            order = orc.rank_by_score(z)
+            ranked, scores = cand[order], np.asarray(z, np.float32)[order]
+            if req["lambda_param"] < 1.0:
+                ranked = ranked[orc.mmr_rerank(f.emb, ranked, scores, req["lambda_param"])]
+            got = [f.rev[int(x)] for x in ranked]
+        assert got == req["ranked_hotels"], (req, got)
+    for case in f.expected["similar_items"]:
+        row = f.item_map.get(case["item_id"])
+        if row is None:
+            assert case["status"] == 404
+            continue
+        _, nn = orc.cosine_kneighbors(f.emb, f.emb[row:row + 1], case["n"] + 1)
+        assert [f.rev[int(x)] for x in nn[0, 1:]] == case["ids"], case

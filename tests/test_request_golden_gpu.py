@@ -3,108 +3,55 @@
 tests/golden/make_request_golden.py on a synthetic dataset) reproduced by
 ``dcnr.RankingPipeline`` on the GPU.
 
-The test is the service's caller: it reads the same CSVs and artifacts,
-restates main.py's host-side pandas steps (friends / personal positives and
-negatives main.py:170-193, the popular-hotel fallback :204-207, the city and
-negative filters :208-210, preprocess_for_ranking's per-hotel features
-:215-230) and hands the device path what main.py hands the model and the
-index: hotel rows, the user row, the filters.  Everything from candidate
-generation to the MMR order runs in libdcnr (top-k, candidate union, ranking
-batch, eval forward, stable sort, MMR).  The ranked hotel ids must equal the
-reference's response exactly (fp32 model; the reference ran on the CPU).
+The test is the service's caller: tests/f7_common.py restates main.py's
+host-side pandas steps and hands the device path what main.py hands the
+model and the index (hotel rows, the user row, the filters).  Everything from
+candidate generation to the MMR order runs in libdcnr (top-k, candidate
+union, ranking batch, eval forward, stable sort, MMR).  The ranked hotel ids
+must equal the reference's response exactly (fp32 model; the reference ran
+on the CPU).  tests/test_oracle_golden.py checks the oracle on the same
+fixture.
 """
-import json
-import os
-
-import numpy as np
-import pandas as pd
 import pytest
 import torch
 
+import f7_common
+
 pytestmark = pytest.mark.gpu
 
-DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "f7_request")
 
-
-def _load(dev):
+def _pipe(f, dev):
     import dcnr
-    art = json.load(open(os.path.join(DIR, "artifacts.json")))
-    main_df = pd.read_csv(os.path.join(DIR, "data", "hackathon_augmented_data.csv"))
-    main_df.rename(columns={"guest_id": "user_id", "hotel_id": "item_id"}, inplace=True)
-    friends = pd.read_csv(os.path.join(DIR, "data", "friendships.csv"))
-    # main.py:246-252
-    main_df["price_per_star"] = (main_df["price_rub"] / main_df["stars"]).replace(
-        [np.inf, -np.inf], 0).fillna(0)
-    main_df["cleanliness_vs_service"] = (main_df["rating_cleanliness"] /
-                                         main_df["rating_service"]).replace([np.inf, -np.inf], 0).fillna(0)
-    main_df["location_premium"] = main_df["rating_overall"] - main_df["rating_location"]
-    user_map = {int(k): v for k, v in art["user_id_mapping"].items()}
-    item_map = {int(k): v for k, v in art["item_id_mapping"].items()}
-    n_users, n_items, cat_dims, n_num = art["model_dims"]
-    m = dcnr.DCN_RecSys(n_users, n_items, cat_dims, n_num, dict(art["best_params"]),
+    m = dcnr.DCN_RecSys(f.n_users, f.n_items, f.cat_dims, f.n_num, dict(f.params),
                         precision="fp32")
-    m.load_state_dict(torch.load(os.path.join(DIR, "final_dcn_model.pth"), weights_only=True))
+    m.load_state_dict(f.state)
     m = m.to(dev).eval()
-    # per-hotel ranking features: the hotel's first main_df row (drop_duplicates
-    # keeps it, main.py:314), encoded / scaled as preprocess_for_ranking does
-    first = main_df.drop_duplicates(subset=["item_id"]).set_index("item_id")
-    item_cat = np.zeros((n_items, len(art["cat_encoders"])), np.int64)
-    item_num = np.zeros((n_items, n_num), np.float32)
-    mn, sc = np.array(art["scaler_min"]), np.array(art["scaler_scale"])
-    for h, r in item_map.items():
-        row = first.loc[h]
-        item_cat[r] = [enc.get(str(row[c]), enc.get(row[c], 0)) for c, enc in art["cat_encoders"].items()]
-        x = row[art["numerical_cols"]].to_numpy(np.float64)
-        item_num[r] = (x * sc + mn).astype(np.float32)
-    emb = np.load(os.path.join(DIR, "item_embeddings.npy"))
-    pipe = dcnr.RankingPipeline(m, item_cat, item_num, item_embeddings=torch.from_numpy(emb).to(dev))
-    return pipe, main_df, friends, user_map, item_map
-
-
-def _friends_of(friends, uid):   # main.py:170-176
-    return set(friends[friends["user_id_1"] == uid]["user_id_2"].tolist() +
-               friends[friends["user_id_2"] == uid]["user_id_1"].tolist())
+    return dcnr.RankingPipeline(m, f.item_cat, f.item_num,
+                                item_embeddings=torch.from_numpy(f.emb).to(dev))
 
 
 def test_f7_recommendations_match_reference(dev):
-    exp = json.load(open(os.path.join(DIR, "expected.json")))
-    pipe, main_df, friends, user_map, item_map = _load(dev)
-    rev = {v: k for k, v in item_map.items()}
+    f = f7_common.load()
+    pipe = _pipe(f, dev)
     n_mmr = 0
-    for req in exp["recommendations"]:
-        uid, city, mode, lam = req["user_id"], req["city"], req["type"], req["lambda_param"]
-        # host side of _generate_candidates (main.py:179-212)
-        if mode == "friends":
-            src = _friends_of(friends, uid)
-            reviews = main_df[main_df["user_id"].isin(src)] if src else pd.DataFrame()
-        else:
-            reviews = main_df[main_df["user_id"] == uid]
-        pos, neg = [], set()
-        if not reviews.empty:
-            pos = reviews[reviews["rating_overall"] >= 8]["item_id"].unique().tolist()
-            neg = set(reviews[reviews["rating_overall"] <= 4]["item_id"].unique())
-        popular = main_df[main_df["city"] == city].sort_values(
-            by="user_reviews_count", ascending=False).head(100)["item_id"].tolist()
-        city_hotels = set(main_df[main_df["city"] == city]["item_id"].unique())
-        user_row = user_map.get(uid, len(user_map) // 2)   # main.py:217
-        rows, _ = pipe.recommend(user_row, [item_map[h] for h in pos], lambda_param=lam,
-                                 allowed=[item_map[h] for h in city_hotels],
-                                 excluded=[item_map[h] for h in neg],
-                                 fallback=[item_map[h] for h in popular])
-        got = [rev[r] for r in rows.tolist()]
+    for req in f.expected["recommendations"]:
+        r = f7_common.request_rows(f, req)
+        rows, _ = pipe.recommend(r["user_row"], r["pos"], lambda_param=req["lambda_param"],
+                                 allowed=r["allowed"], excluded=r["excluded"],
+                                 fallback=r["fallback"])
+        got = [f.rev[x] for x in rows.tolist()]
         assert got == req["ranked_hotels"], (req, got)
-        n_mmr += lam < 1.0 and len(got) > 1
-    assert n_mmr >= 5 and any(len(r["ranked_hotels"]) == 0 for r in exp["recommendations"])
+        n_mmr += req["lambda_param"] < 1.0 and len(got) > 1
+    assert n_mmr >= 5 and any(len(r["ranked_hotels"]) == 0 for r in f.expected["recommendations"])
 
 
 def test_f7_similar_items_match_reference(dev):
-    exp = json.load(open(os.path.join(DIR, "expected.json")))
-    pipe, _, _, _, item_map = _load(dev)
-    rev = {v: k for k, v in item_map.items()}
-    for case in exp["similar_items"]:
-        row = item_map.get(case["item_id"])
+    f = f7_common.load()
+    pipe = _pipe(f, dev)
+    for case in f.expected["similar_items"]:
+        row = f.item_map.get(case["item_id"])
         if row is None:   # main.py:297-298: HTTP 404
             assert case["status"] == 404
             continue
-        got = [rev[r] for r in pipe.similar_items(row, case["n"]).tolist()]
+        got = [f.rev[x] for x in pipe.similar_items(row, case["n"]).tolist()]
         assert case["status"] == 200 and got == case["ids"], (case, got)
