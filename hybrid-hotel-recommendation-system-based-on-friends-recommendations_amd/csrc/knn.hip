@@ -442,20 +442,35 @@ __global__ __launch_bounds__(K2_NT) void scan3_kernel(const float* __restrict__ 
 constexpr int TH_S = KNN_TH_S;   // sample rows: the bound sits near quantile k / TH_S
 constexpr float TH_MARGIN = 1e-5f;
 
-// The k-th smallest sample distance by a 2-pass radix select over the
-// distances' bits (exponent + 7 mantissa bits): the upper edge of the
-// selected bin, an upper bound within 2^-7 relative of the exact k-th value.
+// Block qq: normalises query qq (sklearn normalize(): zero norm -> unchanged;
+// written to qn for the scan) and takes the k-th smallest sample distance by
+// a 2-pass radix select over the distances' bits (exponent + 7 mantissa
+// bits): the upper edge of the selected bin, an upper bound within 2^-7
+// relative of the exact k-th value.
 template <int DV>
 __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict__ tab,
                                                         const float* __restrict__ inv, int64_t N,
-                                                        const float* __restrict__ qn, int k,
-                                                        float* thr0) {
+                                                        const float* __restrict__ q, float* qn,
+                                                        int k, float* thr0) {
   constexpr int PT = TH_S / 256;
+  constexpr int d = DV * 4;   // <= 64: one element per lane
   __shared__ unsigned hist[256];
   __shared__ unsigned sel_prefix, sel_need;
   __shared__ int sel_fail;
+  __shared__ __attribute__((aligned(16))) float qs[d];
   const int64_t qq = blockIdx.x;
-  const float4* qv = reinterpret_cast<const float4*>(qn + qq * DV * 4);
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const float v = lane < d ? q[qq * d + lane] : 0.f;
+    const float ss = wave_sum(v * v);
+    const float in = ss > 0.f ? 1.f / sqrtf(ss) : 1.f;
+    if (lane < d) {
+      qs[lane] = v * in;
+      qn[qq * d + lane] = v * in;
+    }
+  }
+  __syncthreads();
+  const float4* qv = reinterpret_cast<const float4*>(qs);
   const int S = (int)min<int64_t>(N, TH_S);
   unsigned key[PT];
 #pragma unroll 4
@@ -521,23 +536,6 @@ __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict_
     const float kth = __uint_as_float(sel_prefix | 0xffffu);
     thr0[qq] = (sel_fail || !(kth < 2.5f)) ? FLT_MAX : kth + TH_MARGIN;
   }
-}
-
-__global__ void fill_kernel(float* p, int64_t n, float v) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) p[i] = v;
-}
-
-// normalised queries (sklearn normalize(): zero norm -> unchanged), one wave per query
-__global__ void qnorm_kernel(const float* q, int64_t Q, int d, float* qn) {
-  const int lane = threadIdx.x & 63;
-  const int64_t qq = (int64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
-  if (qq >= Q) return;
-  float s = 0.f;
-  for (int i = lane; i < d; i += 64) { const float v = q[qq * d + i]; s += v * v; }
-  s = wave_sum(s);
-  const float in = s > 0.f ? 1.f / sqrtf(s) : 1.f;
-  for (int i = lane; i < d; i += 64) qn[qq * d + i] = q[qq * d + i] * in;
 }
 
 // Per query: the k best of nslices k-lists.  All of a chunk's candidates are
@@ -859,24 +857,17 @@ dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, cons
   if (use_v2(d, k)) {
     plan2(N, &ns, &rps);
     float* qn = (float*)((char*)ws + rup((size_t)Q * ns * k * sizeof(Cand), 256));
-    hipLaunchKernelGGL(qnorm_kernel, dim3((unsigned)cdiv(Q, 4)), dim3(256), 0, s, q, Q, d, qn);
-    DCNR_LAUNCH_CHECK();
-    // admission bounds: worth their launch once several queries share a scan
+    // normalised queries + admission bounds, one block per query
     float* thr0 = qn + Q * d;
-    if (Q >= 1) {
-      switch (d / 4) {
+    switch (d / 4) {
 #define CASEK(n)                                                                           \
   case n:                                                                                  \
     hipLaunchKernelGGL(kth_bound_kernel<n>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, \
-                       qn, k, thr0);                                                       \
+                       q, qn, k, thr0);                                                    \
     break;
-        CASEK(1) CASEK(2) CASEK(3) CASEK(4) CASEK(5) CASEK(6) CASEK(7) CASEK(8)
-        CASEK(9) CASEK(10) CASEK(11) CASEK(12) CASEK(13) CASEK(14) CASEK(15) CASEK(16)
+      CASEK(1) CASEK(2) CASEK(3) CASEK(4) CASEK(5) CASEK(6) CASEK(7) CASEK(8)
+      CASEK(9) CASEK(10) CASEK(11) CASEK(12) CASEK(13) CASEK(14) CASEK(15) CASEK(16)
 #undef CASEK
-      }
-    } else {
-      hipLaunchKernelGGL(fill_kernel, dim3((unsigned)cdiv(Q, 256)), dim3(256), 0, s, thr0, Q,
-                         FLT_MAX);
     }
     DCNR_LAUNCH_CHECK();
     if (Q >= MFMA_MIN_Q && d % 16 == 0) {
