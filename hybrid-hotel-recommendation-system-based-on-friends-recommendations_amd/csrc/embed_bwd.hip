@@ -142,18 +142,35 @@ SortPlan make_plan(const int64_t* rows, int nt, int64_t B) {
 }
 
 // ids[t*B + b] = clamped id of sample b in table t (the forward gather's
-// clamp): one thread per sample reads its user, item and K categorical ids
-// (contiguous), the sort kernels then read each table's ids coalesced.
+// clamp), table-major for the sort kernels.  A block takes ENT samples: the
+// user and item ids one per thread; the block's K categorical columns (one
+// contiguous K x ENT int64 run of `cat`) are read coalesced, transposed
+// through LDS and written as K coalesced rows.
 __global__ __launch_bounds__(ENT) void emb_ids_kernel(SortTabs st, int nt, const int64_t* user,
                                                       const int64_t* item, const int64_t* cat,
                                                       int64_t B, uint32_t* ids) {
-  const int64_t b = (int64_t)blockIdx.x * ENT + threadIdx.x;
-  if (b >= B) return;
-  for (int t = 0; t < nt; ++t) {
-    const int64_t id = t == 0 ? user[b] : t == 1 ? item[b] : cat[b * (nt - 2) + (t - 2)];
+  extern __shared__ uint32_t tr[];   // [K][ENT]
+  const int K = nt - 2;
+  const int64_t b0 = (int64_t)blockIdx.x * ENT;
+  const int nb = (int)min<int64_t>(ENT, B - b0);
+  auto clampr = [&](int64_t id, int t) {
     const int64_t rows = st.rows[t];
-    ids[(int64_t)t * B + b] = (uint32_t)(id < 0 ? 0 : (id >= rows ? rows - 1 : id));
+    return (uint32_t)(id < 0 ? 0 : (id >= rows ? rows - 1 : id));
+  };
+  if (threadIdx.x < nb) {
+    const int64_t b = b0 + threadIdx.x;
+    ids[b] = clampr(user[b], 0);
+    ids[B + b] = clampr(item[b], 1);
   }
+  if (K <= 0) return;
+  const int64_t* cb = cat + b0 * K;
+  for (int j = threadIdx.x; j < nb * K; j += ENT) {
+    const int s = j / K, t = j - s * K;
+    tr[t * ENT + s] = clampr(cb[j], t + 2);
+  }
+  __syncthreads();
+  if (threadIdx.x < nb)
+    for (int t = 0; t < K; ++t) ids[(int64_t)(t + 2) * B + b0 + threadIdx.x] = tr[t * ENT + threadIdx.x];
 }
 
 // Lanes holding the same v (v < 2^nb, among `valid` lanes): this lane's rank
@@ -832,8 +849,9 @@ dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* it
     attr_low = lds_low;
   }
   const dim3 gc((unsigned)p.C, (unsigned)e.n_tab);
-  hipLaunchKernelGGL(emb_ids_kernel, dim3((unsigned)cdiv(B, ENT)), dim3(ENT), 0, s, p.st,
-                     e.n_tab, user, item, cat, B, sb.ids);
+  hipLaunchKernelGGL(emb_ids_kernel, dim3((unsigned)cdiv(B, ENT)), dim3(ENT),
+                     (size_t)std::max(e.n_tab - 2, 1) * ENT * 4, s, p.st, e.n_tab, user, item,
+                     cat, B, sb.ids);
   DCNR_LAUNCH_CHECK();
   hipLaunchKernelGGL(emb_hist_kernel, gc, dim3(ENT), (size_t)p.max_bk * 4, s, p.st, sb.ids, B,
                      p.C, hist);
