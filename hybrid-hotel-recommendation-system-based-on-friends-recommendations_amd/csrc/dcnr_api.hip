@@ -831,6 +831,21 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   if (check) TRYP(DCNR_K_PACK, fill_zero(L.err, 4, s));
   GatherDesc g = make_gather(d, P, desc->n_num);
   CrossParams cp = make_cross(d, P);
+  // train: the embedding backward's id sort needs the ids alone, so it runs
+  // on the side stream under this forward (joined before returning, so the
+  // caller's id tensors are free to go once the forward's work is done)
+  SideJoin sj;
+  if (train) {
+    TRY(sj.fork(s));
+    EmbBwdDesc eb;
+    memset(&eb, 0, sizeof(eb));
+    eb.n_tab = g.n_tab;
+    for (int t = 0; t < g.n_tab; ++t) { eb.rows[t] = g.rows[t]; eb.width[t] = g.width[t]; }
+    hipStream_t s = sj.side;   // TRYB launches and times on the side stream
+    TRYB(DCNR_K_EMB_SORT, 2.0 * 8.0 * g.n_tab * B + 8.0 * B * (2 + d.K) + 4.0 * B * 2,
+         emb_sort(eb, user_ids, item_ids, cat_features, B, L.emb, s));
+    TRY(sj.record());
+  }
   {
     const GcOut o{nullptr, L.x0, L.zc, 0, d.Dp, train ? L.sc : nullptr};
     TRYB(DCNR_K_GATHER_CROSS, (double)B * (gather_row_b(d, desc->n_num) + (double)d.Dp * d.es + 4.0),
@@ -900,6 +915,7 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     TRYB(DCNR_K_HEAD, act_b(d, B) + 4.0 * B, row_dot(d.prec, L.h[d.R], d.Hp, d.H, P.wf, B, L.zdeep, s));
     TRYB(DCNR_K_HEAD, 12.0 * B, head_logits(L.zdeep, L.zc, P.bf, B, logits, s));
   }
+  if (train) TRY(sj.join(s));   // the sorted ids (workspace) for dcnr_backward
   return DCNR_OK;
 }
 
@@ -935,10 +951,8 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     TRYB(DCNR_K_PACK, zb, fill_zero_multi(2 + d.K, zp, zn, s));
   }
 
-  // embedding backward, part 1: sort the (table row, sample) pairs (they
-  // depend on the ids alone).  Measured: on a side stream overlapped with the
-  // deep-tower backward the sort's blocks held CU slots the GEMMs waited for
-  // and the step got slower than running it here.
+  // embedding backward, part 1 (the stable sort of the (table row, sample)
+  // pairs) ran under the train forward (dcnr_forward); its result is in ws
   GatherDesc g = make_gather(d, P, desc->n_num);
   EmbBwdDesc eb;
   memset(&eb, 0, sizeof(eb));
@@ -946,16 +960,14 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   for (int t = 0; t < g.n_tab; ++t) {
     eb.grad[t] = Gr.tab[t]; eb.rows[t] = g.rows[t]; eb.width[t] = g.width[t]; eb.off[t] = g.off[t];
   }
-  // The id sort and the cross backward depend on the ids, dz and the
-  // forward's outputs alone: they run on a side stream under the deep-tower
-  // backward and join before the dense-gradient hook.
+  // The cross backward depends on dz and the forward's outputs alone: it
+  // runs on a side stream under the deep-tower backward and joins before the
+  // dense-gradient hook.
   SideJoin sj;
   TRY(sj.fork(s));
   const CrossParams cpx = make_cross(d, P);
   {
   hipStream_t s = sj.side;   // TRYB launches and times on the side stream
-  TRYB(DCNR_K_EMB_SORT, 2.0 * 8.0 * g.n_tab * B + 8.0 * B * (2 + d.K) + 4.0 * B * 2,
-       emb_sort(eb, user_ids, item_ids, cat_features, B, L.emb, s));
   // ---- cross network + head bias (low-rank form, from the forward's
   // per-sample scalars, dz and the stored x0 alone; cross_bwd.hip)
   CrossGrads cg;

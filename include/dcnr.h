@@ -31,9 +31,11 @@
  *  - All tensor pointers are DEVICE pointers owned by the caller; the
  *    library allocates nothing on the hot path (workspace is caller-owned,
  *    size from dcnr_workspace_size / dcnr_cosine_topk_workspace_size).
- *    dcnr_backward forks part of its work onto one library-owned stream per
- *    device (created on first use) and joins it back into `stream` before it
- *    returns its last kernels; callers see ordinary stream semantics.
+ *    dcnr_forward (train mode: the embedding backward's id sort) and
+ *    dcnr_backward (the cross backward) fork part of their work onto one
+ *    library-owned stream per device (created on first use) and join it back
+ *    into `stream` before they return their last kernels; callers see
+ *    ordinary stream semantics.
  *  - Parameter tables are HOST arrays of device pointers:
  *      params: in the reference's state_dict() order (train.py:136-153):
  *        user_embedding.weight, item_embedding.weight,
