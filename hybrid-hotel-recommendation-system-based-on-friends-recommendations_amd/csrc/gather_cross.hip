@@ -537,8 +537,14 @@ dcnr_status launch_fwd(const GatherDesc& g, const CrossParams& cp, const int64_t
 #ifndef GC_V4_SPW
 #define GC_V4_SPW 4
 #endif
+// waves per launch (measured, same box, tools/ab_variants.sh): writing x0
+// (train / eval forward) 3072 (2048: +20 %, 6144: +12 % kernel time); the
+// gather + cross front alone (configs[1]) 2048 (+6 % pairs/s over 3072)
 #ifndef GC_V4_WAVES
 #define GC_V4_WAVES 3072
+#endif
+#ifndef GC_V4_WAVES_NOX0
+#define GC_V4_WAVES_NOX0 2048
 #endif
 
 template <int R4, int X0BF16>
@@ -547,10 +553,11 @@ dcnr_status launch_v4(const GatherDesc& g, const CrossParams& cp, const int64_t*
                       const GcOut& o, int* err, int check, hipStream_t s) {
   constexpr int SPW = GC_V4_SPW;
   const size_t lds = (size_t)(2 * cp.L + 1) * R4 * WAVE * 16;
-  // about GC_V4_WAVES waves (measured best: ~3 per SIMD resident at once),
-  // every wave taking the same number of tiles
+  // about `target` waves (~2-3 per SIMD resident at once), every wave
+  // taking the same number of tiles
   const int64_t ntiles = cdiv(B, SPW);
-  const int64_t waves = cdiv(ntiles, cdiv(ntiles, GC_V4_WAVES));
+  const int64_t target = o.x0 ? GC_V4_WAVES : GC_V4_WAVES_NOX0;
+  const int64_t waves = cdiv(ntiles, cdiv(ntiles, target));
   const unsigned blocks = (unsigned)cdiv(waves, WPB);
   if (SPW * g.n_tab <= 64)
     hipLaunchKernelGGL((gather_cross_v4_kernel<R4, SPW, 1, X0BF16>), dim3(blocks), dim3(NT), lds, s,
