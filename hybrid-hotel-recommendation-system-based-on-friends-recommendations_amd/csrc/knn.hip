@@ -152,8 +152,12 @@ __global__ __launch_bounds__(NT) void scan_kernel(const float* __restrict__ tab,
 // is XCD-grouped: the blocks that share a row slice run on one XCD, whose L2
 // serves the repeated reads of the slice.
 constexpr int K2_NT = 256, K2_WPB = K2_NT / 64, K2_QT = 32, K2_CAP = 64, K2_KMAX = 32;
+// queries from which the fp32-MFMA scan (v3) is used: measured on one box
+// (tools/ab_knn.sh, 1M x 64, k = 11), the VALU scan is faster up to Q = 8
+// (Q=4: 73 vs 104 us, Q=8: 97 vs 116 us), the MFMA scan from Q = 16
+// (138 vs 153 us; Q=32: 189 vs 265 us)
 #ifndef MFMA_MIN_Q
-#define MFMA_MIN_Q 4   // queries from which the fp32-MFMA scan (v3) is used
+#define MFMA_MIN_Q 16
 #endif
 
 __device__ __forceinline__ void wave_sort64(float& d, int& i, int lane) {
