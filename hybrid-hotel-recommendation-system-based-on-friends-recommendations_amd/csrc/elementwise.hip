@@ -20,7 +20,10 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int UNROLL = 4;
-constexpr int TARGET_CHUNKS = 2048;  // 8 blocks/CU in flight for HBM latency hiding
+#ifndef ROWWISE_RED_CHUNKS
+#define ROWWISE_RED_CHUNKS 2048
+#endif
+constexpr int TARGET_CHUNKS = ROWWISE_RED_CHUNKS;  // 8 blocks/CU in flight for HBM latency hiding
 #ifndef ROWWISE_APPLY_CHUNKS
 #define ROWWISE_APPLY_CHUNKS 8192
 #endif
