@@ -40,7 +40,10 @@ namespace dcnr {
 namespace {
 
 constexpr int ENT = 256;          // threads per block
-constexpr int LIM = 16;           // longest run the short kernel sums in one thread
+#ifndef EMB_SHORT_LIM
+#define EMB_SHORT_LIM 16
+#endif
+constexpr int LIM = EMB_SHORT_LIM;   // longest run the short kernel sums in one thread
 
 struct EmbTabs {
   float* grad[MAX_TABLES];
