@@ -381,7 +381,10 @@ template <typename T> struct Bwd1ApplyOp {
   }
 };
 
-template <typename T, bool G> struct RowUnroll<Bwd2StatsOp<T, G>> { static constexpr int v = 2; };
+#ifndef BWD2_STATS_UNROLL
+#define BWD2_STATS_UNROLL 2
+#endif
+template <typename T, bool G> struct RowUnroll<Bwd2StatsOp<T, G>> { static constexpr int v = BWD2_STATS_UNROLL; };
 template <typename T> struct RowUnroll<BnAddReluHeadOp<T>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<Bwd1ApplyOp<T>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<Bwd2ApplyOp<T>> { static constexpr int v = 2; };
