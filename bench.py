@@ -381,6 +381,40 @@ def bench_fp32(B, dev, pool, world, steps=5, warmup=2):
             "steps": steps, "dtype": "f32"}
 
 
+def measured_peaks(dev, iters=10):
+    """the box's achievable peaks next to the spec ones -- a
+    1 GiB device-to-device stream copy (read + write bytes / time) and a
+    large bf16 GEMM through torch (hipBLASLt), both with HIP events."""
+    n = 1 << 28   # 1 GiB of fp32
+    src = torch.empty(n, dtype=torch.float32, device=dev).uniform_()
+    dst = torch.empty_like(src)
+    for _ in range(2):
+        dst.copy_(src)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        dst.copy_(src)
+    e1.record()
+    torch.cuda.synchronize()
+    copy_gbs = 2 * 4 * n * iters / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del src, dst
+    m = 8192
+    a = torch.randn((m, m), device=dev).to(torch.bfloat16)
+    b = torch.randn((m, m), device=dev).to(torch.bfloat16)
+    for _ in range(2):
+        torch.mm(a, b)
+    e0.record()
+    for _ in range(iters):
+        torch.mm(a, b)
+    e1.record()
+    torch.cuda.synchronize()
+    gemm_tf = 2 * m ** 3 * iters / (e0.elapsed_time(e1) / 1e3) / 1e12
+    del a, b
+    torch.cuda.empty_cache()
+    return {"copy_gbs": copy_gbs, "copy": "1 GiB fp32 device copy (torch), read + write bytes",
+            "bf16_gemm_tflops": gemm_tf, "gemm": "8192^3 bf16 torch.mm (hipBLASLt)"}
+
+
 def pmc_traffic(kernel_class):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -511,6 +545,7 @@ def main():
         dist.all_reduce(ev, op=dist.ReduceOp.MAX)
     pairs_per_s = world * B * args.eval_steps / float(ev.item())
     zipf = None if args.no_zipf else bench_zipf(trainer, dev, B, world)
+    peaks = measured_peaks(dev) if rank == 0 else None
     fp32 = None if args.no_fp32 else bench_fp32(B, dev, pool, world)
     cfg2 = bench_cfg2(model, gen, dev, max(args.steps, 10), world)
     cfg5 = bench_cfg5(dev, 10, world == 1 and rank == 0 and not args.no_cpu_baseline) \
@@ -547,6 +582,7 @@ def main():
                 "achieved": dt["achieved_gbs"], "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                 "frac": dt["frac"], "traffic": pmc_traffic(dom),
                 "bytes_per_launch": dt["bytes_per_launch"], "avg_launch_ms": dt["avg_launch_ms"]}
+        roof["frac_of_measured_copy"] = dt["achieved_gbs"] / peaks["copy_gbs"]
         if dom in GEMM_FLOP:
             flop_launch = GEMM_FLOP[dom] * B * args.steps / prof[dom][1]
             roof["mfma_view"] = {"achieved_tflops": flop_launch / (dt["avg_launch_ms"] / 1e3) / 1e12,
@@ -588,9 +624,12 @@ def main():
             "deep_tower_mfma": {"gemm_ms_per_step": deep_ms, "flop_per_step": deep_flop,
                                 "achieved_tflops": deep_flop / (deep_ms / 1e3) / 1e12 if deep_ms else None,
                                 "frac_of_bf16_peak": deep_flop / (deep_ms / 1e3) / PEAK_BF16 if deep_ms else None,
-                                "step_tflops": deep_flop / (el / args.steps) / 1e12},
+                                "step_tflops": deep_flop / (el / args.steps) / 1e12,
+                                "frac_of_measured_gemm": deep_flop / (deep_ms / 1e3) / 1e12 /
+                                peaks["bf16_gemm_tflops"] if deep_ms else None},
             "fp32_parity_mode": fp32,
             "zipf_ids": zipf,
+            "measured_peaks": peaks,
             "roofline_gather": {"bound": "hbm", "kernel": "gather_cross", "achieved": gather_gbs,
                                 "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                                 "frac": gather_gbs / (PEAK_HBM / 1e9),
