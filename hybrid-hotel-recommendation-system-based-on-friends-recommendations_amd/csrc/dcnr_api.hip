@@ -941,7 +941,9 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   const float* dz = dlogits;
   const int Hp = d.Hp, H = d.H;
   const float p = d.dropout;
-  // dense embedding grads: zeroed, then scatter-added by the cross backward
+  // dense embedding grads: zeroed; the per-row sums (emb_segment_sum) then
+  // write every row an id references.  (On the side stream under the deep
+  // tower instead: 3.99-4.00 vs 3.98-3.99 ms/step, same box; kept here.)
   if (!accumulate) {
     void* zp[2 + MAX_CAT];
     int64_t zn[2 + MAX_CAT];
