@@ -255,7 +255,7 @@ struct Layout {
   void* duk[MAX_RES]; void* dt2k[MAX_RES]; void* dak[MAX_RES]; void* dt1k[MAX_RES];
   float* dx0;                 // deep part of dL/dx0, [B][Dq] (Dq = Dp rounded up to 32)
   float* slab; int64_t slab_elems;
-  float* sc;                  // forward -> backward cross scalars [B][2L+1]
+  float* sc;                 // forward -> backward cross scalars [B][2L+1]
   float* xcoef; float* xalpha;  // [B][L+1] each (cross_bwd.hip)
   void* cscratch; size_t cscratch_bytes;
   // 1-bit keep masks for the backward GEMM epilogues (bf16, Hp % 32 == 0):
@@ -589,11 +589,67 @@ dcnr_status wgrad_bf16(const void* dY, int64_t ldy, int N, const void* X, int64_
   return DCNR_OK;
 }
 
+// The backward's bf16 weight gradients run on the side stream: each call's
+// gemm_dw + split-K reduce are ordered after the main stream's work so far
+// (its dY is complete) and overlap the main stream's next dX GEMM and BN
+// passes. The main stream's next writer of a dY buffer comes after the next
+// call, which first waits for the previous call's GEMM, so the operands stay
+// alive; the reduces share one slab because they are serialised on the side
+// stream. join() orders the main stream after all of it. Same kernels, same
+// order per output: the gradients are unchanged (same-box A/B in DESIGN.md).
+struct DwPipe {
+  hipStream_t side = nullptr;
+  hipEvent_t in_ev = nullptr, dw_ev = nullptr, done_ev = nullptr;
+  int calls = 0;
+  dcnr_status init(hipStream_t side_stream) {
+    side = side_stream;
+    DCNR_HIP(hipEventCreateWithFlags(&in_ev, hipEventDisableTiming));
+    DCNR_HIP(hipEventCreateWithFlags(&dw_ev, hipEventDisableTiming));
+    DCNR_HIP(hipEventCreateWithFlags(&done_ev, hipEventDisableTiming));
+    return DCNR_OK;
+  }
+  dcnr_status wgrad(const Layout& L, const void* dY, int64_t ldy, int N, const void* X, int64_t ldx,
+                    int Kc, int64_t B, float* out, int Nr, int Kr, int accumulate, hipStream_t main_s) {
+    if (calls++) DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev, 0));
+    DCNR_HIP(hipEventRecord(in_ev, main_s));
+    DCNR_HIP(hipStreamWaitEvent(side, in_ev, 0));
+    hipStream_t s = side;   // TRYB launches and times on the side stream
+    const int S = gemm_dw_splits(N, Kc, B);
+    if ((int64_t)S * N * Kc > L.slab_elems) {
+      set_error("wgrad: slab too small");
+      return DCNR_WORKSPACE_TOO_SMALL;
+    }
+    DwArgs a;
+    memset(&a, 0, sizeof(a));
+    a.A = (const bf16*)dY; a.lda = ldy; a.B = (const bf16*)X; a.ldb = ldx;
+    a.C = L.slab; a.ldc = Kc; a.slab_stride = (int64_t)N * Kc;
+    a.Btot = B; a.k_per_split = rup(cdiv(B, S), 64);
+    a.N = N; a.K = Kc; a.splits = S;
+    TRYB(DCNR_K_GEMM_DW, 2.0 * B * (N + Kc) + 4.0 * Nr * Kr * (accumulate ? 2 : 1), gemm_dw(a, s));
+    DCNR_HIP(hipEventRecord(dw_ev, s));
+    TRYB(DCNR_K_REDUCE, 4.0 * S * N * Kc + 4.0 * Nr * Kr * (accumulate ? 2 : 1),
+         splitk_reduce(L.slab, S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s));
+    return DCNR_OK;
+  }
+  dcnr_status join(hipStream_t main_s) {
+    if (!calls) return DCNR_OK;
+    DCNR_HIP(hipEventRecord(done_ev, side));
+    DCNR_HIP(hipStreamWaitEvent(main_s, done_ev, 0));
+    return DCNR_OK;
+  }
+  ~DwPipe() {
+    for (auto e : {in_ev, dw_ev, done_ev})
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
 dcnr_status linear_dw(const Dims& d, const Layout& L, const void* dY, int ldy, int N,
                       const void* X, int ldx, int Kc, int64_t B, float* out, int Nr, int Kr,
-                      int accumulate, hipStream_t s) {
-  if (d.prec == DCNR_PREC_BF16 && gemm_dw_supported(N, Kc, ldy, ldx, B))
+                      int accumulate, hipStream_t s, DwPipe* pipe = nullptr) {
+  if (d.prec == DCNR_PREC_BF16 && gemm_dw_supported(N, Kc, ldy, ldx, B)) {
+    if (pipe) return pipe->wgrad(L, dY, ldy, N, X, ldx, Kc, B, out, Nr, Kr, accumulate, s);
     return wgrad_bf16(dY, ldy, N, X, ldx, Kc, B, L.slab, L.slab_elems, out, Nr, Kr, accumulate, s);
+  }
   int64_t tiles = cdiv(N, 128) * cdiv(Kc, 128);
   int64_t S = std::max<int64_t>(1, std::min<int64_t>(512 / tiles, cdiv(B, 256)));
   int64_t kps = rup(cdiv(B, S), 64);
@@ -983,6 +1039,14 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
                       L.xalpha, L.cscratch, L.cscratch_bytes, accumulate, s));
   }
   TRY(sj.record());
+  DwPipe dwp;
+  DwPipe* pipe = nullptr;
+  // (not while kernel classes are being timed: there every launch is priced
+  // alone, on the main stream, as before the overlap)
+  if (d.prec == DCNR_PREC_BF16 && !g_prof) {
+    TRY(dwp.init(sj.side));
+    pipe = &dwp;
+  }
 
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   const bool fuse = epi_stats_ok(d);   // BN partials from the dX GEMM epilogues
@@ -1012,7 +1076,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn2_apply2(d.prec, du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
                        dt2, L.part, &nc, s));
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
-    TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s));
+    TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe));
     if (fuse) {
       // dy1 = (dt2 W2) * [a1 != 0] / (1-p): relu and dropout masks from the
       // saved activation, BN1 partials (and, without SyncBN, its backward
@@ -1035,7 +1099,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_apply2(d.prec, da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, dt1,
                        L.part, &nc, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
-    TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s));
+    TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe));
     if (fuse && j > 0) {
       // G is only consumed by block j-1's BN2 backward: emit its du = G * [h_j > 0]
       // (in place over this block's du, the residual operand, unless
@@ -1059,8 +1123,11 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   int nc = 0;
   TRYB(DCNR_K_ROWWISE, act_b(d, B), col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
   TRY(bias_reduce(d, L, nc, Gr.b0, accumulate, s));
-  TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s));
+  TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s, pipe));
   TRY(sj.join(s));   // the side stream's cross gradients, coefficients and sorted ids
+  // and the weight gradients; without a hook nothing reads them before the
+  // optimizer, so they join at the end (under the dx0 GEMM and embedding sums)
+  if (desc->grad_ready) TRY(dwp.join(s));
   TRY(grads_ready(desc, DCNR_GRADS_DENSE, s));   // every non-embedding gradient is enqueued
   {
     GemmArgs g;
@@ -1078,6 +1145,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   eb.V[d.L] = cpx.wf_cross;
   TRYB(DCNR_K_EMB_SUM, (double)B * (4.0 * ew + (8.0 + 4.0 * (d.L + 1)) * g.n_tab),
        emb_segment_sum(eb, L.emb, B, L.dx0, dq_of(d), L.xcoef, accumulate, s));
+  if (!desc->grad_ready) TRY(dwp.join(s));
   TRY(grads_ready(desc, DCNR_GRADS_EMBEDDING, s));
   return DCNR_OK;
 }

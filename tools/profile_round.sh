@@ -18,4 +18,6 @@ python3 tools/stats_summary.py $OUT/trace/run_kernel_stats.csv \
     "rocprofv3 --kernel-trace --stats of \`python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-serving --no-fp32 --no-zipf\`" \
     > $OUT/kernel_summary.txt &&
 python3 tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \
-    --json $OUT/pmc_traffic.json > $OUT/pmc_traffic.txt
+    --json $OUT/pmc_traffic.json > $OUT/pmc_traffic.txt &&
+python3 tools/trace_passes.py $OUT/trace/run_kernel_trace.csv gemm_dw_kernel --per-step 9 \
+    --warmup 5 --steps 20 > $OUT/gemm_dw_passes.txt
