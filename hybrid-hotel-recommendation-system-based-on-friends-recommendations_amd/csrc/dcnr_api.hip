@@ -608,11 +608,18 @@ struct DwPipe {
     DCNR_HIP(hipEventCreateWithFlags(&done_ev, hipEventDisableTiming));
     return DCNR_OK;
   }
-  dcnr_status wgrad(const Layout& L, const void* dY, int64_t ldy, int N, const void* X, int64_t ldx,
-                    int Kc, int64_t B, float* out, int Nr, int Kr, int accumulate, hipStream_t main_s) {
-    if (calls++) DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev, 0));
+  // order the side stream after the main stream's work so far (and the main
+  // stream after the previous call's GEMM, see above)
+  dcnr_status enter(hipStream_t main_s) {
+    if (calls) DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev, 0));
     DCNR_HIP(hipEventRecord(in_ev, main_s));
     DCNR_HIP(hipStreamWaitEvent(side, in_ev, 0));
+    return DCNR_OK;
+  }
+  dcnr_status wgrad(const Layout& L, const void* dY, int64_t ldy, int N, const void* X, int64_t ldx,
+                    int Kc, int64_t B, float* out, int Nr, int Kr, int accumulate, hipStream_t main_s) {
+    TRY(enter(main_s));
+    ++calls;
     hipStream_t s = side;   // TRYB launches and times on the side stream
     // (the full-chip split count: 32 / 16 splits, leaving CUs to the main
     // stream and halving the slab, measured 2 % / 21 % slower per step)
@@ -1122,9 +1129,17 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     }
   }
   // ---- initial layer
-  int nc = 0;
-  TRYB(DCNR_K_ROWWISE, act_b(d, B), col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
-  TRY(bias_reduce(d, L, nc, Gr.b0, accumulate, s));
+  // its bias gradient (column sums of G) also goes under the dx0 GEMM and
+  // the embedding sums when the pipe runs (L.part and the reduction counters
+  // are not used by the main stream after the blocks)
+  {
+    hipStream_t main_s = s;
+    if (pipe) TRY(pipe->enter(main_s));
+    hipStream_t s = pipe ? pipe->side : main_s;
+    int nc = 0;
+    TRYB(DCNR_K_ROWWISE, act_b(d, B), col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
+    TRY(bias_reduce(d, L, nc, Gr.b0, accumulate, s));
+  }
   TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s, pipe));
   TRY(sj.join(s));   // the side stream's cross gradients, coefficients and sorted ids
   // and the weight gradients; without a hook nothing reads them before the
