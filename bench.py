@@ -468,10 +468,19 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # DCNR_BENCH_REHEARSE=1: every rank on cuda:0 over gloo, to exercise the
+    # N>1 code path (exchange, max-over-ranks timing, sharded index, the JSON
+    # line) on a one-GPU box; its numbers are not a scaling measurement
+    rehearse = os.environ.get("DCNR_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     import dcnr
     from dcnr import _lib
@@ -641,6 +650,8 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
+        if rehearse:
+            out["rehearsal"] = "DCNR_BENCH_REHEARSE: all ranks on cuda:0 over gloo (not a scaling number)"
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
