@@ -40,6 +40,8 @@ GEMM_FLOP = {  # algorithmic FLOPs per sample per step (13.98 MFLO
     "gemm_dx": 2 * (2 * R * H * H + H * D),
     "gemm_dw": 2 * (2 * R * H * H + H * D),
 }
+# eval forward (scoring) FLOPs per (user, hotel) pair: the deep tower's GEMMs
+EVAL_FLOP_PER_PAIR = 2 * (D * H + 2 * R * H * H)
 # gather + x0 + 3 cross: 14 idx x 8 B + 14 rows x 128 B + 8 x 4 B read; x0 bf16 + zc written
 GATHER_BYTES = 14 * 8 + 14 * 32 * 4 + 8 * 4 + D * 2 + 4
 # algorithmic HBM bytes of the forward Linear class per step: X read + C write
@@ -550,9 +552,35 @@ def main():
         if world > 1:
             dist.barrier()
         ev = torch.tensor([time.perf_counter() - t1], device=dev, dtype=torch.float64)
+        # the same eval calls once more with every launch bracketed by HIP
+        # events: the library's algorithmic bytes per scored pair and the
+        # per-class times of the eval forward (main.py:319-322)
+        torch.cuda.synchronize()
+        _lib.profile_enable(True)
+        _lib.profile_collect()
+        for k in range(args.eval_steps):
+            model(*pool[k % len(pool)][:4])
+        torch.cuda.synchronize()
+        _lib.profile_enable(False)
+        eprof = _lib.profile_collect(with_bytes=True)
     if world > 1:
         dist.all_reduce(ev, op=dist.ReduceOp.MAX)
     pairs_per_s = world * B * args.eval_steps / float(ev.item())
+    n_pairs = B * args.eval_steps
+    eval_bytes_pair = sum(v[2] for v in eprof.values() if v[1]) / n_pairs
+    eval_gbs = eval_bytes_pair * pairs_per_s / world / 1e9   # per GPU
+    eval_tf = EVAL_FLOP_PER_PAIR * pairs_per_s / world / 1e12
+    eval_roof = {
+        "bound": "hbm", "unit": "GB/s", "scope": "whole eval forward (every launch), per GPU",
+        "bytes_per_pair": eval_bytes_pair, "achieved": eval_gbs, "peak": PEAK_HBM / 1e9,
+        "frac": eval_gbs * 1e9 / PEAK_HBM,
+        "flop_per_pair": EVAL_FLOP_PER_PAIR,
+        "mfma_view": {"achieved_tflops": eval_tf, "peak_tflops": PEAK_BF16 / 1e12,
+                      "frac": eval_tf * 1e12 / PEAK_BF16},
+        "by_class": {k: {"ms_per_call": v[0] / args.eval_steps, "launches_per_call":
+                         v[1] / args.eval_steps, "bytes_per_pair": v[2] / n_pairs}
+                     for k, v in eprof.items() if v[1]},
+    }
     zipf = None if args.no_zipf else bench_zipf(trainer, dev, B, world)
     peaks = measured_peaks(dev) if rank == 0 else None
     fp32 = None if args.no_fp32 else bench_fp32(B, dev, pool, world)
@@ -627,6 +655,7 @@ def main():
                            else "dense params: all-reduce started in the backward (overlapped); "
                                 "tables: reduce-scatter + sharded AdamW + all-gather")},
             "scored_pairs_per_sec": pairs_per_s,
+            "scored_pairs_roofline": eval_roof,
             "final_loss": final_loss,
             "roofline": roof,
             "roofline_by_class": table,

@@ -17,7 +17,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 namespace dcnr {
@@ -31,6 +33,19 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
 }
 
+dcnr_status set_max_dyn_lds(const void* kernel, size_t bytes) {
+  static std::mutex mu;
+  static std::map<std::pair<const void*, int>, size_t> done;
+  int dev = 0;
+  DCNR_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lk(mu);
+  size_t& cur = done[{kernel, dev}];
+  if (bytes > cur) {
+    DCNR_HIP(hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+    cur = bytes;
+  }
+  return DCNR_OK;
+}
 
 // ------------------------------------------------------------ profiling
 // Optional per-launch HIP-event timing by kernel class (dcnr_profile_*).
@@ -106,23 +121,31 @@ dcnr_status side_stream(hipStream_t* out) {
   *out = streams[dev];
   return DCNR_OK;
 }
+// Every exit path orders the side stream's work before the caller's stream:
+// an error return between fork() and join() (a failed hook, a too-small
+// scratch) must not let the caller free buffers the side stream still
+// writes, so the destructor joins whatever was not joined.
 struct SideJoin {
-  hipStream_t side = nullptr;
+  hipStream_t side = nullptr, main = nullptr;
   hipEvent_t fork_ev = nullptr, join_ev = nullptr, mark_ev = nullptr;
+  bool recorded = false, joined = false;
   dcnr_status fork(hipStream_t s) {
     TRY(side_stream(&side));
     DCNR_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
     DCNR_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
     DCNR_HIP(hipEventRecord(fork_ev, s));
     DCNR_HIP(hipStreamWaitEvent(side, fork_ev, 0));
+    main = s;
     return DCNR_OK;
   }
   dcnr_status record() {
     DCNR_HIP(hipEventRecord(join_ev, side));
+    recorded = true;
     return DCNR_OK;
   }
   dcnr_status join(hipStream_t s) {
     DCNR_HIP(hipStreamWaitEvent(s, join_ev, 0));
+    joined = true;
     return DCNR_OK;
   }
   // an intermediate point of the side stream's work that `s` waits for alone
@@ -136,6 +159,10 @@ struct SideJoin {
     return DCNR_OK;
   }
   ~SideJoin() {
+    if (main && join_ev && !joined) {   // error path: join everything enqueued so far
+      (void)hipEventRecord(join_ev, side);
+      (void)hipStreamWaitEvent(main, join_ev, 0);
+    }
     if (mark_ev) (void)hipEventDestroy(mark_ev);
     if (fork_ev) (void)hipEventDestroy(fork_ev);
     if (join_ev) (void)hipEventDestroy(join_ev);
@@ -609,9 +636,10 @@ dcnr_status wgrad_bf16(const void* dY, int64_t ldy, int N, const void* X, int64_
 // stream. join() orders the main stream after all of it. Same kernels, same
 // order per output: the gradients are unchanged (same-box A/B in DESIGN.md).
 struct DwPipe {
-  hipStream_t side = nullptr;
+  hipStream_t side = nullptr, main = nullptr;
   hipEvent_t in_ev = nullptr, dw_ev = nullptr, done_ev = nullptr;
   int calls = 0;
+  bool pending = false;   // side work enqueued since the last join
   dcnr_status init(hipStream_t side_stream) {
     side = side_stream;
     DCNR_HIP(hipEventCreateWithFlags(&in_ev, hipEventDisableTiming));
@@ -625,6 +653,8 @@ struct DwPipe {
     if (calls) DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev, 0));
     DCNR_HIP(hipEventRecord(in_ev, main_s));
     DCNR_HIP(hipStreamWaitEvent(side, in_ev, 0));
+    main = main_s;
+    pending = true;
     return DCNR_OK;
   }
   dcnr_status wgrad(const Layout& L, const void* dY, int64_t ldy, int N, const void* X, int64_t ldx,
@@ -652,12 +682,17 @@ struct DwPipe {
     return DCNR_OK;
   }
   dcnr_status join(hipStream_t main_s) {
-    if (!calls) return DCNR_OK;
+    if (!pending) return DCNR_OK;
     DCNR_HIP(hipEventRecord(done_ev, side));
     DCNR_HIP(hipStreamWaitEvent(main_s, done_ev, 0));
+    pending = false;
     return DCNR_OK;
   }
   ~DwPipe() {
+    if (pending && main) {   // error path: order the side work before the caller's stream
+      (void)hipEventRecord(done_ev, side);
+      (void)hipStreamWaitEvent(main, done_ev, 0);
+    }
     for (auto e : {in_ev, dw_ev, done_ev})
       if (e) (void)hipEventDestroy(e);
   }
@@ -670,6 +705,9 @@ dcnr_status linear_dw(const Dims& d, const Layout& L, const void* dY, int ldy, i
     if (pipe) return pipe->wgrad(L, dY, ldy, N, X, ldx, Kc, B, out, Nr, Kr, accumulate, s);
     return wgrad_bf16(dY, ldy, N, X, ldx, Kc, B, L.slab, L.slab_elems, out, Nr, Kr, accumulate, s);
   }
+  // the generic path below writes the slab on this stream: the side stream's
+  // split-K reduces of earlier calls may still be reading it
+  if (pipe) TRY(pipe->join(s));
   int64_t tiles = cdiv(N, 128) * cdiv(Kc, 128);
   int64_t S = std::max<int64_t>(1, std::min<int64_t>(512 / tiles, cdiv(B, 256)));
   int64_t kps = rup(cdiv(B, S), 64);

@@ -19,6 +19,10 @@ constexpr int WAVE = 64;
 
 // ---------------------------------------------------------------- errors
 void set_error(const char* fmt, ...);
+// Raise a kernel's dynamic-LDS limit to at least `bytes` on the current
+// device: thread-safe and per device (the serving path runs the eval forward
+// from several host threads; one process may drive several devices).
+dcnr_status set_max_dyn_lds(const void* kernel, size_t bytes);
 #define DCNR_HIP(call)                                                              \
   do {                                                                              \
     hipError_t e_ = (call);                                                         \
@@ -27,6 +31,12 @@ void set_error(const char* fmt, ...);
       return DCNR_HIP_ERROR;                                                        \
     }                                                                               \
   } while (0)
+#define TRY_ST(x)                         \
+  do {                                    \
+    dcnr_status st_ = (x);                \
+    if (st_ != DCNR_OK) return st_;       \
+  } while (0)
+
 #define DCNR_LAUNCH_CHECK()                                                         \
   do {                                                                              \
     hipError_t e_ = hipGetLastError();                                              \

@@ -36,6 +36,8 @@
 #include <cstring>
 #include <algorithm>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 namespace dcnr {
 namespace {
 
@@ -412,6 +414,35 @@ __global__ __launch_bounds__(ENT) void emb_bucket_sort_kernel(SortTabs st, L2Map
     }
     if (last) *slot = pos - rank + cnt;
   }
+}
+
+// Tables of more than 2^24 rows (beyond the two counting levels): one stable
+// LSD radix sort (rocPRIM) of key = base_t + id, value = sample over all
+// tables at once.  Every table contributes exactly B keys and the keys of
+// table t lie in [base_t, base_t + rows_t), so table t still lands in
+// [t*B, (t+1)*B) in ascending (id, sample) order: the same output as the
+// counting sort, at the cost of ~4 8-bit passes.
+__global__ __launch_bounds__(ENT) void emb_keys_kernel(SortTabs st, const uint32_t* ids, int64_t B,
+                                                       int64_t n, uint32_t* keys, uint32_t* vals) {
+  const int64_t i = (int64_t)blockIdx.x * ENT + threadIdx.x;
+  if (i >= n) return;
+  const int t = (int)(i / B);
+  keys[i] = st.base[t] + ids[i];
+  vals[i] = (uint32_t)(i - (int64_t)t * B);
+}
+
+size_t radix_tmp_bytes(int64_t n, int end_bit) {
+  size_t bytes = 0;
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                  (const uint32_t*)nullptr, (uint32_t*)nullptr, (size_t)n, 0u,
+                                  (unsigned)end_bit, (hipStream_t)0);
+  return bytes;
+}
+
+uint64_t total_rows(const int64_t* rows, int nt) {
+  uint64_t total = 0;
+  for (int i = 0; i < nt; ++i) total += (uint64_t)rows[i];
+  return total;
 }
 
 template <int VEC> struct Vec;
@@ -816,41 +847,56 @@ int64_t huge_segs(int nt, int64_t B) { return cdiv((int64_t)nt * B, (int64_t)HSE
 
 size_t emb_sort_tmp_bytes(const int64_t* rows, const int* width, int nt, int64_t B) {
   const SortPlan p = make_plan(rows, nt, B);
-  // the sort's counts are dead once the sort is done: the sums reuse them
-  // for the huge-run pieces
-  return std::max((size_t)p.total_bk * (size_t)std::max(p.C, 1) * 4,
-                  (size_t)huge_segs(nt, B) * 2 * huge_stride(width, nt) * 4);
+  // the sort's counts (or the radix sort's scratch) are dead once the sort
+  // is done: the sums reuse them for the huge-run pieces
+  const size_t pieces = (size_t)huge_segs(nt, B) * 2 * huge_stride(width, nt) * 4;
+  if (!p.ok) {
+    const uint64_t total = total_rows(rows, nt);
+    return std::max(radix_tmp_bytes((int64_t)nt * B, std::max(1, nbits64(total - 1))), pieces);
+  }
+  return std::max((size_t)p.total_bk * (size_t)std::max(p.C, 1) * 4, pieces);
 }
 
 dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* item,
                      const int64_t* cat, int64_t B, const EmbSortBufs& sb, hipStream_t s) {
   const int64_t n = (int64_t)e.n_tab * B;
   if (n <= 0) return DCNR_OK;
-  uint64_t total = 0;
-  for (int i = 0; i < e.n_tab; ++i) total += (uint64_t)e.rows[i];
+  const uint64_t total = total_rows(e.rows, e.n_tab);
   const SortPlan p = make_plan(e.rows, e.n_tab, B);
-  if (!p.ok || total >= (1ull << 32) || n >= (1ll << 32)) {
-    set_error("embedding backward: tables of > 2^24 rows, %llu rows in all or %lld ids "
-              "unsupported", (unsigned long long)total, (long long)n);
+  if (total >= (1ull << 32) || n >= (1ll << 32)) {   // 32-bit sort keys / positions
+    set_error("embedding backward: %llu table rows in all or %lld ids (>= 2^32) unsupported",
+              (unsigned long long)total, (long long)n);
     return DCNR_UNSUPPORTED_SHAPE;
+  }
+  if (!p.ok) {   // a table of > 2^24 rows: one stable radix sort (emb_keys_kernel)
+    const int end_bit = std::max(1, nbits64(total - 1));
+    size_t need = radix_tmp_bytes(n, end_bit);
+    if (need > sb.tmp_bytes) {
+      set_error("embedding backward: radix-sort scratch too small");
+      return DCNR_WORKSPACE_TOO_SMALL;
+    }
+    hipLaunchKernelGGL(emb_ids_kernel, dim3((unsigned)cdiv(B, ENT)), dim3(ENT),
+                       (size_t)std::max(e.n_tab - 2, 1) * ENT * 4, s, p.st, e.n_tab, user, item,
+                       cat, B, sb.ids);
+    DCNR_LAUNCH_CHECK();
+    hipLaunchKernelGGL(emb_keys_kernel, dim3((unsigned)cdiv(n, ENT)), dim3(ENT), 0, s, p.st, sb.ids,
+                       B, n, sb.keys, sb.vals);
+    DCNR_LAUNCH_CHECK();
+    size_t tb = sb.tmp_bytes;
+    DCNR_HIP(rocprim::radix_sort_pairs(sb.tmp, tb, (const uint32_t*)sb.keys, sb.keys_s,
+                                       (const uint32_t*)sb.vals, sb.vals_s, (size_t)n, 0u,
+                                       (unsigned)end_bit, s));
+    return DCNR_OK;
   }
   if ((size_t)p.total_bk * p.C * 4 > sb.tmp_bytes) {
     set_error("embedding backward: sort scratch too small");
     return DCNR_WORKSPACE_TOO_SMALL;
   }
   uint32_t* hist = (uint32_t*)sb.tmp;
-  static size_t attr_bk = 0, attr_low = 0;   // dynamic LDS above the 64 KiB default
+  // dynamic LDS above the 64 KiB default
   const size_t lds_bk = (size_t)SC_W * p.max_bk * 4, lds_low = (size_t)4 * p.max_low * 4;
-  if (lds_bk > 65536 && lds_bk > attr_bk) {
-    DCNR_HIP(hipFuncSetAttribute((const void*)emb_scatter_kernel,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bk));
-    attr_bk = lds_bk;
-  }
-  if (lds_low + ENT * 4 > 65536 && lds_low > attr_low) {
-    DCNR_HIP(hipFuncSetAttribute((const void*)emb_bucket_sort_kernel,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_low));
-    attr_low = lds_low;
-  }
+  if (lds_bk > 65536) TRY_ST(set_max_dyn_lds((const void*)emb_scatter_kernel, lds_bk));
+  if (lds_low + ENT * 4 > 65536) TRY_ST(set_max_dyn_lds((const void*)emb_bucket_sort_kernel, lds_low));
   const dim3 gc((unsigned)p.C, (unsigned)e.n_tab);
   hipLaunchKernelGGL(emb_ids_kernel, dim3((unsigned)cdiv(B, ENT)), dim3(ENT),
                      (size_t)std::max(e.n_tab - 2, 1) * ENT * 4, s, p.st, e.n_tab, user, item,

@@ -177,12 +177,7 @@ dcnr_status gemm_dw(const DwArgs& a0, hipStream_t s) {
     set_error("gemm_dw: unsupported N=%d K=%d splits=%d", a.N, a.K, a.splits);
     return DCNR_UNSUPPORTED_SHAPE;
   }
-  static bool attr_set = false;
-  if (!attr_set) {
-    DCNR_HIP(hipFuncSetAttribute((const void*)gemm_dw_kernel,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, LDS_DW));
-    attr_set = true;
-  }
+  TRY_ST(set_max_dyn_lds((const void*)gemm_dw_kernel, LDS_DW));
   a.tiles_n = (int)cdiv(a.N, TNW);
   a.tiles_k = (int)cdiv(a.K, TKW);
   const int grid = a.tiles_n * a.tiles_k * a.splits;

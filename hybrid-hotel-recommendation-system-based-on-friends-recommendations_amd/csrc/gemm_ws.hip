@@ -31,6 +31,17 @@
 #ifndef WS_PREFETCH_PIN
 #define WS_PREFETCH_PIN 1
 #endif
+// lab overrides (tools/ws_lab.sh EXTRA=...): tile rows, ring depth, static
+// priority of waves 4-7
+#ifndef WS_TM_OVR
+#define WS_TM_OVR 0
+#endif
+#ifndef WS_NB_OVR
+#define WS_NB_OVR 0
+#endif
+#ifndef WS_PRIO
+#define WS_PRIO 0
+#endif
 
 namespace dcnr {
 namespace {
@@ -42,12 +53,14 @@ namespace {
 // ahead, DROP_BN 104.7 vs 111.9 us at 64 rows); eval BN_RELU at 32 rows
 // (71.5 vs 75.4-77.2 us at 64).
 constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
-template <int EPI> constexpr int ws_tm() { return EPI <= NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS ? 64 : 32; }
+template <int KTP, int EPI> constexpr int ws_tm() {
+  return WS_TM_OVR && KTP == 16 ? WS_TM_OVR : (EPI <= NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS ? 64 : 32);
+}
 template <int EPI> constexpr bool ws_ops_early() {
   return EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN || EPI == NT_EPI_BN_RESID_RELU;
 }
 // X-tile buffers in the LDS ring: one tile in flight while one is consumed.
-template <int EPI> constexpr int ws_nb() { return 2; }
+template <int KTP, int EPI> constexpr int ws_nb() { return WS_NB_OVR && KTP == 16 ? WS_NB_OVR : 2; }
 
 template <int KTP, int TM, int NB = 2> struct WsCfg {
   static constexpr int P = KTP * 64;                      // LDS bytes per X row
@@ -57,6 +70,8 @@ template <int KTP, int TM, int NB = 2> struct WsCfg {
   static constexpr int DPW = TM / RPD / WS_WAVES;         // DMAs per wave per tile
   static constexpr int RB = TM / 16;                      // 16-row blocks per tile
   static constexpr size_t LDS_BYTES = NB * (size_t)TILE + 3 * WS_TN * 4 + 16;  // + hand-off flag
+  static_assert(TM % (RPD * WS_WAVES) == 0 && TM % 16 == 0, "tile rows");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
 typedef float f2v __attribute__((ext_vector_type(2)));
@@ -104,8 +119,8 @@ __device__ __forceinline__ void issue_tile(u32x4 xr, int64_t ldx, int K, uint32_
 
 template <int KTP, int EPI>
 __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
-  constexpr int WS_TM = ws_tm<EPI>();
-  constexpr int NB = ws_nb<EPI>();
+  constexpr int WS_TM = ws_tm<KTP, EPI>();
+  constexpr int NB = ws_nb<KTP, EPI>();
   using C = WsCfg<KTP, WS_TM, NB>;
   constexpr int WS_RB = C::RB;
   constexpr bool STATS = EPI >= NT_EPI_BIAS_STATS && EPI <= NT_EPI_DROP_BN;
@@ -198,6 +213,9 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   int coff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) coff[j] = ((4 * j + q) ^ l15) * 16;
+  if constexpr (WS_PRIO) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
   int buf = 0;
   for (int64_t mt = group; mt < a.mtiles; mt += groups, buf = buf + 1 == NB ? 0 : buf + 1) {
     const int64_t mn = mt + (int64_t)(NB - 1) * groups;
@@ -413,14 +431,9 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
 
 template <int KTP, int EPI>
 dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
-  constexpr int WS_TM = ws_tm<EPI>();
-  using C = WsCfg<KTP, WS_TM, ws_nb<EPI>()>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    DCNR_HIP(hipFuncSetAttribute((const void*)gemm_ws_kernel<KTP, EPI>,
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)C::LDS_BYTES));
-    attr_set = true;
-  }
+  constexpr int WS_TM = ws_tm<KTP, EPI>();
+  using C = WsCfg<KTP, WS_TM, ws_nb<KTP, EPI>()>;
+  TRY_ST(set_max_dyn_lds((const void*)gemm_ws_kernel<KTP, EPI>, C::LDS_BYTES));
   a.nslices = (int)cdiv(a.N, WS_TN);
   // 32-bit buffer offsets: launch in M-chunks of < 2^29 bytes per operand
   const int64_t maxld = std::max<int64_t>({a.ldx, a.ldc * 2, a.R ? a.ldr : 0, a.Hb ? a.ldhb * 2 : 0,

@@ -387,12 +387,7 @@ dcnr_status mmr_rerank(const float* table, const float* inv, int d, const int64_
   // same order, as the kernel that re-reads them from the table)
   const size_t lds = ((size_t)n * (d + 1) + (size_t)n) * sizeof(float);
   if (lds <= MMR_LDS_MAX) {
-    static bool attr = false;
-    if (!attr) {
-      DCNR_HIP(hipFuncSetAttribute((const void*)mmr_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (int)MMR_LDS_MAX));
-      attr = true;
-    }
+    TRY_ST(set_max_dyn_lds((const void*)mmr_lds_kernel, MMR_LDS_MAX));
     hipLaunchKernelGGL(mmr_lds_kernel, dim3(1), dim3(SV_NT), lds, s, table, inv, d, rows, scores, (int)n,
                        lambda, top_k, out_pos, out_count);
   } else {

@@ -23,6 +23,7 @@ synchronisation per call); ``False`` clamps silently.
 from __future__ import annotations
 
 import ctypes
+import threading
 from typing import Any, Dict, List, Optional
 
 import numpy as np
@@ -99,27 +100,35 @@ def dropout_seed(dev: torch.device, advance: bool = True) -> int:
 class IndexErrorWatch:
     """Deferred id checks: the device error word of each call is copied into
     a pinned ring slot after the call (stream-ordered, no host wait) and
-    polled without blocking; a set word raises IndexError."""
+    polled without blocking; a set word raises IndexError.  Thread-safe:
+    the serving path scores from Starlette's threadpool (main.py:306-307 is
+    a sync ``def``), so slot assignment and polling hold a lock."""
     RING = 8
 
     def __init__(self):
         self.ring = None
         self.pending = []
         self.next = 0
+        self.lock = threading.Lock()
 
     def push(self, word: torch.Tensor):
-        if self.ring is None:
-            self.ring = torch.zeros(self.RING, dtype=torch.int32, pin_memory=True)
-        if len(self.pending) == self.RING:
-            self.poll(oldest=True)
-        slot = self.next
-        self.next = (slot + 1) % self.RING
-        self.ring[slot:slot + 1].copy_(word.view(torch.int32)[:1], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self.pending.append((ev, slot))
+        with self.lock:
+            if self.ring is None:
+                self.ring = torch.zeros(self.RING, dtype=torch.int32, pin_memory=True)
+            if len(self.pending) == self.RING:
+                self._poll(oldest=True)
+            slot = self.next
+            self.next = (slot + 1) % self.RING
+            self.ring[slot:slot + 1].copy_(word.view(torch.int32)[:1], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self.pending.append((ev, slot))
 
     def poll(self, oldest=False, all_=False):
+        with self.lock:
+            self._poll(oldest, all_)
+
+    def _poll(self, oldest=False, all_=False):
         keep = []
         for n, (ev, slot) in enumerate(self.pending):
             if all_ or (oldest and n == 0):
@@ -172,12 +181,13 @@ class DCN_RecSys(nn.Module):
         self.keep_intermediates = False   # tests: per-block backward buffers (stage checks)
         self.bn_allreduce = None   # set by dcnr.parallel for SyncBN
         self._sync_bn_hook = None
-        self.grad_ready = None     # set by FusedTrainer (data-parallel exchange overlap)
         self._active_ws = None
         self._flat = None
 
     # ------------------------------------------------------------ native glue
-    def desc(self) -> _lib.ModelDesc:
+    def desc(self, grad_ready=None) -> _lib.ModelDesc:
+        """The native model descriptor.  ``grad_ready``: the backward's
+        gradient-group hook (FusedTrainer passes it per call)."""
         d = self._dims
         desc = _lib.ModelDesc()
         desc.n_users = d['n_users']
@@ -195,8 +205,8 @@ class DCN_RecSys(nn.Module):
             (_lib.FLAG_KEEP_INTERMEDIATES if getattr(self, 'keep_intermediates', False) else 0)
         if self.bn_allreduce is not None:
             desc.bn_allreduce = self.bn_allreduce
-        if getattr(self, 'grad_ready', None) is not None:
-            desc.grad_ready = self.grad_ready
+        if grad_ready is not None:
+            desc.grad_ready = grad_ready
         return desc
 
     # Host-side dispatch cost matters for small serving batches: building
@@ -214,7 +224,6 @@ class DCN_RecSys(nn.Module):
         st.pop('_ptr_cache', None)
         st['_index_watch'] = IndexErrorWatch()
         st.pop('_gc_flag', None)
-        st['grad_ready'] = None   # bound to a trainer; ctypes callbacks do not copy
         return st
 
     def check_index_errors(self):
@@ -350,11 +359,13 @@ class DCN_RecSys(nn.Module):
             raise ValueError("out must be a contiguous fp32 [B, D] tensor")
         x0 = torch.empty((B, D), dtype=torch.float32, device=dev) if return_x0 else None
         flag = None
-        if self.check_indices:
-            flag = self.__dict__.get('_gc_flag')
-            if flag is None or flag.device != dev:
+        if self.check_indices:   # one error flag per host thread (re-entrant)
+            flags = self.__dict__.setdefault('_gc_flag', {})
+            key = (threading.get_ident(), dev)
+            flag = flags.get(key)
+            if flag is None:
                 flag = torch.zeros(1, dtype=torch.int32, device=dev)
-                self.__dict__['_gc_flag'] = flag
+                flags[key] = flag
             else:
                 flag.zero_()
         lib = _lib.load()
@@ -447,11 +458,12 @@ def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
 
 
 def run_backward(model: DCN_RecSys, user, item, cat, num, dlogits, ws, grads: List[torch.Tensor],
-                 seed: int, accumulate=False):
-    """``seed`` must be the dropout seed of the train-mode forward that filled ws."""
+                 seed: int, accumulate=False, grad_ready=None):
+    """``seed`` must be the dropout seed of the train-mode forward that filled ws.
+    ``grad_ready``: optional dcnr_grad_ready_fn for this call only."""
     lib = _lib.load()
     B = user.shape[0]
-    desc = model.desc()
+    desc = model.desc(grad_ready)
     model._active_ws = ws
     st = lib.dcnr_backward(ctypes.byref(desc), model.state_ptr_array(),
                            _lib.ptr_array(grads), user.data_ptr(), item.data_ptr(),

@@ -68,9 +68,11 @@ class FusedTrainer:
                                   device=self.flat.device) if self.shard else None
         self._dense_work = None
         self._hook_error = None
-        if self.world > 1:   # start the dense segment's all-reduce from inside the backward
-            self._grad_ready_cb = _lib.GRAD_READY_FN(self._on_grads_ready)
-            model.grad_ready = self._grad_ready_cb
+        # world > 1: the dense segment's all-reduce starts from inside the
+        # backward.  The hook is handed to this trainer's own dcnr_backward
+        # calls only (run_backward(grad_ready=...)), never installed on the
+        # model: a plain autograd backward must not start an exchange.
+        self._grad_ready_cb = _lib.GRAD_READY_FN(self._on_grads_ready) if self.world > 1 else None
         self.lr, self.wd, self.betas, self.eps = lr, weight_decay, betas, eps
         self.decoupled = optimizer_name == 'AdamW'
         self.step_count = 0
@@ -95,13 +97,16 @@ class FusedTrainer:
         self._dense_work = None
         try:
             run_backward(model, user, item, cat, num, dz, self._ws, self._grads, seed,
-                         accumulate=False)
+                         accumulate=False, grad_ready=self._grad_ready_cb)
         except RuntimeError as e:
+            self._dense_work = None
             if self._hook_error is not None:
                 err, self._hook_error = self._hook_error, None
                 raise RuntimeError("gradient exchange hook failed") from err
             raise
-        self.exchange_and_update(user_ids=user)
+        # the all-reduce this step's backward started (None: start it now)
+        dense, self._dense_work = self._dense_work, None
+        self._exchange_and_update(None, user, dense)
         return (loss, logits) if return_logits else loss
 
     def _on_grads_ready(self, ctx, group, stream):
@@ -126,17 +131,18 @@ class FusedTrainer:
         flat buffers.  ``adam(p, g, m, v, step)`` defaults to dcnr_adam_step
         (the CPU tests pass a host restatement to check the exchange).
         ``user_ids``: this rank's batch user ids (the sparse exchange)."""
+        self._exchange_and_update(adam, user_ids, None)
+
+    def _exchange_and_update(self, adam, user_ids, dense):
         adam = adam or self._adam
         self.step_count += 1
         E, Es, world = self.E, self.Es, self.world
         if world == 1:
             adam(self.flat, self.gflat, self.m, self.v, self.step_count)
             return
-        dense = self._dense_work   # started by the backward's hook, or now
-        if dense is None:
+        if dense is None:   # not started by this step's backward: start it now
             dense = dist.all_reduce(self.gflat[E:], op=dist.ReduceOp.SUM, group=self.pg,
                                     async_op=True)
-        self._dense_work = None
         if self.exchange == "sparse":
             from .parallel import sparse_rows_allreduce
             uw = self.model.user_embedding.weight

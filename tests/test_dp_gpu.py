@@ -8,8 +8,18 @@ fp64 statistics buffer across ranks inside the native forward/backward).
 Rank r trains on rows [r*B/2, (r+1)*B/2) of the batch the single process
 trains on whole.  After one step the summed gradient, the logits, the BN
 running statistics and the updated parameters must match the single-process
-step (fp32 mode, dropout 0: the counter-based dropout mask is a function of
-the local row index).
+step (dropout 0: the counter-based dropout mask is a function of the local
+row index), in fp32 (tight bounds) and in bf16 -- the benchmarked N>1 path,
+where the backward's weight gradients run on the library's side stream and
+are joined before the DCNR_GRADS_DENSE hook starts the all-reduce (bounds of
+test_bf16_train_gpu: cos >= 0.98, rel <= 0.25 per tensor; running stats
+1e-2).
+
+test_dp_bf16_hook_ordering pins that join at dropout 0.6: the dense segment
+each rank holds after the exchange the hook started must be bit-identical to
+an explicit all-reduce of the same ranks' gradients from a second, identical
+step run without the hook (the side stream then joins at the end of the
+backward); likewise the embedding segment (all-reduce or reduce-scatter).
 """
 import os
 import socket
@@ -31,13 +41,21 @@ CFG = dict(n_users=3000, n_items=700, cat_dims={"a": 50, "b": 1000, "c": 7}, n_n
 B = 2048
 
 
-def _model(dev):
+def _model(dev, precision="fp32", dropout=0.0):
     import dcnr
     torch.manual_seed(5)
+    params = dict(CFG["params"], dropout=dropout)
     m = dcnr.DCN_RecSys(CFG["n_users"], CFG["n_items"], CFG["cat_dims"], CFG["n_num"],
-                        dict(CFG["params"]), precision="fp32")
+                        params, precision=precision)
     gc.perturb_state(m, 6)
     return m.to(dev)
+
+
+def _cos_rel(a, b):
+    a, b = a.double().reshape(-1), b.double().reshape(-1)
+    cos = (a @ b / (a.norm() * b.norm()).clamp_min(1e-300)).item()
+    rel = ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+    return cos, rel
 
 
 def _batch(dev):
@@ -45,7 +63,7 @@ def _batch(dev):
     return [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (u, i, c, n, y)]
 
 
-def _worker(rank, world, port, path, shard):
+def _worker(rank, world, port, path, shard, precision):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -53,7 +71,7 @@ def _worker(rank, world, port, path, shard):
         import dcnr
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
-        m = _model(dev)
+        m = _model(dev, precision)
         tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, sync_bn=True,
                                shard_optimizer=shard)
         seen = []
@@ -64,7 +82,6 @@ def _worker(rank, world, port, path, shard):
             return hook(ctx, group, stream)
         tr._on_grads_ready = spy
         tr._grad_ready_cb = dcnr._lib.GRAD_READY_FN(spy)
-        m.grad_ready = tr._grad_ready_cb
         lo, hi = rank * B // world, (rank + 1) * B // world
         batch = [t[lo:hi] for t in _batch(dev)]
         loss, z = tr.step(*batch, return_logits=True)
@@ -72,7 +89,27 @@ def _worker(rank, world, port, path, shard):
         assert seen == [dcnr._lib.GRADS_DENSE, dcnr._lib.GRADS_EMBEDDING], seen
         zs = [torch.empty_like(z) for _ in range(world)]
         dist.all_gather(zs, z.contiguous())
-        if rank == 0:
+        if rank == 0 and precision == "bf16":
+            ref = torch.load(path, weights_only=True)
+            zz = torch.cat(zs).cpu().double()
+            assert (zz - ref["z"]).abs().max().item() <= 2e-2 * max(1.0, ref["z"].abs().max().item())
+            bad = []
+            for k, p in m.named_parameters():   # the exchanged (summed) gradients
+                if ".layer" in k and k.endswith(".bias"):    # BN-invariant: ~0
+                    continue
+                if shard and "embedding" in k:   # reduce-scattered into tr.gshard
+                    continue
+                cos, rel = _cos_rel(p.grad.cpu(), ref["grads"][k])
+                if cos < 0.98 or rel > 0.25:
+                    bad.append((k, cos, rel))
+            assert not bad, bad
+            for k, v in m.state_dict().items():
+                if "running" in k:
+                    np.testing.assert_allclose(v.cpu().numpy(), ref["sd"][k].numpy(),
+                                               rtol=1e-2, atol=1e-2, err_msg=k)
+                if "num_batches_tracked" in k:
+                    assert int(v) == int(ref["sd"][k]) == 1
+        elif rank == 0:
             ref = torch.load(path, weights_only=True)
             zz = torch.cat(zs).cpu().double()
             assert (zz - ref["z"]).abs().max().item() <= 1e-5 * max(1.0, ref["z"].abs().max().item())
@@ -106,13 +143,22 @@ def _worker(rank, world, port, path, shard):
         dist.destroy_process_group()
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
 @pytest.mark.parametrize("shard", [False, True])
-def test_dp_world2_syncbn_equals_single_process(dev, shard):
+def test_dp_world2_syncbn_equals_single_process(dev, shard, precision):
     """shard=True: the embedding segment goes through reduce-scatter -> shard
     AdamW -> all-gather, the dense segment's all-reduce is started by the
     backward's DCNR_GRADS_DENSE hook; shard=False: all-reduce of both."""
     import dcnr
-    m = _model(dev)
+    m = _model(dev, precision)
     tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4)
     batch = _batch(dev)
     loss, z = tr.step(*batch, return_logits=True)
@@ -124,8 +170,62 @@ def test_dp_world2_syncbn_equals_single_process(dev, shard):
     with tempfile.TemporaryDirectory() as d:
         path = os.path.join(d, "ref.pt")
         torch.save(ref, path)
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-        s.close()
-        mp.spawn(_worker, args=(2, port, path, shard), nprocs=2, join=True)
+        mp.spawn(_worker, args=(2, _free_port(), path, shard, precision), nprocs=2, join=True)
+
+
+def _worker_hook(rank, world, port, shard):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dcnr
+        from dcnr.model import dropout_seed, run_backward, run_forward
+        from dcnr.ops import bce_with_logits
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        m = _model(dev, "bf16", dropout=0.6)
+        tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, sync_bn=True,
+                               shard_optimizer=shard)
+        lo, hi = rank * B // world, (rank + 1) * B // world
+        u, i, c, n, y = [t[lo:hi] for t in _batch(dev)]
+        gen = torch.cuda.default_generators[0]
+        off0 = gen.get_offset()
+        flat0 = tr.flat.clone()
+        bufs0 = {k: v.clone() for k, v in m.named_buffers()}
+        # 1) the trainer's step: the hook starts the dense all-reduce inside
+        #    the backward, right after the side stream's weight gradients join
+        tr.step(u, i, c, n, y)
+        torch.cuda.synchronize()
+        E = tr.E
+        dense_hook = tr.gflat[E:].clone()
+        emb_hook = (tr.gshard if shard else tr.gflat[:E]).clone()
+        # 2) the same step (same parameters, running stats, dropout seed) with
+        #    no hook: the backward joins its side stream at the end; then an
+        #    explicit all-reduce of the local gradients
+        tr.flat.copy_(flat0)
+        for k, v in m.named_buffers():
+            v.copy_(bufs0[k])
+        gen.set_offset(off0)
+        seed = dropout_seed(dev)
+        uu, ii, cc, nn_ = m.prepare_inputs(u, i, c, n)
+        logits, ws = run_forward(m, True, seed, uu, ii, cc, nn_)
+        _, dz = bce_with_logits(logits, y.reshape(-1).float().contiguous(), True, 1.0 / world)
+        run_backward(m, uu, ii, cc, nn_, dz, ws, tr._grads, seed, accumulate=False)
+        torch.cuda.synchronize()
+        g = tr.gflat.clone()
+        dist.all_reduce(g, op=dist.ReduceOp.SUM)
+        assert torch.equal(dense_hook, g[E:]), "dense segment: hook exchange != explicit all-reduce"
+        Es = tr.Es
+        emb_ref = g[rank * Es:(rank + 1) * Es] if shard else g[:E]
+        assert torch.equal(emb_hook, emb_ref), "embedding segment differs"
+        assert dense_hook.abs().sum().item() > 0
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("shard", [False, True])
+def test_dp_bf16_hook_ordering(dev, shard):
+    """configs[3]'s path in one-GPU rehearsal form: bf16, dropout 0.6, SyncBN,
+    side-stream weight gradients, the grad-ready hook, sharded or all-reduce
+    exchange (train.py:219-226)."""
+    mp.spawn(_worker_hook, args=(2, _free_port(), shard), nprocs=2, join=True)

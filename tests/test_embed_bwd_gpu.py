@@ -297,3 +297,57 @@ def test_side_stream_backward_matches_serial(dev):
         _lib.profile_collect()
     for k, a, b in zip([k for k, _ in m.named_parameters()], g_side, g_serial):
         assert torch.equal(a, b), k
+
+
+def test_huge_table_radix_fallback(dev):
+    """A user table of more than 2^24 rows (beyond the two-level counting
+    sort) takes the stable radix-sort path (emb_keys_kernel + rocPRIM).  The
+    batch's user ids are k * MUL + 11 for small ids k: mapped through that
+    increasing map, the huge model is the small model (same weights on the
+    used rows), the sorted (id, sample) order and the run structure are the
+    same, so every gradient must be BIT-identical to the small model's
+    counting-sort gradients (the user table's at the mapped rows, zero
+    elsewhere) and the logits equal."""
+    import dcnr
+    cat_dims = {"a": 40, "b": 7}
+    params = dict(emb_dim=8, hidden_dim=64, n_cross_layers=2, n_res_blocks=1, dropout=0.0)
+    NS, MUL = 3000, 5600
+    NB = NS * MUL + 16                       # 16.8 M rows > 2^24
+    assert NB > (1 << 24)
+    torch.manual_seed(0)
+    small = dcnr.DCN_RecSys(NS, 120, cat_dims, 3, params, precision="bf16").to(dev)
+    big = dcnr.DCN_RecSys(NB, 120, cat_dims, 3, params, precision="bf16").to(dev)
+    rows = torch.arange(NS, device=dev) * MUL + 11
+    with torch.no_grad():
+        for (k, ps), (_, pb) in zip(small.state_dict().items(), big.state_dict().items()):
+            if k == "user_embedding.weight":
+                pb.zero_()
+                pb[rows] = ps
+            else:
+                pb.copy_(ps)
+    rng = np.random.default_rng(7)
+    B = 4096
+    u = np.minimum(rng.zipf(1.3, B) - 1, NS - 1)   # long runs (popular users) and short ones
+    i = rng.integers(0, 120, B)
+    c = np.stack([rng.integers(0, 40, B), rng.integers(0, 7, B)], 1)
+    x = rng.random((B, 3), dtype=np.float32)
+    y = (rng.random(B) < 0.5).astype(np.float32)
+    T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+    out = []
+    for m, uu in ((small, T(u)), (big, T(u) * MUL + 11)):
+        m.train()
+        z = m(uu, T(i), T(c), T(x))
+        loss = dcnr.BCEWithLogitsLoss()(z, T(y))
+        loss.backward()
+        out.append((z.detach(), {k: p.grad.detach().clone() for k, p in m.named_parameters()}))
+    torch.cuda.synchronize()
+    (zs, gs), (zb, gb) = out
+    assert torch.equal(zs, zb)
+    for k, g in gs.items():
+        if k == "user_embedding.weight":
+            assert torch.equal(gb[k][rows], g), k
+            mask = torch.ones(NB, dtype=torch.bool, device=dev)
+            mask[rows] = False
+            assert gb[k][mask].abs().max().item() == 0.0
+        else:
+            assert torch.equal(gb[k], g), k

@@ -15,6 +15,10 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
   fprintf(stderr, "\n");
 }
+dcnr_status set_max_dyn_lds(const void* k, size_t bytes) {
+  return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess
+             ? DCNR_OK : DCNR_HIP_ERROR;
+}
 }  // namespace dcnr
 
 int main() {

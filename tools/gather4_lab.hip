@@ -20,6 +20,10 @@ void set_error(const char* fmt, ...) {
   va_end(ap);
   fprintf(stderr, "\n");
 }
+dcnr_status set_max_dyn_lds(const void* k, size_t bytes) {
+  return hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) == hipSuccess
+             ? DCNR_OK : DCNR_HIP_ERROR;
+}
 }  // namespace dcnr
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
