@@ -536,6 +536,22 @@ def main():
     el_prof, prof, _ = timed(True)
     trainer.check_indices()
     final_loss = float(loss.item())
+    # N > 1: the same K steps with the other table exchange on the same
+    # trainer (both are ZeRO-1: the moments are sharded the same way), so the
+    # line reports both (DESIGN.md section 6 has the per-rank byte model)
+    other_exchange = None
+    if world > 1 and trainer.shard:
+        keep = trainer.exchange
+        trainer.exchange = "sparse" if keep == "dense" else "dense"
+        try:
+            el_o, _, _ = timed(False)
+            other_exchange = {"exchange": trainer.exchange, "ms_per_step": el_o / args.steps * 1e3,
+                              "value": world * B * args.steps / el_o}
+            if trainer.exchange == "sparse" and trainer.last_exchange:
+                other_exchange["last_step"] = trainer.last_exchange
+        except ValueError as e:   # layout not shard-aligned
+            other_exchange = {"exchange": trainer.exchange, "error": str(e)}
+        trainer.exchange = keep
 
     # scored pairs/s: eval-mode forward (running-stat BN, no dropout) per GPU
     model.eval()
@@ -651,11 +667,15 @@ def main():
                        "tables": "1M x 32 users, 100k x 32 hotels, 12 x 1000 x 32 cat, 8 dense",
                        "deep": "3 cross + 4 x 512 residual", "parallelism": f"dp{world}",
                        "exchange": "none" if world == 1 else (
-                           "sparse user rows + all-reduce" if args.exchange == "sparse"
+                           "dense params: all-reduce started in the backward (overlapped); "
+                           "user/item tables: touched rows all_to_all to the shard owners + "
+                           "sharded AdamW + all-gather; categorical tables: all-reduce"
+                           if args.exchange == "sparse"
                            else "dense params: all-reduce started in the backward (overlapped); "
                                 "tables: reduce-scatter + sharded AdamW + all-gather")},
             "scored_pairs_per_sec": pairs_per_s,
             "scored_pairs_roofline": eval_roof,
+            "other_exchange": other_exchange,
             "final_loss": final_loss,
             "roofline": roof,
             "roofline_by_class": table,

@@ -1298,6 +1298,45 @@ dcnr_status dcnr_mmr_rerank(const float* table, const float* inv_norms, int32_t 
 
 size_t dcnr_bce_workspace_size(void) { return bce_ws_bytes() + 256; }
 
+dcnr_status dcnr_emb_touched_rows(const dcnr_model_desc* desc, const void* ws, size_t ws_bytes,
+                                  int64_t B, int32_t n_tables, const int32_t* tables,
+                                  const int64_t* elem_off, int64_t shard_elems, int32_t world,
+                                  int64_t* out_offsets, int64_t* table_counts,
+                                  int64_t* owner_counts, dcnr_stream_t stream) {
+  Dims d;
+  TRY(make_dims(desc, &d));
+  if (!ws || B < 0 || n_tables < 1 || n_tables > 2 + d.K || !tables || !elem_off ||
+      !out_offsets || !table_counts || !owner_counts) {
+    set_error("dcnr_emb_touched_rows: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  Layout L = make_layout(d, B, DCNR_TRAIN, (void*)ws, keep_of(desc));
+  if (ws_bytes < L.total) {
+    set_error("workspace too small: %zu < %zu", ws_bytes, L.total);
+    return DCNR_WORKSPACE_TOO_SMALL;
+  }
+  TouchedArgs a;
+  memset(&a, 0, sizeof(a));
+  a.n = n_tables;
+  a.shard = shard_elems;
+  a.world = world;
+  for (int i = 0; i < n_tables; ++i) {
+    const int t = tables[i];
+    if (t < 0 || t >= 2 + d.K) {
+      set_error("dcnr_emb_touched_rows: table %d out of range", t);
+      return DCNR_BAD_ARG;
+    }
+    uint32_t base = 0;
+    for (int u = 0; u < t; ++u) base += (uint32_t)d.rows[u];
+    a.tab[i] = t;
+    a.base[i] = base;
+    a.width[i] = d.widths[t];
+    a.elem_off[i] = elem_off[i];
+  }
+  return emb_touched_rows(a, L.emb, B, out_offsets, table_counts, owner_counts,
+                          (hipStream_t)stream);
+}
+
 dcnr_status dcnr_bce_with_logits(const float* logits, const float* labels, int64_t B, float* loss,
                                  float* dlogits, float grad_scale, void* ws, size_t ws_bytes,
                                  dcnr_stream_t stream) {

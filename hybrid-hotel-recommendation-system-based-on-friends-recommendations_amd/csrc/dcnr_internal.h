@@ -443,6 +443,18 @@ struct EmbSortBufs {
 size_t emb_sort_tmp_bytes(const int64_t* rows, const int* width, int n_tab, int64_t B);
 dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* item,
                      const int64_t* cat, int64_t B, const EmbSortBufs& sb, hipStream_t s);
+// distinct touched rows of tables `tabs` from the sorted keys (dcnr_emb_touched_rows)
+struct TouchedArgs {
+  int n;                         // tables asked for
+  int tab[MAX_TABLES];           // their indices
+  uint32_t base[MAX_TABLES];     // first sort key of each (sum of earlier tables' rows)
+  int width[MAX_TABLES];
+  int64_t elem_off[MAX_TABLES];
+  int64_t shard;                 // owner = offset / shard
+  int world;
+};
+dcnr_status emb_touched_rows(const TouchedArgs& a, const EmbSortBufs& sb, int64_t B, int64_t* out,
+                             int64_t* table_counts, int64_t* owner_counts, hipStream_t s);
 // grad row r of table t = sum over its samples of dx0_deep[b][off_t:off_t+w_t]
 // + sum_k (sum over its samples of coef[b][k]) V[k][off_t:off_t+w_t]
 dcnr_status emb_segment_sum(const EmbBwdDesc& e, const EmbSortBufs& sb, int64_t B,

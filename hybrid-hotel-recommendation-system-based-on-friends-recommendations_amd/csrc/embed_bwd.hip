@@ -923,6 +923,94 @@ dcnr_status emb_sort(const EmbBwdDesc& e, const int64_t* user, const int64_t* it
 
 namespace {
 
+// ------------------------------------------------------- touched rows
+// One block per asked table walks its B sorted keys in chunks of TR_T * TR_U
+// positions: a position is a run head when its key differs from the previous
+// one; heads are compacted in order by a block scan (ascending rows, as the
+// sort left them) and counted per owner in LDS.  ~2 x 512 KB per table: a
+// latency-bound single-CU stream, off the backward's critical path.
+constexpr int TR_T = 1024, TR_U = 4, TR_MAXW = 64;
+
+__global__ __launch_bounds__(TR_T) void emb_touched_kernel(TouchedArgs a, const uint32_t* keys,
+                                                           int64_t B, int64_t* out,
+                                                           int64_t* table_counts,
+                                                           int64_t* owner_counts) {
+  __shared__ uint32_t wsum[TR_T / WAVE];
+  __shared__ int own[TR_MAXW];
+  const int i = blockIdx.x, t = a.tab[i], tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int r = tid; r < TR_MAXW; r += TR_T) own[r] = 0;
+  __syncthreads();
+  const uint32_t* k = keys + (int64_t)t * B;
+  int64_t* o = out + (int64_t)i * B;
+  const uint32_t base = a.base[i];
+  const int64_t eoff = a.elem_off[i], wd = a.width[i];
+  int64_t total = 0;
+  for (int64_t c0 = 0; c0 < B; c0 += (int64_t)TR_T * TR_U) {
+    uint32_t kv[TR_U];
+    bool head[TR_U];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int u = 0; u < TR_U; ++u) {   // thread-contiguous positions: in-order compaction
+      const int64_t p = c0 + (int64_t)tid * TR_U + u;
+      kv[u] = p < B ? k[p] : 0u;
+      head[u] = p < B && (p == 0 || k[p - 1] != kv[u]);
+      cnt += head[u];
+    }
+    // block exclusive scan of the per-thread head counts
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int d = 1; d < WAVE; d <<= 1) {
+      const uint32_t v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    if (lane == WAVE - 1) wsum[w] = incl;
+    __syncthreads();
+    uint32_t wpre = 0, all = 0;
+    for (int j = 0; j < TR_T / WAVE; ++j) {
+      const uint32_t v = wsum[j];
+      wpre += j < w ? v : 0u;
+      all += v;
+    }
+    uint32_t pos = wpre + incl - cnt;
+#pragma unroll
+    for (int u = 0; u < TR_U; ++u)
+      if (head[u]) {
+        const int64_t off = eoff + (int64_t)(kv[u] - base) * wd;
+        o[total + pos++] = off;
+        const int64_t r = off / a.shard;
+        if (r < a.world) atomicAdd(&own[r], 1);
+      }
+    total += all;
+    __syncthreads();   // wsum reused
+  }
+  __syncthreads();
+  if (tid == 0) table_counts[i] = total;
+  for (int r = tid; r < a.world; r += TR_T)
+    if (own[r]) atomicAdd((unsigned long long*)&owner_counts[r], (unsigned long long)own[r]);
+}
+
+}  // namespace
+
+dcnr_status emb_touched_rows(const TouchedArgs& a, const EmbSortBufs& sb, int64_t B, int64_t* out,
+                             int64_t* table_counts, int64_t* owner_counts, hipStream_t s) {
+  if (a.n < 1 || a.world < 1 || a.world > TR_MAXW || a.shard < 1) {
+    set_error("emb_touched_rows: %d tables, world %d (1..%d), shard %lld", a.n, a.world, TR_MAXW,
+              (long long)a.shard);
+    return DCNR_BAD_ARG;
+  }
+  DCNR_HIP(hipMemsetAsync(owner_counts, 0, (size_t)a.world * 8, s));
+  if (B <= 0) {
+    DCNR_HIP(hipMemsetAsync(table_counts, 0, (size_t)a.n * 8, s));
+    return DCNR_OK;
+  }
+  hipLaunchKernelGGL(emb_touched_kernel, dim3((unsigned)a.n), dim3(TR_T), 0, s, a, sb.keys_s, B, out,
+                     table_counts, owner_counts);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+namespace {
+
 template <int VEC, int NV>
 void launch_sums(const EmbTabs& et, int nt, int64_t B, const EmbSortBufs& sb, const float* dx0,
                  int ld, const float* coef, int hps, int accumulate, hipStream_t s) {

@@ -111,6 +111,13 @@ class IndexErrorWatch:
         self.next = 0
         self.lock = threading.Lock()
 
+    # copies (deepcopy / pickle of the model) start with an empty watch
+    def __getstate__(self):
+        return {}
+
+    def __setstate__(self, state):
+        self.__init__()
+
     def push(self, word: torch.Tensor):
         with self.lock:
             if self.ring is None:
@@ -224,7 +231,13 @@ class DCN_RecSys(nn.Module):
         st.pop('_ptr_cache', None)
         st['_index_watch'] = IndexErrorWatch()
         st.pop('_gc_flag', None)
+        st.pop('_cat_rows', None)   # ctypes array: rebuilt by __setstate__
         return st
+
+    def __setstate__(self, st):
+        super().__setstate__(st)
+        cd = self._dims['cat_dims']
+        self.__dict__['_cat_rows'] = (ctypes.c_int64 * max(1, len(cd)))(*[int(n) for n in cd])
 
     def check_index_errors(self):
         """Wait for every deferred id check of this model; raises IndexError

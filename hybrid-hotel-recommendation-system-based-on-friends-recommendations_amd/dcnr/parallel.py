@@ -18,9 +18,15 @@ plain data-parallel split of each batch across ranks:
 Default (sync_bn=False) is local BN: every rank normalises with its own
 batch, like torch DDP without SyncBatchNorm.
 
-``sparse_rows_allreduce`` is the owner-bucketed sparse exchange of one
-embedding table's gradient (SURVEY.md 8e option B), used by
-``FusedTrainer(exchange="sparse")`` for the user table.
+``sparse_reduce_scatter`` is the owner-bucketed sparse exchange of the big
+embedding tables' gradients (SURVEY.md 8e option B), used by
+``FusedTrainer(exchange="sparse")``: the rows the rank's batch touched
+(``touched_rows``: read from the backward's own stable id sort by
+``dcnr_emb_touched_rows``, no torch.unique) go to the rank that owns their
+ZeRO-1 shard of the flat parameter buffer (one all_to_all of offsets and
+rows), and each owner sums what it received in source-rank order into its
+gradient shard.  ``sparse_rows_allreduce`` is the earlier host-sized
+variant for one table (kept for the CPU tests of the protocol).
 """
 from __future__ import annotations
 
@@ -148,3 +154,86 @@ def sparse_rows_allreduce(grad: torch.Tensor, local_ids: torch.Tensor, group=Non
     grad.zero_()
     grad.index_copy_(0, aid[keep], aval[keep])
     return {"rows_sent": int(uniq.numel()), "rows_owned": int(mine.numel()), "rows_total": sum(cnts)}
+
+
+def touched_rows(model, ws: torch.Tensor, B: int, tables, elem_off, shard_elems: int, world: int):
+    """Distinct rows of ``tables`` the batch of the last train-mode forward on
+    ``ws`` touched, as flat-buffer element offsets (dcnr_emb_touched_rows):
+    returns (offsets [len(tables), B] int64, table_counts [len(tables)],
+    owner_counts [world]) on the device; offsets[i, :table_counts[i]] are
+    ascending."""
+    lib = _lib.load()
+    dev = ws.device
+    n = len(tables)
+    offs = torch.empty((n, max(B, 1)), dtype=torch.int64, device=dev)
+    tcnt = torch.empty(n, dtype=torch.int64, device=dev)
+    ocnt = torch.empty(world, dtype=torch.int64, device=dev)
+    tabs = (ctypes.c_int32 * n)(*[int(t) for t in tables])
+    eoff = (ctypes.c_int64 * n)(*[int(o) for o in elem_off])
+    desc = model.desc()
+    _lib.check(lib.dcnr_emb_touched_rows(ctypes.byref(desc), ws.data_ptr(), ws.numel(), int(B), n,
+                                         ctypes.cast(tabs, ctypes.c_void_p),
+                                         ctypes.cast(eoff, ctypes.c_void_p), int(shard_elems),
+                                         int(world), offs.data_ptr(), tcnt.data_ptr(),
+                                         ocnt.data_ptr(), _lib.stream_ptr(dev)),
+               "dcnr_emb_touched_rows")
+    return offs, tcnt, ocnt
+
+
+def sparse_reduce_scatter(gflat: torch.Tensor, gshard: torch.Tensor, width: int,
+                          offsets: torch.Tensor, table_counts: torch.Tensor,
+                          owner_counts: torch.Tensor, dense_lo: int, dense_hi: int,
+                          group=None) -> dict:
+    """The reduce-scatter of the embedding segment of ``gflat`` into this
+    rank's shard ``gshard`` (ZeRO-1: rank r owns elements [r*Es, (r+1)*Es)),
+    moving only touched rows:
+
+      * ``offsets`` [n_tables, B]: per sparse table, this rank's touched rows
+        as ascending flat element offsets (row i of table t at
+        offsets[t, i] for i < table_counts[t]; each row ``width`` elements,
+        never straddling a shard; the tables in flat order);
+        ``owner_counts`` [world] how many go to each rank (device tensors,
+        as ``touched_rows`` returns them);
+      * one all_to_all of the counts, ONE host read of the send / receive /
+        table counts, one all_to_all of the offsets and of the rows;
+      * the owner zeroes its shard and adds what it received in source-rank
+        order (rows distinct per source: the sum is 0 + g_0 + g_1 + ..., the
+        same bits for every run);
+      * elements [dense_lo, dense_hi) (the small categorical tables) go
+        through an all-reduce and their part of the shard is copied in.
+
+    Rows no rank touched have an exactly-zero gradient (the backward
+    zero-fills them), so the shard equals the dense reduce-scatter's sum."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    Es = gshard.numel()
+    dev = gflat.device
+    recv_counts = torch.empty_like(owner_counts)
+    dist.all_to_all_single(recv_counts, owner_counts, group=group)
+    counts = torch.cat([owner_counts, recv_counts, table_counts]).cpu().tolist()   # one host sync
+    sc, rc, tc = counts[:world], counts[world:2 * world], counts[2 * world:]
+    send_off = torch.cat([offsets[t, :tc[t]] for t in range(len(tc))])
+    col = torch.arange(width, device=dev, dtype=torch.int64)
+    rows = gflat[send_off[:, None] + col[None, :]] if send_off.numel() else \
+        torch.empty((0, width), dtype=gflat.dtype, device=dev)
+    r_off = torch.empty(sum(rc), dtype=torch.int64, device=dev)
+    r_rows = torch.empty((sum(rc), width), dtype=gflat.dtype, device=dev)
+    dist.all_to_all_single(r_off, send_off, rc, sc, group=group)
+    dist.all_to_all_single(r_rows, rows, rc, sc, group=group)
+    gshard.zero_()
+    gv = gshard.view(-1, width)
+    lo = rank * Es
+    pos = 0
+    for r in range(world):                    # fixed source order
+        if rc[r]:
+            gv.index_add_(0, torch.div(r_off[pos:pos + rc[r]] - lo, width, rounding_mode="floor"),
+                          r_rows[pos:pos + rc[r]])
+        pos += rc[r]
+    if dense_hi > dense_lo:                   # the small tables: dense all-reduce
+        dense = gflat[dense_lo:dense_hi].clone()
+        dist.all_reduce(dense, op=dist.ReduceOp.SUM, group=group)
+        a, b = max(dense_lo, lo), min(dense_hi, lo + Es)
+        if b > a:
+            gshard[a - lo:b - lo].copy_(dense[a - dense_lo:b - dense_lo])
+    return {"rows_sent": sum(sc), "rows_received": sum(rc),
+            "bytes_sent": sum(sc) * (8 + 4 * width) + 4 * max(0, dense_hi - dense_lo)}

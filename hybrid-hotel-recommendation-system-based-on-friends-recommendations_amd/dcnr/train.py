@@ -18,12 +18,14 @@ optimizer.step) as native calls over flat parameter/gradient/moment buffers:
              1/world of the optimizer's HBM traffic and moment memory
              (ZeRO-1 style); the dense segment is updated whole on every rank
            shard_optimizer=False: all-reduce, every rank updates everything
-           exchange="sparse": the user table's gradient goes through the
-             owner-bucketed sparse exchange (dcnr.parallel.
-             sparse_rows_allreduce: only the rows the ranks' batches
-             touched; it synchronises the host for its message sizes), the
-             other tables through an all-reduce, every rank updates
-             everything
+           exchange="sparse" (ZeRO-1 like the default): the user and item
+             tables' gradient rows the rank's batch touched -- read from the
+             backward's own id sort (dcnr_emb_touched_rows) -- go to the
+             owners of their parameter shard (all_to_all), each owner sums
+             them in rank order into its shard (dcnr.parallel.
+             sparse_reduce_scatter; one host read of the message sizes), the
+             small categorical tables go through an all-reduce; then AdamW
+             on the shard and the all-gather of the parameters, as above
 
 Numerically the same update as ``torch.optim.AdamW``/``Adam`` on the
 reference's dense gradients (every embedding row's moments decay every step).
@@ -56,12 +58,26 @@ class FusedTrainer:
             raise ValueError("exchange must be 'dense' or 'sparse'")
         self.exchange = exchange
         if exchange == "sparse":
-            shard_optimizer = False
+            shard_optimizer = True
         self.shard = (self.world > 1) if shard_optimizer is None else bool(shard_optimizer)
         self.flat, self.gflat = model.flatten_(pad_to=64 * self.world)
         self.E = model.flat_emb_end                      # embedding segment [0, E)
         N = self.flat.numel()
         self.Es = self.E // self.world if self.shard else self.E   # this rank's embedding moments
+        # the sparse exchange's layout: the user and item tables at flat
+        # offsets 0 and nu (rows of emb_dim elements), the categorical tables
+        # after them (dense all-reduce); rows must not straddle a shard
+        d = model._dims['emb_dim']
+        pad = lambda x: ((x + 63) // 64) * 64   # noqa: E731 (flatten_'s per-tensor padding)
+        nu = pad(model._dims['n_users'] * d)
+        self._sparse_layout = dict(width=d, tables=(0, 1), elem_off=(0, nu),
+                                   dense_lo=nu + pad(model._dims['n_items'] * d), dense_hi=self.E)
+        self._sparse_ok = self.shard and not (self.Es % d or nu % d)
+        if exchange == "sparse" and not self._sparse_ok:
+            raise ValueError("exchange='sparse' needs table rows aligned to the optimizer "
+                             f"shards (emb_dim {d}, shard {self.Es} elements)")
+        self._B = 0
+        self.last_exchange = None
         self.m = torch.zeros(self.Es + N - self.E, dtype=torch.float32, device=self.flat.device)
         self.v = torch.zeros_like(self.m)
         self.gshard = torch.empty(self.Es, dtype=torch.float32,
@@ -92,6 +108,7 @@ class FusedTrainer:
         seed = dropout_seed(user.device)
         model._index_watch.poll()
         logits, self._ws = run_forward(model, True, seed, user, item, cat, num, self._ws)
+        self._B = user.shape[0]
         # grad_scale 1/world: the SUM all-reduce then yields the global mean gradient
         loss, dz = bce_with_logits(logits, y, True, 1.0 / self.world)
         self._dense_work = None
@@ -106,7 +123,7 @@ class FusedTrainer:
             raise
         # the all-reduce this step's backward started (None: start it now)
         dense, self._dense_work = self._dense_work, None
-        self._exchange_and_update(None, user, dense)
+        self._exchange_and_update(None, None, dense)
         return (loss, logits) if return_logits else loss
 
     def _on_grads_ready(self, ctx, group, stream):
@@ -126,14 +143,24 @@ class FusedTrainer:
         (the checks are otherwise reported by a later step)."""
         self.model.check_index_errors()
 
-    def exchange_and_update(self, adam=None, user_ids=None):
+    def exchange_and_update(self, adam=None, touched=None):
         """The data-parallel gradient exchange and the optimizer step on the
         flat buffers.  ``adam(p, g, m, v, step)`` defaults to dcnr_adam_step
         (the CPU tests pass a host restatement to check the exchange).
-        ``user_ids``: this rank's batch user ids (the sparse exchange)."""
-        self._exchange_and_update(adam, user_ids, None)
+        ``touched``: for the sparse exchange, (offsets, table_counts,
+        owner_counts) as dcnr.parallel.touched_rows returns them (default:
+        read from the last step's backward)."""
+        self._exchange_and_update(adam, touched, None)
 
-    def _exchange_and_update(self, adam, user_ids, dense):
+    def touched_rows(self):
+        """The rows the last step's batch touched in the sparse-exchanged
+        tables (dcnr_emb_touched_rows over the step's workspace)."""
+        from .parallel import touched_rows
+        lay = self._sparse_layout
+        return touched_rows(self.model, self._ws, self._B, lay["tables"], lay["elem_off"], self.Es,
+                            self.world)
+
+    def _exchange_and_update(self, adam, touched, dense):
         adam = adam or self._adam
         self.step_count += 1
         E, Es, world = self.E, self.Es, self.world
@@ -143,17 +170,19 @@ class FusedTrainer:
         if dense is None:   # not started by this step's backward: start it now
             dense = dist.all_reduce(self.gflat[E:], op=dist.ReduceOp.SUM, group=self.pg,
                                     async_op=True)
-        if self.exchange == "sparse":
-            from .parallel import sparse_rows_allreduce
-            uw = self.model.user_embedding.weight
-            nu = ((uw.numel() + 63) // 64) * 64     # its padded segment at offset 0
-            assert uw.data_ptr() == self.flat.data_ptr()
-            self.last_exchange = sparse_rows_allreduce(uw.grad, user_ids, self.pg)
-            dist.all_reduce(self.gflat[nu:E], op=dist.ReduceOp.SUM, group=self.pg)
-            adam(self.flat[:E], self.gflat[:E], self.m[:E], self.v[:E], self.step_count)
-        elif self.shard:
-            dist.reduce_scatter_tensor(self.gshard, self.gflat[:E], op=dist.ReduceOp.SUM,
-                                       group=self.pg)
+        if self.shard:
+            if self.exchange == "sparse":
+                if not self._sparse_ok:
+                    raise ValueError("exchange='sparse': table rows not aligned to the shards")
+                from .parallel import sparse_reduce_scatter
+                lay = self._sparse_layout
+                offs, tcnt, ocnt = touched if touched is not None else self.touched_rows()
+                self.last_exchange = sparse_reduce_scatter(
+                    self.gflat, self.gshard, lay["width"], offs, tcnt, ocnt, lay["dense_lo"],
+                    lay["dense_hi"], self.pg)
+            else:
+                dist.reduce_scatter_tensor(self.gshard, self.gflat[:E], op=dist.ReduceOp.SUM,
+                                           group=self.pg)
             pshard = self.flat[self.rank * Es:(self.rank + 1) * Es]
             adam(pshard, self.gshard, self.m[:Es], self.v[:Es], self.step_count)
             dist.all_gather_into_tensor(self.flat[:E], pshard, group=self.pg)

@@ -206,6 +206,24 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
                           const float* dlogits, uint64_t dropout_seed, int accumulate, void* ws, size_t ws_bytes,
                           dcnr_stream_t stream);
 
+/* The embedding rows the batch of the last train-mode dcnr_forward on `ws`
+ * touched, read from that forward's stable id sort (the sorted (id, sample)
+ * pairs the backward's fixed-order sums walk; still in `ws` after
+ * dcnr_backward): the data-parallel sparse gradient exchange
+ * (SURVEY.md 8(e) option B; the gradient rows come from train.py:156-158
+ * under train.py:225) buckets them by owner without a torch.unique.
+ * For each of n_tables tables (indices into the model's tables: 0 = user,
+ * 1 = item, 2.. = categorical) writes the flat element offsets
+ * elem_off[i] + row * width of its distinct rows, ascending, to
+ * out_offsets[i*B ..] and their number to table_counts[i]; owner_counts[r]
+ * (r < world) counts the offsets in [r*shard_elems, (r+1)*shard_elems).
+ * Stream-ordered; outputs are device memory. */
+dcnr_status dcnr_emb_touched_rows(const dcnr_model_desc* desc, const void* ws, size_t ws_bytes,
+                                  int64_t B, int32_t n_tables, const int32_t* tables,
+                                  const int64_t* elem_off, int64_t shard_elems, int32_t world,
+                                  int64_t* out_offsets, int64_t* table_counts,
+                                  int64_t* owner_counts, dcnr_stream_t stream);
+
 size_t dcnr_bce_workspace_size(void);
 
 /* BCEWithLogitsLoss (mean): loss[0] = mean(max(z,0) - z*y + log1p(exp(-|z|)));

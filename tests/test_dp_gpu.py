@@ -229,3 +229,52 @@ def test_dp_bf16_hook_ordering(dev, shard):
     side-stream weight gradients, the grad-ready hook, sharded or all-reduce
     exchange (train.py:219-226)."""
     mp.spawn(_worker_hook, args=(2, _free_port(), shard), nprocs=2, join=True)
+
+
+def _worker_sparse(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import dcnr
+        dev = torch.device("cuda:0")
+        torch.cuda.set_device(dev)
+        lo, hi = rank * B // world, (rank + 1) * B // world
+        flats = []
+        for exchange in ("dense", "sparse"):
+            m = _model(dev, "bf16", dropout=0.6)
+            tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, sync_bn=True, exchange=exchange)
+            gen = torch.cuda.default_generators[0]
+            gen.set_offset(0)                      # the same dropout seeds in both runs
+            for step in range(2):
+                batch = [t[lo:hi] for t in _batch(dev)]
+                tr.step(*batch)
+                if exchange == "sparse" and step == 0:
+                    # the touched rows of this rank's batch, from the backward's sort
+                    offs, tcnt, own = tr.touched_rows()
+                    lay = tr._sparse_layout
+                    d = lay["width"]
+                    want = [torch.unique(batch[0].long()) * d,
+                            torch.unique(batch[1].long()) * d + lay["elem_off"][1]]
+                    tc = tcnt.cpu().tolist()
+                    for t in range(2):
+                        assert torch.equal(offs[t, :tc[t]], want[t]), t
+                    allw = torch.cat(want)
+                    assert torch.equal(own.cpu(), torch.bincount((allw // tr.Es).cpu(),
+                                                                 minlength=world))
+            torch.cuda.synchronize()
+            flats.append(tr.flat.clone())
+            assert tr.exchange != "sparse" or tr.last_exchange["rows_sent"] > 0
+        # world 2: the owner's rank-order sum (0 + g_0) + g_1 is the dense
+        # reduce-scatter's g_0 + g_1: every parameter bit-identical
+        assert torch.equal(flats[0], flats[1])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_sparse_exchange_equals_dense(dev):
+    """exchange="sparse" (touched rows from the backward's sort ->
+    all_to_all to the shard owners -> rank-order sums; categorical tables
+    all-reduced) gives exactly the dense reduce-scatter step: bf16, dropout
+    0.6, SyncBN, two steps, two ranks on one GPU (train.py:156-158, 225)."""
+    mp.spawn(_worker_sparse, args=(2, _free_port()), nprocs=2, join=True)

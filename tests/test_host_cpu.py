@@ -151,3 +151,25 @@ def test_reference_artifacts_load_cpu():
         sd2 = torch.load(os.path.join(t, "final_dcn_model.pth"), weights_only=True)
         assert all(torch.equal(sd2[k], v) for k, v in sd.items())
         assert np.array_equal(np.load(os.path.join(t, "item_embeddings.npy")), emb)
+
+
+def test_model_copies_and_pickles():
+    """deepcopy / pickle of the module (the reference's torch.save-of-model
+    and copy idioms): the copy has its own (empty) id-check watch and equal
+    parameters."""
+    import copy
+    import pickle
+    m = our_model(gc.CFG1)
+    for c in (copy.deepcopy(m), pickle.loads(pickle.dumps(m))):
+        assert c._index_watch is not m._index_watch and c._index_watch.pending == []
+        for (k, a), (_, b) in zip(m.state_dict().items(), c.state_dict().items()):
+            assert torch.equal(a, b), k
+
+
+def test_workspace_query_huge_table():
+    """A table of more than 2^24 rows sizes its workspace for the radix-sort
+    path (embed_bwd.hip) instead of failing."""
+    import dcnr
+    cfg = dict(gc.CFG1, n_users=(1 << 24) + 3)
+    m = our_model(cfg, precision="bf16")
+    assert m.workspace_bytes(4096, 1) > m.workspace_bytes(4096, 0) > 0

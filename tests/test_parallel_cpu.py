@@ -264,32 +264,53 @@ def _sparse_worker(rank, world, port):
         assert torch.equal(mine, want)
         assert info["rows_sent"] == torch.unique(ids[rank]).numel()
         assert info["rows_total"] == torch.unique(torch.cat(ids)).numel()
-        # through FusedTrainer
+        # through FusedTrainer(exchange="sparse"): the user and item tables'
+        # touched rows go to the owners of their ZeRO-1 shard
+        # (sparse_reduce_scatter), the categorical tables through an
+        # all-reduce; AdamW on the shard, all-gather of the parameters
+        n_items = 40
         torch.manual_seed(0)
-        m = dcnr.DCN_RecSys(n_users, 40, {"a": 10, "b": 3}, 3,
+        m = dcnr.DCN_RecSys(n_users, n_items, {"a": 10, "b": 3}, 3,
                             dict(emb_dim=d, hidden_dim=16, n_cross_layers=1, n_res_blocks=1,
                                  dropout=0.0))
         tr = dcnr.FusedTrainer(m, lr=1e-2, weight_decay=1e-2, exchange="sparse")
-        assert not tr.shard and tr.m.numel() == tr.flat.numel()
+        assert tr.shard and tr.m.numel() == tr.E // world + tr.flat.numel() - tr.E
+        lay = tr._sparse_layout
+        nu = lay["elem_off"][1]
+        iids = [torch.randint(0, n_items, (40,), generator=torch.Generator().manual_seed(80 + r))
+                for r in range(world)]
         ref_p, ref_m, ref_v = tr.flat.clone(), torch.zeros_like(tr.flat), torch.zeros_like(tr.flat)
-        nu = ((n_users * d + 63) // 64) * 64
         for step in range(1, 3):
-            full = []
+            full, touched = [], []
             for r in range(world):
                 gg = torch.randn(tr.flat.numel(), generator=torch.Generator().manual_seed(9 * step + r))
-                gu = torch.zeros(n_users, d)
-                u = torch.unique(ids[r])
-                gu[u] = gg[:n_users * d].view(n_users, d)[u]
-                gg[:nu] = 0
-                gg[:n_users * d] = gu.reshape(-1)
+                gg[:lay["dense_lo"]] = 0          # the sparse tables: touched rows only
+                offs = torch.zeros((2, 40), dtype=torch.int64)
+                tcnt = torch.zeros(2, dtype=torch.int64)
+                for t, (ids_t, base) in enumerate(((ids[r], 0), (iids[r], nu))):
+                    u = torch.unique(ids_t) * d + base     # what dcnr_emb_touched_rows returns
+                    for o in u.tolist():
+                        gg[o:o + d] = torch.randn(d, generator=torch.Generator().manual_seed(o + r))
+                    offs[t, :u.numel()] = u
+                    tcnt[t] = u.numel()
+                own = torch.bincount(torch.cat([offs[t, :tcnt[t]] for t in range(2)]) // tr.Es,
+                                     minlength=world)
                 full.append(gg)
+                touched.append((offs, tcnt, own))
             tr.gflat.copy_(full[rank])
-            tr.exchange_and_update(adam=_host_adam, user_ids=ids[rank])
-            _host_adam(ref_p, sum(full), ref_m, ref_v, step)
+            tr.exchange_and_update(adam=_host_adam, touched=touched[rank])
+            want = sum(full)
+            lo, hi = rank * tr.Es, (rank + 1) * tr.Es
+            sp = min(hi, lay["dense_lo"])
+            if sp > lo:   # the sparse tables' part of the shard: the rank-order sum, bit for bit
+                assert torch.equal(tr.gshard[:sp - lo], want[lo:sp])
+            np.testing.assert_allclose(tr.gshard.numpy(), want[lo:hi].numpy(), rtol=1e-6, atol=1e-7)
+            _host_adam(ref_p, want, ref_m, ref_v, step)
             np.testing.assert_allclose(tr.flat.numpy(), ref_p.numpy(), rtol=2e-6, atol=1e-7)
             allp = [torch.empty_like(tr.flat) for _ in range(world)]
             dist.all_gather(allp, tr.flat)
             assert all(torch.equal(allp[0], a) for a in allp[1:])
+            assert tr.last_exchange["rows_sent"] == int(sum(c for c in touched[rank][1]))
     finally:
         dist.destroy_process_group()
 
