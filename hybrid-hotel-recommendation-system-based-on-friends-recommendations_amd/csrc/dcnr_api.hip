@@ -618,12 +618,12 @@ dcnr_status wgrad_bf16(const void* dY, int64_t ldy, int N, const void* X, int64_
   DwArgs a;
   memset(&a, 0, sizeof(a));
   a.A = (const bf16*)dY; a.lda = ldy; a.B = (const bf16*)X; a.ldb = ldx;
-  a.C = slab; a.ldc = Kc; a.slab_stride = (int64_t)N * Kc;
+  a.C = slab; a.ldc = N; a.slab_stride = (int64_t)N * Kc;   // transposed slab [Kc][N]
   a.Btot = B; a.k_per_split = rup(cdiv(B, S), 64);
   a.N = N; a.K = Kc; a.splits = S;
   TRYB(DCNR_K_GEMM_DW, 2.0 * B * (N + Kc) + 4.0 * Nr * Kr * (accumulate ? 2 : 1), gemm_dw(a, s));
   TRYB(DCNR_K_REDUCE, 4.0 * S * N * Kc + 4.0 * Nr * Kr * (accumulate ? 2 : 1),
-       splitk_reduce(slab, S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s));
+       splitk_reduce_t(slab, S, (int64_t)N * Kc, N, Nr, Kr, out, accumulate, s));
   return DCNR_OK;
 }
 
@@ -672,13 +672,13 @@ struct DwPipe {
     DwArgs a;
     memset(&a, 0, sizeof(a));
     a.A = (const bf16*)dY; a.lda = ldy; a.B = (const bf16*)X; a.ldb = ldx;
-    a.C = L.slab; a.ldc = Kc; a.slab_stride = (int64_t)N * Kc;
+    a.C = L.slab; a.ldc = N; a.slab_stride = (int64_t)N * Kc;   // transposed slab [Kc][N]
     a.Btot = B; a.k_per_split = rup(cdiv(B, S), 64);
     a.N = N; a.K = Kc; a.splits = S;
     TRYB(DCNR_K_GEMM_DW, 2.0 * B * (N + Kc) + 4.0 * Nr * Kr * (accumulate ? 2 : 1), gemm_dw(a, s));
     DCNR_HIP(hipEventRecord(dw_ev, s));
     TRYB(DCNR_K_REDUCE, 4.0 * S * N * Kc + 4.0 * Nr * Kr * (accumulate ? 2 : 1),
-         splitk_reduce(L.slab, S, (int64_t)N * Kc, Kc, Nr, Kr, out, accumulate, s));
+         splitk_reduce_t(L.slab, S, (int64_t)N * Kc, N, Nr, Kr, out, accumulate, s));
     return DCNR_OK;
   }
   dcnr_status join(hipStream_t main_s) {

@@ -513,6 +513,10 @@ dcnr_status sums_to_grad(const double* sums, int N, float* out, int accumulate, 
 // out[n][k] (+)= sum_s slab[s][n][k]  (n < N, k < K; slab row stride ld_slab)
 dcnr_status splitk_reduce(const float* slab, int splits, int64_t slab_stride, int ld_slab,
                           int N, int K, float* out, int accumulate, hipStream_t s);
+// the same over transposed slabs [splits][K][ld] (gemm_dw.hip's layout):
+// out[n][k] (+)= sum_z slab[z][k][n]
+dcnr_status splitk_reduce_t(const float* slab, int splits, int64_t slab_stride, int ld_slab, int N,
+                            int K, float* out, int accumulate, hipStream_t s);
 
 // head
 // last block + head fused: out = relu(BN2(t) + x); logits = out . wf[:Nr] + zc + bf

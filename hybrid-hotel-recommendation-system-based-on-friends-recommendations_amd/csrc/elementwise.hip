@@ -923,6 +923,76 @@ dcnr_status splitk_reduce(const float* slab, int splits, int64_t slab_stride, in
   return DCNR_OK;
 }
 
+namespace {
+// out[n][k] (+)= sum_z slab[z][k][n]: the weight-gradient GEMM's transposed
+// slabs (gemm_dw.hip stores 4 consecutive n per lane as one 16-B store).  A
+// block takes 64 k x 16 n: reads along n (4 lanes x 16 B per 64-B row
+// segment, 16 slab loads in flight per lane), sums in fixed z order (the same
+// bits as summing the untransposed slabs), transposes through LDS, writes
+// rows of out along k (16-B stores when out's rows allow).
+constexpr int RT_K = 64, RT_N = 16;
+__global__ __launch_bounds__(256) void splitk_reduce_t_kernel(const float* slab, int splits,
+                                                              int64_t stride, int ld, int N, int K,
+                                                              float* out, int accumulate, int vec_out) {
+  __shared__ float t[RT_K][RT_N + 1];
+  const int k0 = blockIdx.x * RT_K, n0 = blockIdx.y * RT_N;
+  {
+    const int kk = threadIdx.x >> 2, nq = threadIdx.x & 3;
+    const int k = k0 + kk, n = n0 + 4 * nq;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (k < K && n < N) {
+      const float* base = slab + (int64_t)k * ld + n;
+      int z = 0;
+      for (; z + 16 <= splits; z += 16) {
+        float4 v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const float4*>(base + (int64_t)(z + u) * stride);
+#pragma unroll
+        for (int u = 0; u < 16; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+      }
+      for (; z < splits; ++z) {
+        const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)z * stride);
+        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      }
+    }
+    t[kk][4 * nq] = s.x; t[kk][4 * nq + 1] = s.y; t[kk][4 * nq + 2] = s.z; t[kk][4 * nq + 3] = s.w;
+  }
+  __syncthreads();
+  const int nn = threadIdx.x >> 4, kq = threadIdx.x & 15;
+  const int n = n0 + nn, k = k0 + 4 * kq;
+  if (n >= N) return;
+  float v[4] = {t[4 * kq][nn], t[4 * kq + 1][nn], t[4 * kq + 2][nn], t[4 * kq + 3][nn]};
+  float* o = out + (int64_t)n * K + k;
+  if (vec_out && k + 3 < K) {
+    float4 r = make_float4(v[0], v[1], v[2], v[3]);
+    if (accumulate) {
+      const float4 a = *reinterpret_cast<const float4*>(o);
+      r.x += a.x; r.y += a.y; r.z += a.z; r.w += a.w;
+    }
+    *reinterpret_cast<float4*>(o) = r;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (k + j < K) o[j] = accumulate ? o[j] + v[j] : v[j];
+  }
+}
+}  // namespace
+
+dcnr_status splitk_reduce_t(const float* slab, int splits, int64_t slab_stride, int ld_slab, int N,
+                            int K, float* out, int accumulate, hipStream_t s) {
+  if ((int64_t)N * K <= 0) return DCNR_OK;
+  if (ld_slab % 4 || slab_stride % 4 || (uintptr_t)slab % 16) {
+    set_error("splitk_reduce_t: slab not 16-B aligned");
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  const int vec_out = K % 4 == 0 && (uintptr_t)out % 16 == 0;
+  hipLaunchKernelGGL(splitk_reduce_t_kernel, dim3((unsigned)cdiv(K, RT_K), (unsigned)cdiv(N, RT_N)),
+                     dim3(256), 0, s, slab, splits, slab_stride, ld_slab, N, K, out, accumulate,
+                     vec_out);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
 dcnr_status fill_zero(void* p, size_t bytes, hipStream_t s) {
   if (!bytes) return DCNR_OK;
   DCNR_HIP(hipMemsetAsync(p, 0, bytes, s));

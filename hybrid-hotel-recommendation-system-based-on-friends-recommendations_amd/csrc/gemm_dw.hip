@@ -20,7 +20,8 @@
 //    rows hit different banks (a 16-row read touches each bank twice: the floor);
 //  * out-of-range rows/columns are fetched at an out-of-range buffer offset
 //    and read as 0 (branch-free tails);
-//  * fp32 split partials go to a slab [S][N][ldc] (summed by splitk_reduce).
+//  * fp32 split partials go to a TRANSPOSED slab [S][K][ldc] (16-B stores of
+//    4 consecutive n; summed and transposed back by splitk_reduce_t).
 #include "dcnr_internal.h"
 
 // tools/dw_lab.hip rebuilds this file with DW_LAB_MODE bits (1: no MFMA,
@@ -138,22 +139,22 @@ __global__ __launch_bounds__(NTW, 1) void gemm_dw_kernel(DwArgs g) {
           acc[i][j][0] += (float)af[i][0] * (float)bf[j][1];
   }
 
-  // epilogue: acc[i][j][r] = dW[n0 + wn*128 + i*16 + (lane>>4)*4 + r][c0 + wk*64 + j*16 + (lane&15)]
+  // epilogue: acc[i][j][r] = dW[n0 + wn*128 + i*16 + (lane>>4)*4 + r][c0 + wk*64 + j*16 + (lane&15)],
+  // four consecutive n per lane: the slab is stored transposed ([k][n], row
+  // ldc) so each (i, j) is ONE 16-B store (32 per lane instead of 128 4-B
+  // stores: the store-issue tail of this kernel); splitk_reduce_t transposes back
   float* out = g.C + (int64_t)split * g.slab_stride;
-  const __amdgpu_buffer_rsrc_t cr = buf_rsrc(out, (int64_t)g.N * g.ldc * 4);
+  const __amdgpu_buffer_rsrc_t cr = buf_rsrc(out, (int64_t)g.K * g.ldc * 4);
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = c0 + wk * 64 + j * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4 + r;
-        const bool ok = n < g.N && k < g.K;
-        if (!(DW_LAB_MODE & 4) || acc[i][j][r] == 1234.5f)
-          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[i][j][r]), cr,
-                                                ok ? (n * g.ldc + k) * 4 : OOR, 0, 0);
-      }
+      const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4;   // N % 8 == 0: all 4 or none
+      const bool ok = n < g.N && k < g.K;
+      if (!(DW_LAB_MODE & 4) || acc[i][j][0] == 1234.5f)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), cr,
+                                               ok ? (k * g.ldc + n) * 4 : OOR, 0, 0);
     }
 }
 

@@ -26,7 +26,8 @@
 #include "dcnr_internal.h"
 
 #ifndef WS_LAB_MODE
-#define WS_LAB_MODE 0   // tools/ws_lab.hip: 1 no C stores, 2 no X DMAs, 4 no MFMAs, 8 no epilogue
+#define WS_LAB_MODE 0   // tools/ws_lab.hip: 1 no C stores, 2 no X DMAs, 4 no MFMAs, 8 no epilogue,
+                        // 16 no fragment reads in the K loop
 #endif
 #ifndef WS_PREFETCH_PIN
 #define WS_PREFETCH_PIN 1
@@ -41,6 +42,16 @@
 #endif
 #ifndef WS_PRIO
 #define WS_PRIO 0
+#endif
+// waves 4-7 run each tile's epilogue after the tile's barrier, at the head
+// of the next tile (MI355X_MICROARCH.md "Two waves per SIMD" item 9): the two
+// waves of a SIMD then alternate MFMA and epilogue phases
+// fragment prefetch distance of the MFMA loop, in K steps
+#ifndef WS_PFD
+#define WS_PFD 1
+#endif
+#ifndef WS_STAGGER
+#define WS_STAGGER 0
 #endif
 
 namespace dcnr {
@@ -76,9 +87,11 @@ template <int KTP, int TM, int NB = 2> struct WsCfg {
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
+typedef bf16 bf16x2v __attribute__((ext_vector_type(2)));
+// two floats -> packed bf16 (round to nearest even) in ONE v_cvt_pk_bf16_f32
+// (the scalar casts cost two conversions + a shift + an or)
 __device__ __forceinline__ uint32_t pack2(float a, float b) {
-  bf16 x = (bf16)a, y = (bf16)b;
-  return (uint32_t)__builtin_bit_cast(uint16_t, x) | ((uint32_t)__builtin_bit_cast(uint16_t, y) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2v{a, b}, bf16x2v));
 }
 __device__ __forceinline__ f2v unpack2(uint32_t w) {
   return f2v{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)};
@@ -213,84 +226,28 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   int coff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) coff[j] = ((4 * j + q) ^ l15) * 16;
-  if constexpr (WS_PRIO) {
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-  }
-  int buf = 0;
-  for (int64_t mt = group; mt < a.mtiles; mt += groups, buf = buf + 1 == NB ? 0 : buf + 1) {
-    const int64_t mn = mt + (int64_t)(NB - 1) * groups;
-    const int nbuf = buf + NB - 1 >= NB ? buf - 1 : buf + NB - 1;   // (buf + NB - 1) % NB
-    if (mn < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + nbuf * C::TILE, wave, lane);
-    const int64_t m0 = mt * WS_TM;
-    const int nst = nw + (q & 1) * 16 + (q >> 1) * 8;   // store-layout column
-    // epilogue operands (WS_OPS_EARLY: all issued before the MFMAs, else one
-    // row block ahead of their use)
-    constexpr bool WS_OPS_EARLY = ws_ops_early<EPI>();
-    constexpr int NSLOT = WS_OPS_EARLY ? WS_RB : 2;
-    u32x4 rv[NSLOT], tv[NSLOT];
-    uint32_t hw[NSLOT];   // the mask word of columns nw .. nw+31
-    auto load_ops = [&](int rb, int slot) {
-      const int64_t m = m0 + rb * 16 + l15;
-      const bool ok = m < a.M && nst < a.N;
-      if constexpr (HAS_R)
-        rv[slot] = __builtin_amdgcn_raw_buffer_load_b128(rr_, ok ? (int)((m * a.ldr + nst) * 2) : OOR, 0, 0);
-      if constexpr (HAS_HT) {
-        hw[slot] = __builtin_amdgcn_raw_buffer_load_b32(
-            hr, (m < a.M && nw < a.N) ? (int)((m * a.ldhb + (nw >> 5)) * 4) : OOR, 0, 0);
-        tv[slot] = __builtin_amdgcn_raw_buffer_load_b128(tr, ok ? (int)((m * a.ldt + nst) * 2) : OOR, 0, 0);
-      }
-    };
-    if constexpr (WS_OPS_EARLY) {
-#pragma unroll
-      for (int rb = 0; rb < WS_RB; ++rb) load_ops(rb, rb);
-    } else {
-      load_ops(0, 0);
+  const int nst = nw + (q & 1) * 16 + (q >> 1) * 8;   // store-layout column
+  // epilogue operands (WS_OPS_EARLY: all issued before the MFMAs, else one
+  // row block ahead of their use)
+  constexpr bool WS_OPS_EARLY = ws_ops_early<EPI>();
+  constexpr int NSLOT = WS_OPS_EARLY ? WS_RB : 2;
+  u32x4 rv[NSLOT], tv[NSLOT];
+  uint32_t hw[NSLOT];   // the mask word of columns nw .. nw+31
+  auto load_ops = [&](int64_t m0, int rb, int slot) {
+    const int64_t m = m0 + rb * 16 + l15;
+    const bool ok = m < a.M && nst < a.N;
+    if constexpr (HAS_R)
+      rv[slot] = __builtin_amdgcn_raw_buffer_load_b128(rr_, ok ? (int)((m * a.ldr + nst) * 2) : OOR, 0, 0);
+    if constexpr (HAS_HT) {
+      hw[slot] = __builtin_amdgcn_raw_buffer_load_b32(
+          hr, (m < a.M && nw < a.N) ? (int)((m * a.ldhb + (nw >> 5)) * 4) : OOR, 0, 0);
+      tv[slot] = __builtin_amdgcn_raw_buffer_load_b128(tr, ok ? (int)((m * a.ldt + nst) * 2) : OOR, 0, 0);
     }
-    const char* xb = lds + buf * C::TILE + rowoff;
-
-    f32x4 acc[WS_RB][2];
-#pragma unroll
-    for (int rb = 0; rb < WS_RB; ++rb)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // fragment (kt, rb): row rb*16 + l15, physical chunk (4kt + q) ^ l15 =
-    // 16 (kt >> 2) + coff[kt & 3]: 4 offset registers, the rest immediates
-    auto xrd = [&](int kt, int rb) {
-      return *reinterpret_cast<const bf16x8*>(xb + rb * 16 * C::P + (kt >> 2) * 256 + coff[kt & 3]);
-    };
-    bf16x8 xf[2][WS_RB];
-#pragma unroll
-    for (int rb = 0; rb < WS_RB; ++rb) xf[0][rb] = xrd(0, rb);
-#pragma unroll
-    for (int kt = 0; kt < KTP; ++kt) {
-      const int cur = kt & 1;
-      if (kt + 1 < KTP) {
-#pragma unroll
-        for (int rb = 0; rb < WS_RB; ++rb) xf[cur ^ 1][rb] = xrd(kt + 1, rb);
-      }
-#pragma unroll
-      for (int rb = 0; rb < WS_RB; ++rb)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-          if constexpr (!(WS_LAB_MODE & 4))
-            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][kt], xf[cur][rb], acc[rb][cb], 0, 0, 0);
-          else
-            acc[rb][cb][0] += (float)xf[cur][rb][cb] + (float)wf[cb][kt][0];
-#if WS_PREFETCH_PIN
-      // keep step kt+1's fragment reads in step kt (a full step of MFMAs
-      // between a read and its use), spread between the MFMAs
-      if (kt + 1 < KTP) {
-#pragma unroll
-        for (int rb = 0; rb < WS_RB; ++rb) {
-          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#endif
-    }
-
-    // ---- epilogue: lane holds C[m][nw + 16cb + 4q .. +3], m = m0 + 16rb + l15
+  };
+  f32x4 acc[WS_RB][2];
+  // ---- epilogue of the tile at row m0 (acc, and its operands in the slots)
+  auto epilogue = [&](const int64_t m0) {
+    // lane holds C[m][nw + 16cb + 4q .. +3], m = m0 + 16rb + l15
     if constexpr (WS_LAB_MODE & 8) {   // lab: no epilogue (keep acc alive)
       float t = 0.f;
 #pragma unroll
@@ -301,7 +258,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     for (int rb = 0; rb < WS_RB; ++rb) {
       const int64_t m = m0 + rb * 16 + l15;
       const bool mok = m < a.M;
-      if (!WS_OPS_EARLY && rb + 1 < WS_RB) load_ops(rb + 1, (rb + 1) & 1);
+      if (!WS_OPS_EARLY && rb + 1 < WS_RB) load_ops(m0, rb + 1, (rb + 1) & 1);
       const int slot = WS_OPS_EARLY ? rb : rb & 1;
       u32x2 o[2], rf[2], tf[2];
       u32x4 of[2];
@@ -398,6 +355,75 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
           __builtin_amdgcn_raw_buffer_store_b128(sv, cr, off, 0, 0);
       }
     }
+  };
+
+  if constexpr (WS_PRIO) {
+    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+  }
+  const bool late = WS_STAGGER && wave >= 4;   // wave-uniform
+  int64_t pm0 = -1;                            // late waves: the tile whose epilogue is pending
+  int buf = 0;
+  for (int64_t mt = group; mt < a.mtiles; mt += groups, buf = buf + 1 == NB ? 0 : buf + 1) {
+    const int64_t mn = mt + (int64_t)(NB - 1) * groups;
+    const int nbuf = buf + NB - 1 >= NB ? buf - 1 : buf + NB - 1;   // (buf + NB - 1) % NB
+    if (mn < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + nbuf * C::TILE, wave, lane);
+    const int64_t m0 = mt * WS_TM;
+    if (late && pm0 >= 0) epilogue(pm0);   // the previous tile's, beside the partners' MFMAs
+    if constexpr (WS_OPS_EARLY) {
+#pragma unroll
+      for (int rb = 0; rb < WS_RB; ++rb) load_ops(m0, rb, rb);
+    } else {
+      load_ops(m0, 0, 0);
+    }
+    const char* xb = lds + buf * C::TILE + rowoff;
+#pragma unroll
+    for (int rb = 0; rb < WS_RB; ++rb)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) acc[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // fragment (kt, rb): row rb*16 + l15, physical chunk (4kt + q) ^ l15 =
+    // 16 (kt >> 2) + coff[kt & 3]: 4 offset registers, the rest immediates
+    auto xrd = [&](int kt, int rb) {
+      return *reinterpret_cast<const bf16x8*>(xb + rb * 16 * C::P + (kt >> 2) * 256 + coff[kt & 3]);
+    };
+    // fragments of step kt sit in buffer kt % NXB, read WS_PFD steps ahead
+    constexpr int NXB = WS_PFD + 1;
+    bf16x8 xf[NXB][WS_RB];
+#pragma unroll
+    for (int p = 0; p < WS_PFD; ++p)
+#pragma unroll
+      for (int rb = 0; rb < WS_RB; ++rb) xf[p][rb] = xrd(p, rb);
+#pragma unroll
+    for (int kt = 0; kt < KTP; ++kt) {
+      const int cur = kt % NXB;
+      const bool rd = kt + WS_PFD < KTP && !(WS_LAB_MODE & 16);
+      if (rd) {
+#pragma unroll
+        for (int rb = 0; rb < WS_RB; ++rb) xf[(kt + WS_PFD) % NXB][rb] = xrd(kt + WS_PFD, rb);
+      }
+#pragma unroll
+      for (int rb = 0; rb < WS_RB; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb)
+          if constexpr (!(WS_LAB_MODE & 4))
+            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][kt], xf[cur][rb], acc[rb][cb], 0, 0, 0);
+          else
+            acc[rb][cb][0] += (float)xf[cur][rb][cb] + (float)wf[cb][kt][0];
+#if WS_PREFETCH_PIN
+      // keep step kt+PFD's fragment reads in step kt (PFD full steps of MFMAs
+      // between a read and its use), spread between the MFMAs
+      if (rd) {
+#pragma unroll
+        for (int rb = 0; rb < WS_RB; ++rb) {
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+
+    if (late) pm0 = m0;
+    else epilogue(m0);
     // next tile's X landed and every wave is done reading this buffer.  Younger
     // than the next tile's DMAs: the stores of the last NB-1 tiles and the
     // DMAs of the NB-2 tiles after it -- when all of those were issued (near
@@ -409,6 +435,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
+  if (late && pm0 >= 0) epilogue(pm0);
   if constexpr (STATS) {
     // 16-lane butterfly: lane (q, m) ends with k = bit2(m), cb = bit3(m),
     // column pair element r = 2 bit0(m) + bit1(m) of columns nw + 16cb + 4q

@@ -312,8 +312,10 @@ __global__ __launch_bounds__(K2_NT) void scan3_kernel(const float* __restrict__ 
                                                       const float* __restrict__ qn, int64_t Q,
                                                       int k, int64_t rows_per_block, int nslices,
                                                       int qtiles, Cand* out,
-                                                      const float* __restrict__ thr0) {
+                                                      const float* __restrict__ thr0,
+                                                      const int* gate = nullptr) {
   constexpr int S4 = DV / 4;
+  if (gate && *gate == 0) return;   // scan v4 fallback: only when v4 overflowed
   __shared__ float cd[K2_WPB][K3_QT][K2_CAP];
   __shared__ int ci[K2_WPB][K3_QT][K2_CAP];
   __shared__ int cntl[K2_WPB][K3_QT];
@@ -451,12 +453,13 @@ constexpr float TH_MARGIN = 1e-5f;
 // a 2-pass radix select over the distances' bits (exponent + 7 mantissa
 // bits): the upper edge of the selected bin, an upper bound within 2^-7
 // relative of the exact k-th value.
-template <int DV>
+template <int DV, int SAMPLE = TH_S>
 __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict__ tab,
                                                         const float* __restrict__ inv, int64_t N,
                                                         const float* __restrict__ q, float* qn,
-                                                        int k, float* thr0) {
-  constexpr int PT = TH_S / 256;
+                                                        int k, float* thr0, bf16* qb = nullptr,
+                                                        int* qcnt = nullptr) {
+  constexpr int PT = SAMPLE / 256;
   constexpr int d = DV * 4;   // <= 64: one element per lane
   __shared__ unsigned hist[256];
   __shared__ unsigned sel_prefix, sel_need;
@@ -471,11 +474,13 @@ __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict_
     if (lane < d) {
       qs[lane] = v * in;
       qn[qq * d + lane] = v * in;
+      if (qb) qb[qq * d + lane] = (bf16)(v * in);
     }
+    if (qcnt && lane == 0) qcnt[qq] = 0;
   }
   __syncthreads();
   const float4* qv = reinterpret_cast<const float4*>(qs);
-  const int S = (int)min<int64_t>(N, TH_S);
+  const int S = (int)min<int64_t>(N, SAMPLE);
   unsigned key[PT];
 #pragma unroll 4
   for (int j = 0; j < PT; ++j) {
@@ -542,6 +547,223 @@ __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict_
   }
 }
 
+// ---------------------------------------------------------------- scan v4
+// Batched queries (Q >= V4_MIN_Q, d = 32 or 64): bf16-MFMA coarse scoring of
+// every (row, query) pair + exact fp32 re-scoring of the rows it admits.
+//
+// The coarse cosine is sum_i bf16(x_i * inv_r) * bf16(q_i / |q|), fp32
+// accumulation (v_mfma_f32_16x16x32_bf16: 16x the fp32-MFMA rate).  Each
+// factor carries a relative rounding error <= 2^-9, so for unit vectors
+// |coarse - exact| <= 2^-8 + 2^-16 + fp32 slack < V4_EPS on the distance.
+// Every row of the exact top-k has exact distance <= E_k (the k-th best)
+// <= T0 (the k-th best of a V4_S-row exact sample: any subset's k-th best
+// bounds the table's), hence coarse distance <= T0 + V4_EPS: admitting the
+// rows under that bound keeps every true neighbour, ties included.  The
+// admitted rows (~N k / V4_S per query) are appended to a per-query list;
+// rescore_kernel recomputes their distances EXACTLY as scan v2 does (fp32,
+// float4 dot order) and selects the k best by (distance, row).  A query whose
+// list overflows V4_CAP (or whose k-th distance is shared by more than
+// V4_SCAP rows) raises a flag and the exact scan v3 + merge, launched behind
+// it and gated on the flag, recomputes the batch.
+constexpr float V4_EPS = 0.004f;
+constexpr int V4_S = 8192;       // exact sample rows for the admission bound
+constexpr int V4_CAP = 4096;     // admitted rows per query
+constexpr int V4_SCAP = 256;     // rows at or under the selected k-th bin
+constexpr int V4_QC = 256;       // queries per block (LDS: V4_QC x d bf16)
+constexpr int V4_RPB = 512;      // table rows per block
+#ifndef V4_MIN_Q
+#define V4_MIN_Q 16
+#endif
+
+// one 16-row x 32-k bf16 A fragment of lane (r16, g): row r, k in
+// [32 ks + 8 g, +8), scaled by the row's inverse norm
+template <int KS>
+__device__ __forceinline__ void v4_load_rows(const float* __restrict__ tab, int64_t r, float4 (&x)[KS][2],
+                                             int g) {
+  const float4* rp = reinterpret_cast<const float4*>(tab + r * (KS * 32));
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    x[ks][0] = rp[ks * 8 + 2 * g];
+    x[ks][1] = rp[ks * 8 + 2 * g + 1];
+  }
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void scan4_kernel(const float* __restrict__ tab,
+                                                    const float* __restrict__ inv, int64_t N,
+                                                    const bf16* __restrict__ qb,
+                                                    const float* __restrict__ thr0, int64_t Q,
+                                                    int* qcnt, int* rows, int* flag) {
+  constexpr int D = KS * 32;
+  __shared__ __attribute__((aligned(16))) bf16 qs[V4_QC * D];
+  __shared__ float th[V4_QC];
+  const int64_t qc0 = (int64_t)blockIdx.y * V4_QC;
+  const int nq = (int)min<int64_t>(V4_QC, Q - qc0);
+  for (int i = threadIdx.x; i < V4_QC * D / 8; i += 256) {
+    const int qi = i / (D / 8);
+    reinterpret_cast<bf16x8*>(qs)[i] = qi < nq ? reinterpret_cast<const bf16x8*>(qb + qc0 * D)[i]
+                                               : bf16x8{};
+  }
+  for (int i = threadIdx.x; i < V4_QC; i += 256) th[i] = i < nq ? thr0[qc0 + i] + V4_EPS : -1.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * V4_RPB;
+  const int64_t r1 = min(N, r0 + V4_RPB);
+  const int nqb = (nq + 15) / 16;
+  float4 xn[KS][2];
+  float ivn = 0.f;
+  int64_t base = r0 + 16 * w;
+  if (base < r1) {
+    const int64_t r = base + r16 < r1 ? base + r16 : r0;
+    v4_load_rows<KS>(tab, r, xn, g);
+    ivn = inv[r];
+  }
+  for (; base < r1; base += 64) {
+    bf16x8 a[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const float4 u = xn[ks][0], v = xn[ks][1];
+      a[ks] = bf16x8{(bf16)(u.x * ivn), (bf16)(u.y * ivn), (bf16)(u.z * ivn), (bf16)(u.w * ivn),
+                     (bf16)(v.x * ivn), (bf16)(v.y * ivn), (bf16)(v.z * ivn), (bf16)(v.w * ivn)};
+    }
+    if (base + 64 < r1) {   // next tile's rows in flight under this tile's MFMAs
+      const int64_t r = base + 64 + r16 < r1 ? base + 64 + r16 : r0;
+      v4_load_rows<KS>(tab, r, xn, g);
+      ivn = inv[r];
+    }
+    for (int b = 0; b < nqb; ++b) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 bq = *reinterpret_cast<const bf16x8*>(qs + (16 * b + r16) * D + ks * 32 + 8 * g);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], bq, acc, 0, 0, 0);
+      }
+      // lane (c = r16, g): rows base + 4g + i, query 16 b + c
+      const float t = th[16 * b + r16];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t r = base + 4 * g + i;
+        if (r < r1 && 1.f - acc[i] <= t) {
+          const int64_t qi = qc0 + 16 * b + r16;
+          const int pos = atomicAdd(&qcnt[qi], 1);
+          if (pos < V4_CAP) rows[qi * V4_CAP + pos] = (int)r;
+          else *flag = 1;
+        }
+      }
+    }
+  }
+}
+
+// One block per query: exact distances of its admitted rows (scan v2's fp32
+// float4 dot order), the k-th smallest by a 2-pass radix select over their
+// bits, then a bitonic sort of the rows at or under the selected bin.
+template <int DV>
+__global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ tab,
+                                                      const float* __restrict__ inv,
+                                                      const float* __restrict__ qn, const int* qcnt,
+                                                      const int* rows, int k, int64_t* idx,
+                                                      float* dist, int* flag) {
+  constexpr int PT = V4_CAP / 256;
+  __shared__ unsigned hist[256];
+  __shared__ unsigned sel_prefix, sel_need;
+  __shared__ float cd[V4_SCAP];
+  __shared__ int ci[V4_SCAP];
+  __shared__ int cnt;
+  __shared__ __attribute__((aligned(16))) float qs[DV * 4];
+  const int64_t qq = blockIdx.x;
+  const int n = qcnt[qq];
+  if (n > V4_CAP || n < k) {   // overflow (or fewer admitted rows than k: cannot happen
+    if (threadIdx.x == 0) *flag = 1;   // when N >= k; kept as a guard)
+    return;
+  }
+  for (int i = threadIdx.x; i < DV * 4; i += 256) qs[i] = qn[qq * DV * 4 + i];
+  __syncthreads();
+  const float4* qv = reinterpret_cast<const float4*>(qs);
+  const int* rl = rows + qq * V4_CAP;
+  float dd[PT];
+  int ri[PT];
+#pragma unroll
+  for (int j = 0; j < PT; ++j) {
+    const int t = threadIdx.x + 256 * j;
+    ri[j] = t < n ? rl[t] : -1;
+    dd[j] = FLT_MAX;
+    if (ri[j] >= 0) {
+      const float4* rp = reinterpret_cast<const float4*>(tab + (int64_t)ri[j] * DV * 4);
+      float s = 0.f;
+#pragma unroll
+      for (int v = 0; v < DV; ++v) {
+        const float4 x = rp[v], q = qv[v];
+        s += x.x * q.x + x.y * q.y + x.z * q.z + x.w * q.w;
+      }
+      dd[j] = fminf(fmaxf(1.f - s * inv[ri[j]], 0.f), 2.f);
+    }
+  }
+  if (threadIdx.x == 0) { sel_prefix = 0; sel_need = (unsigned)k; cnt = 0; }
+  unsigned mask = 0;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    const int sh = 24 - 8 * pass;
+    hist[threadIdx.x] = 0;
+    __syncthreads();
+    const unsigned prefix = sel_prefix;
+#pragma unroll
+    for (int j = 0; j < PT; ++j)
+      if (ri[j] >= 0 && (__float_as_uint(dd[j]) & mask) == prefix)
+        atomicAdd(&hist[(__float_as_uint(dd[j]) >> sh) & 255u], 1u);
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      const unsigned need = sel_need;
+      unsigned h[4], sum = 0;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) { h[b] = hist[4 * lane + b]; sum += h[b]; }
+      unsigned incl = sum;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const unsigned v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+      }
+      unsigned cum = incl - sum;
+      if (cum < need && need <= incl) {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          if (cum + h[b] >= need) {
+            sel_prefix = prefix | ((unsigned)(4 * lane + b) << sh);
+            sel_need = need - cum;
+            break;
+          }
+          cum += h[b];
+        }
+      }
+    }
+    mask |= 255u << sh;
+    __syncthreads();
+  }
+  const unsigned tk = sel_prefix | 0xffffu;   // upper edge of the k-th distance's bin
+#pragma unroll
+  for (int j = 0; j < PT; ++j)
+    if (ri[j] >= 0 && __float_as_uint(dd[j]) <= tk) {
+      const int pos = atomicAdd(&cnt, 1);
+      if (pos < V4_SCAP) { cd[pos] = dd[j]; ci[pos] = ri[j]; }
+    }
+  __syncthreads();
+  const int nv = cnt;
+  if (nv > V4_SCAP) {   // too many rows share the k-th bin: exact fallback
+    if (threadIdx.x == 0) *flag = 1;
+    return;
+  }
+  int n2 = 2;
+  while (n2 < nv) n2 <<= 1;
+  for (int t = nv + threadIdx.x; t < n2; t += 256) { cd[t] = FLT_MAX; ci[t] = INT_MAX; }
+  __syncthreads();
+  bitonic(cd, ci, n2);
+  for (int t = threadIdx.x; t < k; t += 256) {
+    idx[qq * k + t] = (int64_t)ci[t];
+    dist[qq * k + t] = cd[t];
+  }
+}
+
 // Per query: the k best of nslices k-lists.  All of a chunk's candidates are
 // loaded up front (MT per thread, one round trip), then filtered against the
 // running k-th best and compacted in LDS.
@@ -552,7 +774,8 @@ constexpr int FT = 24;   // fast path: candidates loaded per thread per round
 // stage writes idx / dist.
 __global__ __launch_bounds__(NT) void merge_kernel(const Cand* in, int nslices, int k,
                                                    int64_t* idx, float* dist, int groups,
-                                                   Cand* gout) {
+                                                   Cand* gout, const int* gate = nullptr) {
+  if (gate && *gate == 0) return;
   __shared__ float cd[CAP];
   __shared__ int ci[CAP];
   __shared__ int cnt;
@@ -813,11 +1036,20 @@ void plan2(int64_t N, int* nslices, int64_t* rows_per_block) {
   *nslices = (int)cdiv(N, *rows_per_block);
 }
 
+bool use_v4(int64_t Q, int d, int k) { return use_v2(d, k) && Q >= V4_MIN_Q && d % 32 == 0; }
+
+// v4 scratch after the v2 layout (cands | qn [Q][d] | thr0 [Q]): bf16
+// queries [Q][d] | per-query counts [Q] | flag | admitted rows [Q][V4_CAP]
+size_t v4_extra(int64_t Q, int d) {
+  return rup((size_t)Q * d * 2, 256) + rup((size_t)Q * 4 + 4, 256) + (size_t)Q * V4_CAP * 4 + 256;
+}
+
 size_t topk_ws_d(int64_t N, int64_t Q, int k, int d) {
   int ns; int64_t rps;
   if (use_v2(d, k)) {
     plan2(N, &ns, &rps);
-    return rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4;
+    const size_t v2 = rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4;
+    return use_v4(Q, d, k) ? rup(v2, 256) + v4_extra(Q, d) : v2;
   }
   plan(N, Q, k, &ns, &rps);
   return (size_t)Q * ns * k * sizeof(Cand);
@@ -829,9 +1061,9 @@ size_t topk_ws_d(int64_t N, int64_t Q, int k, int d) {
 // one-shot 8192-entry bitonic sort by 1024 threads 107 us; a per-wave register
 // merge 50 us -- the block barriers of a one-block kernel dominate all of them.
 dcnr_status merge_lists(const Cand* cands, int64_t Q, int ns, int k, int64_t* idx, float* dist,
-                        hipStream_t s) {
+                        hipStream_t s, const int* gate = nullptr) {
   hipLaunchKernelGGL(merge_kernel, dim3((unsigned)Q), dim3(NT), 0, s, cands, ns, k, idx, dist, 1,
-                     nullptr);
+                     nullptr, gate);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
@@ -874,6 +1106,53 @@ dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, cons
 #undef CASEK
     }
     DCNR_LAUNCH_CHECK();
+    int* gate = nullptr;   // v4: the exact scan v3 below runs only if v4 overflowed
+    if (use_v4(Q, d, k)) {
+      char* x = (char*)ws + rup(rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4, 256);
+      bf16* qb = (bf16*)x;
+      x += rup((size_t)Q * d * 2, 256);
+      int* qcnt = (int*)x;
+      gate = qcnt + Q;
+      x += rup((size_t)Q * 4 + 4, 256);
+      int* rows = (int*)x;
+      DCNR_HIP(hipMemsetAsync(gate, 0, 4, s));
+      switch (d / 32) {
+        case 1:
+          hipLaunchKernelGGL((kth_bound_kernel<8, V4_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv,
+                             N, q, qn, k, thr0, qb, qcnt);
+          break;
+        case 2:
+          hipLaunchKernelGGL((kth_bound_kernel<16, V4_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv,
+                             N, q, qn, k, thr0, qb, qcnt);
+          break;
+      }
+      DCNR_LAUNCH_CHECK();
+      const dim3 g4((unsigned)cdiv(N, V4_RPB), (unsigned)cdiv(Q, V4_QC));
+      if (d == 32)
+        hipLaunchKernelGGL(scan4_kernel<1>, g4, dim3(256), 0, s, t, inv, N, qb, thr0, Q, qcnt, rows, gate);
+      else
+        hipLaunchKernelGGL(scan4_kernel<2>, g4, dim3(256), 0, s, t, inv, N, qb, thr0, Q, qcnt, rows, gate);
+      DCNR_LAUNCH_CHECK();
+      if (d == 32)
+        hipLaunchKernelGGL(rescore_kernel<8>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, qn, qcnt, rows,
+                           k, idx, dist, gate);
+      else
+        hipLaunchKernelGGL(rescore_kernel<16>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, qn, qcnt,
+                           rows, k, idx, dist, gate);
+      DCNR_LAUNCH_CHECK();
+      // the exact fallback below needs the v2 admission bound (512-row sample)
+      switch (d / 32) {
+        case 1:
+          hipLaunchKernelGGL((kth_bound_kernel<8, TH_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv,
+                             N, q, qn, k, thr0, nullptr, nullptr);
+          break;
+        case 2:
+          hipLaunchKernelGGL((kth_bound_kernel<16, TH_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv,
+                             N, q, qn, k, thr0, nullptr, nullptr);
+          break;
+      }
+      DCNR_LAUNCH_CHECK();
+    }
     if (Q >= MFMA_MIN_Q && d % 16 == 0) {
       const int qtiles = (int)cdiv(Q, K3_QT);
       const int64_t blocks = rup(ns, 8) * qtiles;
@@ -881,13 +1160,13 @@ dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, cons
 #define CASE3(n)                                                                                   \
   case n:                                                                                          \
     hipLaunchKernelGGL(scan3_kernel<4 * n>, dim3((unsigned)blocks), dim3(K2_NT), 0, s, t, inv, N,  \
-                       qn, Q, k, rps, ns, qtiles, cands, thr0);                                    \
+                       qn, Q, k, rps, ns, qtiles, cands, thr0, gate);                              \
     break;
         CASE3(1) CASE3(2) CASE3(3) CASE3(4)
 #undef CASE3
       }
       DCNR_LAUNCH_CHECK();
-      return merge_lists(cands, Q, ns, k, idx, dist, s);
+      return merge_lists(cands, Q, ns, k, idx, dist, s, gate);
     }
     const int qtiles = (int)cdiv(Q, K2_QT);
     const int64_t blocks = rup(ns, 8) * qtiles;

@@ -435,15 +435,16 @@ def test_cosine_knn_vs_sklearn_golden(dev):
             np.testing.assert_array_equal(i[r][isolated], ref_i[isolated])
 
 
-@pytest.mark.parametrize("Q", [1, 3, 8])
-def test_cosine_knn_full_size(dev, Q):
-    """configs[4] size: cosine top-11 over 1M x 64 (VALU scan for Q < 4, MFMA
-    scan for Q >= 4; final merge through the list-minima bound) against a
-    brute-force torch fp32 reference on the device (random table: no ties)."""
+@pytest.mark.parametrize("Q,d", [(1, 64), (3, 64), (8, 64), (32, 64), (256, 64), (64, 32)])
+def test_cosine_knn_full_size(dev, Q, d):
+    """configs[4] size: cosine top-11 over 1M x d (VALU scan for Q < 16; from
+    Q = 16 the bf16-MFMA coarse scan + exact fp32 rescoring of its admitted
+    rows, knn.hip scan v4) against a brute-force torch fp32 reference on the
+    device (random table: no ties)."""
     import dcnr
-    g = torch.Generator(device=dev).manual_seed(11 + Q)
-    table = torch.randn(1_000_000, 64, device=dev, generator=g)
-    q = torch.randn(Q, 64, device=dev, generator=g)
+    g = torch.Generator(device=dev).manual_seed(11 + Q + d)
+    table = torch.randn(1_000_000, d, device=dev, generator=g)
+    q = torch.randn(Q, d, device=dev, generator=g)
     nn_ = dcnr.NearestNeighbors(metric="cosine", algorithm="brute").fit(table)
     d, i = nn_.kneighbors(q, n_neighbors=11)
     d = np.asarray(d.cpu() if torch.is_tensor(d) else d)
@@ -454,6 +455,34 @@ def test_cosine_knn_full_size(dev, Q):
     ref_d, ref_i = ref_d.cpu().numpy(), ref_i.cpu().numpy()
     np.testing.assert_allclose(d, ref_d, rtol=0, atol=2e-6)
     for r in range(Q):
+        near = np.diff(ref_d[r]) <= 2e-6
+        isolated = np.ones(11, bool)
+        isolated[1:] &= ~near
+        isolated[:-1] &= ~near
+        np.testing.assert_array_equal(i[r][isolated], ref_i[r][isolated])
+
+
+def test_cosine_knn_v4_overflow_falls_back_exact(dev):
+    """More than V4_CAP rows inside one query's admission bound (12000 rows
+    on the query's own direction, every one at distance 0): scan v4's list
+    overflows, its flag gates the exact scan v3 + merge, and the result is
+    the exact top-k, ties by row index (the duplicates' lowest rows)."""
+    import dcnr
+    g = torch.Generator(device=dev).manual_seed(5)
+    table = torch.randn(200_000, 64, device=dev, generator=g)
+    q = torch.randn(32, 64, device=dev, generator=g)
+    dup = torch.randperm(200_000, device=dev, generator=g)[:12000]
+    table[dup] = q[0] * 2.0
+    nn_ = dcnr.NearestNeighbors(metric="cosine", algorithm="brute").fit(table)
+    d, i = nn_.kneighbors(q, n_neighbors=11)
+    assert np.all(d[0] <= 2e-6)
+    assert i[0].tolist() == sorted(dup.cpu().tolist())[:11]
+    tn = table / table.norm(dim=1, keepdim=True)
+    qn = q / q.norm(dim=1, keepdim=True)
+    ref_d, ref_i = torch.topk(1.0 - qn @ tn.T, 11, dim=1, largest=False)
+    ref_d, ref_i = ref_d.cpu().numpy(), ref_i.cpu().numpy()
+    np.testing.assert_allclose(d[1:], ref_d[1:], rtol=0, atol=2e-6)
+    for r in range(1, 32):
         near = np.diff(ref_d[r]) <= 2e-6
         isolated = np.ones(11, bool)
         isolated[1:] &= ~near

@@ -1,5 +1,6 @@
-import sys, time, torch
-sys.path.insert(0, "hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd")
+import os, sys, time, torch
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd"))
 import dcnr
 from dcnr import _lib
 dev = torch.device("cuda:0")
