@@ -1383,9 +1383,19 @@ size_t dcnr_cosine_topk_workspace_size(int64_t N, int64_t Q, int32_t k) {
   return topk_ws(N, Q, k) + 256;
 }
 
-dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t N, int32_t d,
-                             const float* queries, int64_t Q, int32_t k, int64_t* idx, float* dist,
-                             void* ws, size_t ws_bytes, dcnr_stream_t stream) {
+dcnr_status dcnr_cosine_pack_rows(const float* table, const float* inv_norms, int64_t N, int32_t d,
+                                  uint16_t* packed, dcnr_stream_t stream) {
+  if (!table || !inv_norms || !packed || d < 1 || N < 0) {
+    set_error("dcnr_cosine_pack_rows: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  return cosine_pack_rows(table, inv_norms, N, d, (bf16*)packed, (hipStream_t)stream);
+}
+
+dcnr_status dcnr_cosine_topk_packed(const float* table, const float* inv_norms, const uint16_t* packed,
+                                    int64_t N, int32_t d, const float* queries, int64_t Q, int32_t k,
+                                    int64_t* idx, float* dist, void* ws, size_t ws_bytes,
+                                    dcnr_stream_t stream) {
   if (!table || !inv_norms || !queries || !idx || !dist || (Q > 0 && !ws)) {
     set_error("dcnr_cosine_topk: null argument");
     return DCNR_BAD_ARG;
@@ -1396,8 +1406,16 @@ dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t
     return DCNR_BAD_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  TRYB(DCNR_K_KNN, (double)N * (4.0 * d + 4.0), cosine_topk(table, inv_norms, N, d, queries, Q, k, idx, dist, ws, ws_bytes, s));
+  TRYB(DCNR_K_KNN, (double)N * (4.0 * d + 4.0),
+       cosine_topk(table, inv_norms, (const bf16*)packed, N, d, queries, Q, k, idx, dist, ws, ws_bytes, s));
   return DCNR_OK;
+}
+
+dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t N, int32_t d,
+                             const float* queries, int64_t Q, int32_t k, int64_t* idx, float* dist,
+                             void* ws, size_t ws_bytes, dcnr_stream_t stream) {
+  return dcnr_cosine_topk_packed(table, inv_norms, nullptr, N, d, queries, Q, k, idx, dist, ws, ws_bytes,
+                                 stream);
 }
 
 dcnr_status dcnr_topk_merge(const float* dist, const int64_t* idx, int32_t lists, int64_t Q,

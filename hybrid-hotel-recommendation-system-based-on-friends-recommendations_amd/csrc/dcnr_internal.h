@@ -544,9 +544,12 @@ size_t topk_ws(int64_t N, int64_t Q, int k);
 // k best of lists k-lists [lists][Q][k] by (dist, row as unsigned)
 dcnr_status topk_merge(const float* dist, const int64_t* idx, int lists, int64_t Q, int k,
                        int64_t* out_idx, float* out_dist, hipStream_t s);
-dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, const float* q,
-                        int64_t Q, int k, int64_t* idx, float* dist, void* ws, size_t ws_bytes,
-                        hipStream_t s);
+// tb: the bf16 copy from cosine_pack_rows, or nullptr (scan v4 then rounds
+// the fp32 rows itself)
+dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_t N, int d,
+                        const float* q, int64_t Q, int k, int64_t* idx, float* dist, void* ws,
+                        size_t ws_bytes, hipStream_t s);
+dcnr_status cosine_pack_rows(const float* t, const float* inv, int64_t N, int d, bf16* out, hipStream_t s);
 
 // serving (serving.hip)
 dcnr_status gather_rows(const int64_t* idx, int64_t n, int64_t n_src, int n_arrays,

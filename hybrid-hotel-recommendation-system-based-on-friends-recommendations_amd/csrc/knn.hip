@@ -16,6 +16,7 @@
 
 #include <cfloat>
 #include <climits>
+#include <type_traits>
 
 namespace dcnr {
 namespace {
@@ -31,11 +32,13 @@ __device__ __forceinline__ bool cless(float da, int ia, float db, int ib) {
   return da < db || (da == db && (unsigned)ia < (unsigned)ib);
 }
 
-// bitonic sort of CAP entries in LDS, ascending; all NT threads participate
+// bitonic sort of n2 (a power of two) entries in LDS, ascending by (d, i);
+// all NTB threads of the block participate
+template <int NTB = NT>
 __device__ void bitonic(float* cd, int* ci, int n2 = CAP) {
   for (int k2 = 2; k2 <= n2; k2 <<= 1) {
     for (int j = k2 >> 1; j > 0; j >>= 1) {
-      for (int t = threadIdx.x; t < n2 / 2; t += NT) {
+      for (int t = threadIdx.x; t < n2 / 2; t += NTB) {
         const int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
         const int p = i + j;
         const bool asc = (i & k2) == 0;
@@ -453,13 +456,13 @@ constexpr float TH_MARGIN = 1e-5f;
 // a 2-pass radix select over the distances' bits (exponent + 7 mantissa
 // bits): the upper edge of the selected bin, an upper bound within 2^-7
 // relative of the exact k-th value.
-template <int DV, int SAMPLE = TH_S>
-__global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict__ tab,
+template <int DV, int SAMPLE = TH_S, int NTB = 256>
+__global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict__ tab,
                                                         const float* __restrict__ inv, int64_t N,
                                                         const float* __restrict__ q, float* qn,
                                                         int k, float* thr0, bf16* qb = nullptr,
-                                                        int* qcnt = nullptr) {
-  constexpr int PT = SAMPLE / 256;
+                                                        int* qcnt = nullptr, int* gate = nullptr) {
+  constexpr int PT = SAMPLE / NTB;
   constexpr int d = DV * 4;   // <= 64: one element per lane
   __shared__ unsigned hist[256];
   __shared__ unsigned sel_prefix, sel_need;
@@ -477,6 +480,7 @@ __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict_
       if (qb) qb[qq * d + lane] = (bf16)(v * in);
     }
     if (qcnt && lane == 0) qcnt[qq] = 0;
+    if (gate && qq == 0 && lane == 0) *gate = 0;
   }
   __syncthreads();
   const float4* qv = reinterpret_cast<const float4*>(qs);
@@ -484,7 +488,7 @@ __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict_
   unsigned key[PT];
 #pragma unroll 4
   for (int j = 0; j < PT; ++j) {
-    const int t = threadIdx.x + j * 256;
+    const int t = threadIdx.x + j * NTB;
     float dist = FLT_MAX;
     if (t < S) {
       const float4* rp = reinterpret_cast<const float4*>(tab + (int64_t)t * DV * 4);
@@ -506,7 +510,7 @@ __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict_
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     const int sh = 24 - 8 * pass;
-    hist[threadIdx.x] = 0;
+    if (threadIdx.x < 256) hist[threadIdx.x] = 0;
     __syncthreads();
     const unsigned prefix = sel_prefix;
 #pragma unroll
@@ -558,10 +562,12 @@ __global__ __launch_bounds__(256) void kth_bound_kernel(const float* __restrict_
 // Every row of the exact top-k has exact distance <= E_k (the k-th best)
 // <= T0 (the k-th best of a V4_S-row exact sample: any subset's k-th best
 // bounds the table's), hence coarse distance <= T0 + V4_EPS: admitting the
-// rows under that bound keeps every true neighbour, ties included.  The
-// admitted rows (~N k / V4_S per query) are appended to a per-query list;
-// rescore_kernel recomputes their distances EXACTLY as scan v2 does (fp32,
-// float4 dot order) and selects the k best by (distance, row).  A query whose
+// rows under that bound keeps every true neighbour, ties included.  T0 comes
+// from the same machinery run on the sample under the 512-row bound of
+// kth_bound_kernel (pass 1).  The admitted rows (~N k / V4_S per query) are
+// appended to a per-query list; rescore_kernel recomputes their distances in
+// fp32 (the products of scan v2, summed by a 16-lane butterfly) and selects
+// the k best by (distance, row).  A query whose
 // list overflows V4_CAP (or whose k-th distance is shared by more than
 // V4_SCAP rows) raises a flag and the exact scan v3 + merge, launched behind
 // it and gated on the flag, recomputes the batch.
@@ -570,150 +576,53 @@ constexpr int V4_S = 8192;       // exact sample rows for the admission bound
 constexpr int V4_CAP = 4096;     // admitted rows per query
 constexpr int V4_SCAP = 256;     // rows at or under the selected k-th bin
 constexpr int V4_QC = 256;       // queries per block (LDS: V4_QC x d bf16)
-constexpr int V4_RPB = 512;      // table rows per block
+#ifndef V4_RPB_OVR
+#define V4_RPB_OVR 512
+#endif
+constexpr int V4_RPB = V4_RPB_OVR;   // table rows per block
 #ifndef V4_MIN_Q
 #define V4_MIN_Q 16
 #endif
 
-// one 16-row x 32-k bf16 A fragment of lane (r16, g): row r, k in
-// [32 ks + 8 g, +8), scaled by the row's inverse norm
-template <int KS>
-__device__ __forceinline__ void v4_load_rows(const float* __restrict__ tab, int64_t r, float4 (&x)[KS][2],
-                                             int g) {
-  const float4* rp = reinterpret_cast<const float4*>(tab + r * (KS * 32));
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    x[ks][0] = rp[ks * 8 + 2 * g];
-    x[ks][1] = rp[ks * 8 + 2 * g + 1];
-  }
-}
-
-template <int KS>
-__global__ __launch_bounds__(256) void scan4_kernel(const float* __restrict__ tab,
-                                                    const float* __restrict__ inv, int64_t N,
-                                                    const bf16* __restrict__ qb,
-                                                    const float* __restrict__ thr0, int64_t Q,
-                                                    int* qcnt, int* rows, int* flag) {
-  constexpr int D = KS * 32;
-  __shared__ __attribute__((aligned(16))) bf16 qs[V4_QC * D];
-  __shared__ float th[V4_QC];
-  const int64_t qc0 = (int64_t)blockIdx.y * V4_QC;
-  const int nq = (int)min<int64_t>(V4_QC, Q - qc0);
-  for (int i = threadIdx.x; i < V4_QC * D / 8; i += 256) {
-    const int qi = i / (D / 8);
-    reinterpret_cast<bf16x8*>(qs)[i] = qi < nq ? reinterpret_cast<const bf16x8*>(qb + qc0 * D)[i]
-                                               : bf16x8{};
-  }
-  for (int i = threadIdx.x; i < V4_QC; i += 256) th[i] = i < nq ? thr0[qc0 + i] + V4_EPS : -1.f;
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int r16 = lane & 15, g = lane >> 4;
-  const int64_t r0 = (int64_t)blockIdx.x * V4_RPB;
-  const int64_t r1 = min(N, r0 + V4_RPB);
-  const int nqb = (nq + 15) / 16;
-  float4 xn[KS][2];
-  float ivn = 0.f;
-  int64_t base = r0 + 16 * w;
-  if (base < r1) {
-    const int64_t r = base + r16 < r1 ? base + r16 : r0;
-    v4_load_rows<KS>(tab, r, xn, g);
-    ivn = inv[r];
-  }
-  for (; base < r1; base += 64) {
-    bf16x8 a[KS];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const float4 u = xn[ks][0], v = xn[ks][1];
-      a[ks] = bf16x8{(bf16)(u.x * ivn), (bf16)(u.y * ivn), (bf16)(u.z * ivn), (bf16)(u.w * ivn),
-                     (bf16)(v.x * ivn), (bf16)(v.y * ivn), (bf16)(v.z * ivn), (bf16)(v.w * ivn)};
-    }
-    if (base + 64 < r1) {   // next tile's rows in flight under this tile's MFMAs
-      const int64_t r = base + 64 + r16 < r1 ? base + 64 + r16 : r0;
-      v4_load_rows<KS>(tab, r, xn, g);
-      ivn = inv[r];
-    }
-    for (int b = 0; b < nqb; ++b) {
-      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const bf16x8 bq = *reinterpret_cast<const bf16x8*>(qs + (16 * b + r16) * D + ks * 32 + 8 * g);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], bq, acc, 0, 0, 0);
-      }
-      // lane (c = r16, g): rows base + 4g + i, query 16 b + c
-      const float t = th[16 * b + r16];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int64_t r = base + 4 * g + i;
-        if (r < r1 && 1.f - acc[i] <= t) {
-          const int64_t qi = qc0 + 16 * b + r16;
-          const int pos = atomicAdd(&qcnt[qi], 1);
-          if (pos < V4_CAP) rows[qi * V4_CAP + pos] = (int)r;
-          else *flag = 1;
-        }
-      }
-    }
-  }
-}
-
-// One block per query: exact distances of its admitted rows (scan v2's fp32
-// float4 dot order), the k-th smallest by a 2-pass radix select over their
-// bits, then a bitonic sort of the rows at or under the selected bin.
-template <int DV>
-__global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ tab,
-                                                      const float* __restrict__ inv,
-                                                      const float* __restrict__ qn, const int* qcnt,
-                                                      const int* rows, int k, int64_t* idx,
-                                                      float* dist, int* flag) {
-  constexpr int PT = V4_CAP / 256;
+// k-th smallest of n distances (>= 0) held in LDS, by a 2-pass radix select
+// over their bits (exponent + 7 mantissa bits): returns the upper edge of the
+// selected bin (>= the exact k-th value, within 2^-7 relative), or
+// 0xffffffff when n < k.  Every thread of the block calls it.
+template <int NTB>
+__device__ unsigned block_select_kth(const float* v, int n, int k) {
   __shared__ unsigned hist[256];
   __shared__ unsigned sel_prefix, sel_need;
-  __shared__ float cd[V4_SCAP];
-  __shared__ int ci[V4_SCAP];
-  __shared__ int cnt;
-  __shared__ __attribute__((aligned(16))) float qs[DV * 4];
-  const int64_t qq = blockIdx.x;
-  const int n = qcnt[qq];
-  if (n > V4_CAP || n < k) {   // overflow (or fewer admitted rows than k: cannot happen
-    if (threadIdx.x == 0) *flag = 1;   // when N >= k; kept as a guard)
-    return;
-  }
-  for (int i = threadIdx.x; i < DV * 4; i += 256) qs[i] = qn[qq * DV * 4 + i];
-  __syncthreads();
-  const float4* qv = reinterpret_cast<const float4*>(qs);
-  const int* rl = rows + qq * V4_CAP;
-  float dd[PT];
-  int ri[PT];
-#pragma unroll
-  for (int j = 0; j < PT; ++j) {
-    const int t = threadIdx.x + 256 * j;
-    ri[j] = t < n ? rl[t] : -1;
-    dd[j] = FLT_MAX;
-    if (ri[j] >= 0) {
-      const float4* rp = reinterpret_cast<const float4*>(tab + (int64_t)ri[j] * DV * 4);
-      float s = 0.f;
-#pragma unroll
-      for (int v = 0; v < DV; ++v) {
-        const float4 x = rp[v], q = qv[v];
-        s += x.x * q.x + x.y * q.y + x.z * q.z + x.w * q.w;
-      }
-      dd[j] = fminf(fmaxf(1.f - s * inv[ri[j]], 0.f), 2.f);
-    }
-  }
-  if (threadIdx.x == 0) { sel_prefix = 0; sel_need = (unsigned)k; cnt = 0; }
+  __shared__ int sel_fail;
+  if (threadIdx.x == 0) { sel_prefix = 0; sel_need = (unsigned)k; sel_fail = n < k; }
   unsigned mask = 0;
 #pragma unroll
   for (int pass = 0; pass < 2; ++pass) {
     const int sh = 24 - 8 * pass;
-    hist[threadIdx.x] = 0;
+    if (threadIdx.x < 256) hist[threadIdx.x] = 0;
     __syncthreads();
     const unsigned prefix = sel_prefix;
-#pragma unroll
-    for (int j = 0; j < PT; ++j)
-      if (ri[j] >= 0 && (__float_as_uint(dd[j]) & mask) == prefix)
-        atomicAdd(&hist[(__float_as_uint(dd[j]) >> sh) & 255u], 1u);
+    // distances crowd into a few bins (one exponent spans a factor of 2), so
+    // equal bins of a wave are counted with one atomic (up to 4 bins per
+    // wave-instruction; the rest of the lanes add one each): plain per-lane
+    // atomics serialised ~n times on the hottest bin
+    const int lane = threadIdx.x & 63;
+    for (int i0 = threadIdx.x - lane; i0 < n; i0 += NTB) {
+      const int i = i0 + lane;
+      const unsigned key = i < n ? __float_as_uint(v[i]) : 0u;
+      const bool valid = i < n && (key & mask) == prefix;
+      const unsigned bin = (key >> sh) & 255u;
+      uint64_t act = __ballot(valid);
+      for (int it = 0; act && it < 4; ++it) {
+        const int leader = __builtin_ctzll(act);
+        const unsigned lb = (unsigned)__shfl((int)bin, leader, 64);
+        const uint64_t same = __ballot(valid && bin == lb) & act;
+        if (lane == leader) atomicAdd(&hist[lb], (unsigned)__popcll(same));
+        act &= ~same;
+      }
+      if ((act >> lane) & 1ull) atomicAdd(&hist[bin], 1u);
+    }
     __syncthreads();
     if (threadIdx.x < 64) {
-      const int lane = threadIdx.x;
       const unsigned need = sel_need;
       unsigned h[4], sum = 0;
 #pragma unroll
@@ -721,8 +630,8 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
       unsigned incl = sum;
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
-        const unsigned v = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += v;
+        const unsigned x = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += x;
       }
       unsigned cum = incl - sum;
       if (cum < need && need <= incl) {
@@ -740,12 +649,294 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
     mask |= 255u << sh;
     __syncthreads();
   }
-  const unsigned tk = sel_prefix | 0xffffu;   // upper edge of the k-th distance's bin
+  const unsigned r = sel_fail ? 0xffffffffu : (sel_prefix | 0xffffu);
+  __syncthreads();
+  return r;
+}
+
+constexpr int B4_T = 1024;   // threads of the per-query v4 kernels
+
+// one 16-row x 32-k bf16 A fragment of lane (r16, g): row r, k in
+// [32 ks + 8 g, +8), scaled by the row's inverse norm
+template <int KS>
+__device__ __forceinline__ void v4_load_rows(const float* __restrict__ tab, int64_t r, float4 (&x)[KS][2],
+                                             int g) {
+  const float4* rp = reinterpret_cast<const float4*>(tab + r * (KS * 32));
 #pragma unroll
-  for (int j = 0; j < PT; ++j)
-    if (ri[j] >= 0 && __float_as_uint(dd[j]) <= tk) {
+  for (int ks = 0; ks < KS; ++ks) {
+    x[ks][0] = rp[ks * 8 + 2 * g];
+    x[ks][1] = rp[ks * 8 + 2 * g + 1];
+  }
+}
+
+// Admissions go to a wave-private LDS list whose fill count is wave-uniform
+// (ballots + mbcnt, no atomic at all inside the loop: a returning global
+// atomic there put its contended round trip in every tile, a returning LDS
+// atomic ~100 cycles per admitting check).  At the end the block counts its
+// entries per query, reserves each query's range with one global atomic per
+// (block, query), and scatters.
+constexpr int V4_LIST = 2048;    // admitted (query, row) pairs per block
+constexpr int V4_WL = V4_LIST / 4;   // ... per wave
+#ifndef V4_PF
+#define V4_PF 4                  // packed row tiles in flight per wave
+#endif
+#ifndef V4_LAB                   // lab ablations (tools/knn_lab.sh), 0 in the library:
+#define V4_LAB 0                 // 1 no admission checks, 2 B fragments not re-read
+#endif                           // from LDS, 4 no epilogue distances
+
+template <int KS, int NQB, bool PK>
+__global__ __launch_bounds__(256) void scan4_kernel(const float* __restrict__ tab,
+                                                    const float* __restrict__ inv,
+                                                    const bf16* __restrict__ tb, int64_t N, int rpb,
+                                                    const bf16* __restrict__ qb,
+                                                    const float* __restrict__ thr0,
+                                                    const float* __restrict__ qn, int64_t Q, int* qcnt,
+                                                    int* rows, float* dists, int* flag) {
+  constexpr int D = KS * 32;
+  // up to 4 query blocks the B fragments live in registers; beyond that
+  // (64+ KS x 4 VGPRs) in LDS, stored in fragment order -- entry (b, ks,
+  // lane) is lane's 16 B, so a wave's ds_read_b128 is one contiguous 1 KB
+  // with no bank conflicts.  (Left to itself the compiler re-loaded the
+  // register copy from global memory every tile.)
+  constexpr bool BL = NQB > 4;
+  __shared__ int lq[V4_LIST];     // admitted (query, row) pairs of the block
+  __shared__ int lr[V4_LIST];
+  __shared__ int qn_[NQB * 16];   // per-query counts, then this block's bases
+  __shared__ int wcnt[4];
+  __shared__ bf16x8 bqs[BL ? NQB * KS * 64 : 1];
+  const int64_t qc0 = (int64_t)blockIdx.y * (NQB * 16);
+  const int nq = (int)min<int64_t>(NQB * 16, Q - qc0);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, g = lane >> 4;
+  const int64_t r0 = (int64_t)blockIdx.x * rpb;
+  const int64_t r1 = min(N, r0 + rpb);
+  // A fragments of the next PF row tiles in flight per wave (a register
+  // ring, static indices): fp32 rows scaled and rounded here, or (PK) the
+  // fit-time bf16 copy loaded as is.  The first PF loads go out before the
+  // query fragments are staged.
+  constexpr int PF = PK ? V4_PF : 2;
+  using Frag = typename std::conditional<PK, bf16x8[KS], float4[KS][2]>::type;
+  Frag x[PF];
+  float iv[PF];
+  auto load = [&](int64_t bse, Frag& xx, float& ivv) {
+    if (bse < r1) {
+      const int64_t r = bse + r16 < r1 ? bse + r16 : r0;
+      if constexpr (PK) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) xx[ks] = *reinterpret_cast<const bf16x8*>(tb + r * D + ks * 32 + 8 * g);
+      } else {
+        v4_load_rows<KS>(tab, r, xx, g);
+        ivv = inv[r];
+      }
+    }
+  };
+  const int64_t first = r0 + 16 * w;
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load(first + 64 * u, x[u], iv[u]);
+  int wc = 0;   // this wave's list fill (wave-uniform)
+  float labsink = 0.f;
+  // lane (c = r16, g) of B fragment (b, ks): query 16 b + c's k-chunk
+  // [32 ks + 8 g, +8)
+  bf16x8 bq[BL ? 1 : NQB][KS];
+  float th[NQB];
+  // (clamped indices + selects: all of these loads are in flight at once --
+  // as guarded loads the compiler issued them one round trip at a time,
+  // 16 serial misses in the prologue of every NQB = 16 block)
+#pragma unroll
+  for (int b = 0; b < NQB; ++b) {
+    const int qi = 16 * b + r16;
+    const int64_t qs = qc0 + min(qi, nq - 1);
+    if constexpr (!BL) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(qb + qs * D + ks * 32 + 8 * g);
+        bq[b][ks] = qi < nq ? v : bf16x8{};
+      }
+    }
+    const float t = thr0[qs];
+    th[b] = qi < nq ? t + V4_EPS : -1.f;
+  }
+  if constexpr (BL) {
+    constexpr int PER = NQB * KS * 64 / 256;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int e = threadIdx.x + 256 * j;
+      const int l = e & 63, ks = (e >> 6) % KS, b = (e >> 6) / KS;
+      const int qi = 16 * b + (l & 15);
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(qb + (qc0 + min(qi, nq - 1)) * D + ks * 32 + 8 * (l >> 4));
+      bqs[e] = qi < nq ? v : bf16x8{};
+    }
+  }
+  for (int i = threadIdx.x; i < NQB * 16; i += 256) qn_[i] = 0;
+  __syncthreads();
+  for (int64_t b0 = first; b0 < r1; b0 += 64 * PF) {
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int64_t base = b0 + 64 * u;
+      if (base >= r1) break;
+      bf16x8 a[KS];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        if constexpr (PK) {
+          a[ks] = x[u][ks];
+        } else {
+          const float4 p = x[u][ks][0], v = x[u][ks][1];
+          const float s = iv[u];
+          a[ks] = bf16x8{(bf16)(p.x * s), (bf16)(p.y * s), (bf16)(p.z * s), (bf16)(p.w * s),
+                         (bf16)(v.x * s), (bf16)(v.y * s), (bf16)(v.z * s), (bf16)(v.w * s)};
+        }
+      }
+      load(base + 64 * PF, x[u], iv[u]);
+      // every query block's MFMAs first, back to back (interleaving each
+      // block's admission checks serialised LDS read -> MFMA -> result ->
+      // ballot per block: 146 us for 256 queries), then one ballot per block
+      // on the best of its 4 rows -- almost always empty -- before the
+      // per-row ones.  Query slots past nq have zero fragments and bound -1:
+      // never pass.
+      // (LDS fragments: block b + 1's read is issued before block b's MFMAs)
+      f32x4 acc[NQB];
+      bf16x8 nb[KS];
+      if constexpr (BL) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) nb[ks] = bqs[ks * 64 + lane];
+      }
+#pragma unroll
+      for (int b = 0; b < NQB; ++b) {
+        bf16x8 cb[KS];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) cb[ks] = BL ? nb[ks] : bq[BL ? 0 : b][ks];
+        if constexpr (BL && !(V4_LAB & 2)) {
+          if (b + 1 < NQB) {
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) nb[ks] = bqs[((b + 1) * KS + ks) * 64 + lane];
+          }
+        }
+        acc[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], cb[ks], acc[b], 0, 0, 0);
+      }
+      if constexpr ((V4_LAB & 1) != 0) {
+#pragma unroll
+        for (int b = 0; b < NQB; ++b) labsink += acc[b][0] + acc[b][3];
+        continue;
+      }
+#pragma unroll
+      for (int b = 0; b < NQB; ++b) {
+        // lane (c = r16, g): rows base + 4g + i, query 16 b + c
+        const float mx = fmaxf(fmaxf(acc[b][0], acc[b][1]), fmaxf(acc[b][2], acc[b][3]));
+        if (!__ballot(1.f - mx <= th[b])) continue;   // 1 - x is monotone: min over the 4 rows
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const bool pass = base + 4 * g + i < r1 && 1.f - acc[b][i] <= th[b];
+          const uint64_t m = __ballot(pass);
+          if (pass) {
+            const int p = wc + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+            if (p < V4_WL) { lq[w * V4_WL + p] = 16 * b + r16; lr[w * V4_WL + p] = (int)(base + 4 * g + i); }
+          }
+          wc += __popcll(m);
+        }
+      }
+    }
+  }
+  if constexpr ((V4_LAB & 1) != 0) {
+    if (labsink == 12345.f) *flag = 2;
+  }
+  if (lane == 0) wcnt[w] = wc;
+  __syncthreads();
+  const int c0 = wcnt[0], c1 = wcnt[1], c2 = wcnt[2], c3 = wcnt[3];
+  if (max(max(c0, c1), max(c2, c3)) > V4_WL) {   // a wave's list overflowed: exact fallback
+    if (threadIdx.x == 0) *flag = 1;
+    return;
+  }
+  // entry j of the block (waves' lists back to back) -> its LDS slot
+  const int s1 = c0, s2 = c0 + c1, s3 = c0 + c1 + c2, n = s3 + c3;
+  auto slot = [&](int j) {
+    return j < s1 ? j : j < s2 ? V4_WL + j - s1 : j < s3 ? 2 * V4_WL + j - s2 : 3 * V4_WL + j - s3;
+  };
+  for (int e = threadIdx.x; e < n; e += 256) atomicAdd(&qn_[lq[slot(e)]], 1);
+  __syncthreads();
+  for (int q = threadIdx.x; q < nq; q += 256) {
+    const int c = qn_[q];
+    qn_[q] = c ? atomicAdd(&qcnt[qc0 + q], c) : 0;   // this block's range of query q's list
+  }
+  __syncthreads();
+  // exact fp32 distance of every admitted pair, here rather than in the
+  // per-query rescore: the row gathers (one round trip per EU x 16 pairs)
+  // then overlap the other blocks' streaming instead of forming a
+  // one-block-per-query latency chain.  16 lanes per pair: lane c takes
+  // float4 chunk c of the row and of the normalised query, a DPP butterfly
+  // sums the 16 dot4s.
+  constexpr int DV = KS * 8, EU = 4;
+  const int grp = threadIdx.x >> 4, c = threadIdx.x & 15;
+  const float4* tab4 = reinterpret_cast<const float4*>(tab);
+  const float4* qn4 = reinterpret_cast<const float4*>(qn);
+  for (int e0 = 0; e0 < ((V4_LAB & 4) ? 0 : n); e0 += 16 * EU) {
+    float4 xv[EU], qv[EU];
+    float ivv[EU];
+    int qe[EU], re[EU];
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+      const int e = e0 + 16 * u + grp;
+      const bool ok = e < n;
+      const int sl = slot(min(e, n - 1));
+      qe[u] = ok ? lq[sl] : -1;
+      re[u] = ok ? lr[sl] : 0;
+      const bool ld = ok && c < DV;
+      xv[u] = ld ? tab4[(int64_t)re[u] * DV + c] : float4{0.f, 0.f, 0.f, 0.f};
+      qv[u] = ld ? qn4[(qc0 + qe[u]) * DV + c] : float4{0.f, 0.f, 0.f, 0.f};
+      ivv[u] = inv[re[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+      float p = xv[u].x * qv[u].x + xv[u].y * qv[u].y + xv[u].z * qv[u].z + xv[u].w * qv[u].w;
+      p = row16_sum(p);
+      if (c == 0 && qe[u] >= 0) {
+        const int pos = atomicAdd(&qn_[qe[u]], 1);
+        if (pos < V4_CAP) {
+          const int64_t o = (qc0 + qe[u]) * V4_CAP + pos;
+          rows[o] = re[u];
+          dists[o] = fminf(fmaxf(1.f - p * ivv[u], 0.f), 2.f);
+        } else {
+          *flag = 1;
+        }
+      }
+    }
+  }
+}
+
+
+// One block per query: the exact distances of its admitted rows (computed
+// by scan4's epilogue), the k-th smallest by block_select_kth, then a bitonic
+// sort of the rows at or under the selected bin by (distance, row).  SMP: the
+// pass over the V4_S-row sample -- its exact k-th distance becomes the
+// query's admission bound thr0 for the table scan, and the list count is
+// reset for it.
+template <bool SMP>
+__global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__ dists, int* qcnt,
+                                                       const int* rows, int k, int64_t* idx,
+                                                       float* dist, int* flag, float* thr0) {
+  __shared__ float dl[V4_CAP];
+  __shared__ float cd[V4_SCAP];
+  __shared__ int ci[V4_SCAP];
+  __shared__ int cnt;
+  const int64_t qq = blockIdx.x;
+  const int n = qcnt[qq];
+  if (n > V4_CAP || n < k) {   // overflow (fewer than k admitted rows cannot happen
+    if (threadIdx.x == 0) *flag = 1;   // when N >= k; kept as a guard)
+    return;
+  }
+  if (threadIdx.x == 0) cnt = 0;
+  const int* rl = rows + qq * V4_CAP;
+  const float* dq = dists + qq * V4_CAP;
+  for (int e = threadIdx.x; e < n; e += B4_T) dl[e] = dq[e];
+  __syncthreads();
+  const unsigned tk = block_select_kth<B4_T>(dl, n, k);   // upper edge of the k-th's bin
+  for (int e = threadIdx.x; e < n; e += B4_T)
+    if (__float_as_uint(dl[e]) <= tk) {
       const int pos = atomicAdd(&cnt, 1);
-      if (pos < V4_SCAP) { cd[pos] = dd[j]; ci[pos] = ri[j]; }
+      if (pos < V4_SCAP) { cd[pos] = dl[e]; ci[pos] = rl[e]; }
     }
   __syncthreads();
   const int nv = cnt;
@@ -755,12 +946,20 @@ __global__ __launch_bounds__(256) void rescore_kernel(const float* __restrict__ 
   }
   int n2 = 2;
   while (n2 < nv) n2 <<= 1;
-  for (int t = nv + threadIdx.x; t < n2; t += 256) { cd[t] = FLT_MAX; ci[t] = INT_MAX; }
+  for (int t = nv + threadIdx.x; t < n2; t += B4_T) { cd[t] = FLT_MAX; ci[t] = INT_MAX; }
   __syncthreads();
-  bitonic(cd, ci, n2);
-  for (int t = threadIdx.x; t < k; t += 256) {
-    idx[qq * k + t] = (int64_t)ci[t];
-    dist[qq * k + t] = cd[t];
+  bitonic<B4_T>(cd, ci, n2);
+  if constexpr (SMP) {
+    if (threadIdx.x == 0) {
+      const float kd = cd[k - 1];
+      thr0[qq] = kd < 2.5f ? kd + TH_MARGIN : FLT_MAX;
+      qcnt[qq] = 0;
+    }
+  } else {
+    for (int t = threadIdx.x; t < k; t += B4_T) {
+      idx[qq * k + t] = (int64_t)ci[t];
+      dist[qq * k + t] = cd[t];
+    }
   }
 }
 
@@ -1016,12 +1215,38 @@ void plan(int64_t N, int64_t Q, int k, int* nslices, int64_t* rows_per_slice) {
   *nslices = (int)cdiv(N, *rows_per_slice);
 }
 
+// The fit-time bf16 copy read by scan v4: out[r][c] = bf16(t[r][c] * inv[r])
+// (fp32 product, round to nearest even -- the rounding scan v4 otherwise
+// applies to the fp32 rows on the fly).  8 elements per thread, d % 8 == 0.
+__global__ void pack_rows_kernel(const float* __restrict__ t, const float* __restrict__ inv, int64_t N, int d,
+                                 bf16* __restrict__ out) {
+  const int64_t n8 = N * d / 8;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n8; e += (int64_t)gridDim.x * blockDim.x) {
+    const float iv = inv[e * 8 / d];
+    const float4 u = reinterpret_cast<const float4*>(t)[2 * e], v = reinterpret_cast<const float4*>(t)[2 * e + 1];
+    reinterpret_cast<bf16x8*>(out)[e] = bf16x8{(bf16)(u.x * iv), (bf16)(u.y * iv), (bf16)(u.z * iv), (bf16)(u.w * iv),
+                                               (bf16)(v.x * iv), (bf16)(v.y * iv), (bf16)(v.z * iv), (bf16)(v.w * iv)};
+  }
+}
+
 }  // namespace
 
 dcnr_status row_inv_norms(const float* t, int64_t N, int d, float* out, hipStream_t s) {
   if (N <= 0) return DCNR_OK;
   int64_t blocks = std::min<int64_t>(cdiv(N, 4), 8192);
   hipLaunchKernelGGL(inv_norm_kernel, dim3((unsigned)blocks), dim3(256), 0, s, t, N, d, out);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status cosine_pack_rows(const float* t, const float* inv, int64_t N, int d, bf16* out, hipStream_t s) {
+  if (d % 8) {
+    set_error("cosine_pack_rows: d=%d is not a multiple of 8", d);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  if (N <= 0) return DCNR_OK;
+  const int64_t blocks = std::min<int64_t>(cdiv(N * d / 8, 256), 8192);
+  hipLaunchKernelGGL(pack_rows_kernel, dim3((unsigned)blocks), dim3(256), 0, s, t, inv, N, d, out);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
@@ -1036,12 +1261,15 @@ void plan2(int64_t N, int* nslices, int64_t* rows_per_block) {
   *nslices = (int)cdiv(N, *rows_per_block);
 }
 
-bool use_v4(int64_t Q, int d, int k) { return use_v2(d, k) && Q >= V4_MIN_Q && d % 32 == 0; }
+bool use_v4(int64_t N, int64_t Q, int d, int k) {
+  return use_v2(d, k) && Q >= V4_MIN_Q && d % 32 == 0 && N > V4_S;
+}
 
 // v4 scratch after the v2 layout (cands | qn [Q][d] | thr0 [Q]): bf16
 // queries [Q][d] | per-query counts [Q] | flag | admitted rows [Q][V4_CAP]
+// | their exact distances [Q][V4_CAP]
 size_t v4_extra(int64_t Q, int d) {
-  return rup((size_t)Q * d * 2, 256) + rup((size_t)Q * 4 + 4, 256) + (size_t)Q * V4_CAP * 4 + 256;
+  return rup((size_t)Q * d * 2, 256) + rup((size_t)Q * 4 + 4, 256) + 2 * (size_t)Q * V4_CAP * 4 + 256;
 }
 
 size_t topk_ws_d(int64_t N, int64_t Q, int k, int d) {
@@ -1049,7 +1277,7 @@ size_t topk_ws_d(int64_t N, int64_t Q, int k, int d) {
   if (use_v2(d, k)) {
     plan2(N, &ns, &rps);
     const size_t v2 = rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4;
-    return use_v4(Q, d, k) ? rup(v2, 256) + v4_extra(Q, d) : v2;
+    return use_v4(N, Q, d, k) ? rup(v2, 256) + v4_extra(Q, d) : v2;
   }
   plan(N, Q, k, &ns, &rps);
   return (size_t)Q * ns * k * sizeof(Cand);
@@ -1075,9 +1303,9 @@ size_t topk_ws(int64_t N, int64_t Q, int k) {
   return std::max(topk_ws_d(N, Q, k, 64), (size_t)Q * ns * k * sizeof(Cand));
 }
 
-dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, const float* q,
-                        int64_t Q, int k, int64_t* idx, float* dist, void* ws, size_t ws_bytes,
-                        hipStream_t s) {
+dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_t N, int d,
+                        const float* q, int64_t Q, int k, int64_t* idx, float* dist, void* ws,
+                        size_t ws_bytes, hipStream_t s) {
   if (k < 1 || k > KMAX || d < 4 || d % 4 || d > 256 || N < 1) {
     set_error("cosine_topk: unsupported k=%d d=%d N=%lld (1<=k<=64, d%%4==0, d<=256)", k, d,
               (long long)N);
@@ -1093,65 +1321,77 @@ dcnr_status cosine_topk(const float* t, const float* inv, int64_t N, int d, cons
   if (use_v2(d, k)) {
     plan2(N, &ns, &rps);
     float* qn = (float*)((char*)ws + rup((size_t)Q * ns * k * sizeof(Cand), 256));
-    // normalised queries + admission bounds, one block per query
+    // normalised queries + admission bounds, one block per query (v4 makes
+    // its own, from a larger sample, below)
     float* thr0 = qn + Q * d;
-    switch (d / 4) {
+    const bool v4 = use_v4(N, Q, d, k);
+    bf16* qb = nullptr;
+    int *qcnt = nullptr, *gate = nullptr, *rows = nullptr;   // v4 scratch
+    float* dists = nullptr;
+    if (v4) {
+      char* x = (char*)ws + rup(rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4, 256);
+      qb = (bf16*)x;
+      x += rup((size_t)Q * d * 2, 256);
+      qcnt = (int*)x;
+      gate = qcnt + Q;   // v4: the exact scan v3 below runs only if v4 overflowed
+      x += rup((size_t)Q * 4 + 4, 256);
+      rows = (int*)x;
+      dists = (float*)(rows + Q * V4_CAP);
+    }
+    {   // (v4: also its bf16 queries, zeroed list counts and gate)
+      switch (d / 4) {
 #define CASEK(n)                                                                           \
   case n:                                                                                  \
     hipLaunchKernelGGL(kth_bound_kernel<n>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, \
-                       q, qn, k, thr0);                                                    \
+                       q, qn, k, thr0, qb, qcnt, gate);                                    \
     break;
-      CASEK(1) CASEK(2) CASEK(3) CASEK(4) CASEK(5) CASEK(6) CASEK(7) CASEK(8)
-      CASEK(9) CASEK(10) CASEK(11) CASEK(12) CASEK(13) CASEK(14) CASEK(15) CASEK(16)
+        CASEK(1) CASEK(2) CASEK(3) CASEK(4) CASEK(5) CASEK(6) CASEK(7) CASEK(8)
+        CASEK(9) CASEK(10) CASEK(11) CASEK(12) CASEK(13) CASEK(14) CASEK(15) CASEK(16)
 #undef CASEK
+      }
+      DCNR_LAUNCH_CHECK();
     }
-    DCNR_LAUNCH_CHECK();
-    int* gate = nullptr;   // v4: the exact scan v3 below runs only if v4 overflowed
-    if (use_v4(Q, d, k)) {
-      char* x = (char*)ws + rup(rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4, 256);
-      bf16* qb = (bf16*)x;
-      x += rup((size_t)Q * d * 2, 256);
-      int* qcnt = (int*)x;
-      gate = qcnt + Q;
-      x += rup((size_t)Q * 4 + 4, 256);
-      int* rows = (int*)x;
-      DCNR_HIP(hipMemsetAsync(gate, 0, 4, s));
-      switch (d / 32) {
-        case 1:
-          hipLaunchKernelGGL((kth_bound_kernel<8, V4_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv,
-                             N, q, qn, k, thr0, qb, qcnt);
-          break;
-        case 2:
-          hipLaunchKernelGGL((kth_bound_kernel<16, V4_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv,
-                             N, q, qn, k, thr0, qb, qcnt);
-          break;
+    if (v4) {
+      // pass 1 over the first V4_S rows under the 512-row bound (~2% of them
+      // admitted): their exact k-th distance -> thr0, the admission bound of
+      // pass 2 over the whole table (~k / V4_S of it admitted)
+      constexpr int RPB_S = 64;   // one row tile per wave: the sample pass is latency-bound
+      const dim3 gs((unsigned)cdiv(V4_S, RPB_S), (unsigned)cdiv(Q, 32));
+#define SCAN4(ks, nq, pk, g, n, rpb)                                                                    \
+  hipLaunchKernelGGL((scan4_kernel<ks, nq, pk>), g, dim3(256), 0, s, t, inv, tb, n, rpb, qb, thr0, qn, \
+                     Q, qcnt, rows, dists, gate)
+      if (d == 32) {
+        if (tb) SCAN4(1, 2, true, gs, (int64_t)V4_S, RPB_S);
+        else SCAN4(1, 2, false, gs, (int64_t)V4_S, RPB_S);
+      } else {
+        if (tb) SCAN4(2, 2, true, gs, (int64_t)V4_S, RPB_S);
+        else SCAN4(2, 2, false, gs, (int64_t)V4_S, RPB_S);
       }
       DCNR_LAUNCH_CHECK();
-      const dim3 g4((unsigned)cdiv(N, V4_RPB), (unsigned)cdiv(Q, V4_QC));
-      if (d == 32)
-        hipLaunchKernelGGL(scan4_kernel<1>, g4, dim3(256), 0, s, t, inv, N, qb, thr0, Q, qcnt, rows, gate);
-      else
-        hipLaunchKernelGGL(scan4_kernel<2>, g4, dim3(256), 0, s, t, inv, N, qb, thr0, Q, qcnt, rows, gate);
+      hipLaunchKernelGGL((rescore_kernel<true>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k,
+                         nullptr, nullptr, gate, thr0);
       DCNR_LAUNCH_CHECK();
-      if (d == 32)
-        hipLaunchKernelGGL(rescore_kernel<8>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, qn, qcnt, rows,
-                           k, idx, dist, gate);
-      else
-        hipLaunchKernelGGL(rescore_kernel<16>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, qn, qcnt,
-                           rows, k, idx, dist, gate);
+      // query blocks of 16: NQB per launch row (the table is read once per
+      // NQB * 16 queries)
+      const int nqb = (int)std::min<int64_t>(cdiv(Q, 16), V4_QC / 16);
+      const int NQ = nqb <= 2 ? 2 : nqb <= 4 ? 4 : nqb <= 8 ? 8 : 16;
+      const dim3 g4((unsigned)cdiv(N, V4_RPB), (unsigned)cdiv(Q, NQ * 16));
+#define CASE4(ks, nq)                                                 \
+  if (d == 32 * ks && NQ == nq) {                                     \
+    if (tb) SCAN4(ks, nq, true, g4, N, V4_RPB);                       \
+    else SCAN4(ks, nq, false, g4, N, V4_RPB);                         \
+  }
+      CASE4(1, 2) CASE4(1, 4) CASE4(1, 8) CASE4(1, 16)
+      CASE4(2, 2) CASE4(2, 4) CASE4(2, 8) CASE4(2, 16)
+#undef CASE4
+#undef SCAN4
       DCNR_LAUNCH_CHECK();
-      // the exact fallback below needs the v2 admission bound (512-row sample)
-      switch (d / 32) {
-        case 1:
-          hipLaunchKernelGGL((kth_bound_kernel<8, TH_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv,
-                             N, q, qn, k, thr0, nullptr, nullptr);
-          break;
-        case 2:
-          hipLaunchKernelGGL((kth_bound_kernel<16, TH_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv,
-                             N, q, qn, k, thr0, nullptr, nullptr);
-          break;
-      }
+      hipLaunchKernelGGL((rescore_kernel<false>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k,
+                         idx, dist, gate, nullptr);
       DCNR_LAUNCH_CHECK();
+      // (the exact fallback below admits rows under the same thr0: an upper
+      // bound on every query's k-th best -- the sample's, or the 512-row one
+      // if pass 1 overflowed)
     }
     if (Q >= MFMA_MIN_Q && d % 16 == 0) {
       const int qtiles = (int)cdiv(Q, K3_QT);

@@ -84,6 +84,9 @@ _SIGS = {
     "dcnr_cosine_topk_workspace_size": (ctypes.c_size_t, [_I64, _I64, ctypes.c_int32]),
     "dcnr_cosine_topk": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, _P, _I64, ctypes.c_int32,
                                         _P, _P, _P, ctypes.c_size_t, _P]),
+    "dcnr_cosine_pack_rows": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, _P, _P]),
+    "dcnr_cosine_topk_packed": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.c_int32, _P, _I64,
+                                               ctypes.c_int32, _P, _P, _P, ctypes.c_size_t, _P]),
     "dcnr_topk_merge": (ctypes.c_int, [_P, _P, ctypes.c_int32, _I64, ctypes.c_int32, _P, _P, _P]),
     "dcnr_gather_rows": (ctypes.c_int, [_P, _I64, _I64, ctypes.c_int32, _P, _P, _P, _P]),
     "dcnr_candidate_union": (ctypes.c_int, [_P, _I64, _P, ctypes.c_int32, _P, _P, _P]),

@@ -16,6 +16,11 @@ import torch
 
 from . import _lib
 
+# the batched scan (knn.hip scan v4) serves d = 32 / 64 over tables larger
+# than its 8192-row sample; only those get the fit-time bf16 copy
+PACKED_D = (32, 64)
+PACKED_MIN_ROWS = 8192
+
 
 class NearestNeighbors:
     def __init__(self, n_neighbors=5, metric='cosine', algorithm='brute', device='cuda'):
@@ -30,6 +35,7 @@ class NearestNeighbors:
         self.device = torch.device(device)
         self._table = None
         self._inv = None
+        self._packed = None
 
     def fit(self, X, y=None):
         t = torch.as_tensor(np.asarray(X, dtype=np.float32) if not torch.is_tensor(X) else X)
@@ -43,6 +49,15 @@ class NearestNeighbors:
         lib = _lib.load()
         _lib.check(lib.dcnr_row_inv_norms(t.data_ptr(), t.shape[0], t.shape[1], self._inv.data_ptr(),
                                           _lib.stream_ptr(self.device)), "dcnr_row_inv_norms")
+        self._packed = None
+        if t.shape[1] in PACKED_D and t.shape[0] > PACKED_MIN_ROWS:
+            # bf16 copy of the normalised rows for the batched coarse scan
+            # (2 B / element beside the fp32 table; same results without it)
+            self._packed = torch.empty(t.shape, dtype=torch.int16, device=self.device)
+            _lib.check(lib.dcnr_cosine_pack_rows(t.data_ptr(), self._inv.data_ptr(), t.shape[0],
+                                                 t.shape[1], self._packed.data_ptr(),
+                                                 _lib.stream_ptr(self.device)),
+                       "dcnr_cosine_pack_rows")
         self.n_samples_fit_ = t.shape[0]
         self.n_features_in_ = t.shape[1]
         return self
@@ -61,9 +76,11 @@ class NearestNeighbors:
         dist = torch.empty((Q, k), dtype=torch.float32, device=self.device)
         nb = int(lib.dcnr_cosine_topk_workspace_size(N, Q, k))
         ws = torch.empty(max(nb, 16), dtype=torch.uint8, device=self.device)
-        _lib.check(lib.dcnr_cosine_topk(self._table.data_ptr(), self._inv.data_ptr(), N, d,
-                                        q.data_ptr(), Q, k, idx.data_ptr(), dist.data_ptr(),
-                                        ws.data_ptr(), ws.numel(), _lib.stream_ptr(self.device)),
+        packed = self._packed.data_ptr() if self._packed is not None else None
+        _lib.check(lib.dcnr_cosine_topk_packed(self._table.data_ptr(), self._inv.data_ptr(), packed,
+                                               N, d, q.data_ptr(), Q, k, idx.data_ptr(),
+                                               dist.data_ptr(), ws.data_ptr(), ws.numel(),
+                                               _lib.stream_ptr(self.device)),
                    "dcnr_cosine_topk")
         return dist, idx
 

@@ -254,6 +254,23 @@ dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t
                              const float* queries, int64_t Q, int32_t k, int64_t* idx,
                              float* dist, void* ws, size_t ws_bytes, dcnr_stream_t stream);
 
+/* Fit-time bf16 copy of the normalised table for the batched scan:
+ * packed[r][c] = bf16(table[r][c] * inv_norms[r]) (fp32 product, round to
+ * nearest even), uint16 [N,d], d % 8 == 0.  Optional: 2 bytes per element
+ * resident beside the fp32 table halve the batched (Q >= 16, d = 32 or 64)
+ * scan's HBM stream; results are identical with or without it.  Part of
+ * NearestNeighbors.fit (main.py:268-270) -- sklearn keeps its own copy of
+ * the fitted data there too. */
+dcnr_status dcnr_cosine_pack_rows(const float* table, const float* inv_norms, int64_t N, int32_t d,
+                                  uint16_t* packed, dcnr_stream_t stream);
+
+/* dcnr_cosine_topk reading `packed` (from dcnr_cosine_pack_rows over the same
+ * table, or NULL) for its coarse bf16 scan; same results, same workspace. */
+dcnr_status dcnr_cosine_topk_packed(const float* table, const float* inv_norms, const uint16_t* packed,
+                                    int64_t N, int32_t d, const float* queries, int64_t Q, int32_t k,
+                                    int64_t* idx, float* dist, void* ws, size_t ws_bytes,
+                                    dcnr_stream_t stream);
+
 /* Merge of row-sharded top-k lists (the cfg5 index split over ranks, SURVEY
  * 8(e)): dist fp32 / idx int64 [lists][Q][k] (global rows; padding entries
  * (FLT_MAX, -1) sort last) -> the k best per query, ascending by (dist, row),

@@ -462,6 +462,37 @@ def test_cosine_knn_full_size(dev, Q, d):
         np.testing.assert_array_equal(i[r][isolated], ref_i[r][isolated])
 
 
+@pytest.mark.parametrize("d", [32, 64])
+def test_cosine_pack_rows_and_packed_scan(dev, d):
+    """dcnr_cosine_pack_rows = bf16(x * inv_norm) bit for bit (torch's
+    round-to-nearest-even cast of the same fp32 product), and the top-k read
+    through the packed copy equals the top-k without it, bit for bit, for
+    every query-batch shape scan v4 dispatches (NQB 2 .. 16, a partial tail)."""
+    import dcnr
+    from dcnr import _lib
+    g = torch.Generator(device=dev).manual_seed(40 + d)
+    table = torch.randn(300_000, d, device=dev, generator=g)
+    table[7] = 0.0   # zero row: inv norm 1 (sklearn's normalize)
+    nn_ = dcnr.NearestNeighbors(metric="cosine").fit(table)
+    assert nn_._packed is not None
+    ref = (table * nn_._inv[:, None]).to(torch.bfloat16).view(torch.int16)
+    assert torch.equal(nn_._packed, ref)
+    for Q in (16, 50, 128, 256, 300):
+        q = torch.randn(Q, d, device=dev, generator=g)
+        dp, ip = nn_.kneighbors_device(q, 11)
+        packed, nn_._packed = nn_._packed, None
+        try:
+            du, iu = nn_.kneighbors_device(q, 11)
+        finally:
+            nn_._packed = packed
+        assert torch.equal(ip, iu), Q
+        assert torch.equal(dp, du), Q
+    lib = _lib.load()
+    bad = torch.empty((10, 12), dtype=torch.int16, device=dev)
+    assert lib.dcnr_cosine_pack_rows(table.data_ptr(), nn_._inv.data_ptr(), 10, 12, bad.data_ptr(),
+                                     _lib.stream_ptr(dev)) != 0   # d % 8 != 0
+
+
 def test_cosine_knn_v4_overflow_falls_back_exact(dev):
     """More than V4_CAP rows inside one query's admission bound (12000 rows
     on the query's own direction, every one at distance 0): scan v4's list
