@@ -572,14 +572,20 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 // V4_SCAP rows) raises a flag and the exact scan v3 + merge, launched behind
 // it and gated on the flag, recomputes the batch.
 constexpr float V4_EPS = 0.004f;
-constexpr int V4_S = 8192;       // exact sample rows for the admission bound
+#ifndef V4_S_OVR
+#define V4_S_OVR 32768
+#endif
+constexpr int V4_S = V4_S_OVR;   // exact sample rows for the admission bound
 constexpr int V4_CAP = 4096;     // admitted rows per query
 constexpr int V4_SCAP = 256;     // rows at or under the selected k-th bin
 constexpr int V4_QC = 256;       // queries per block (LDS: V4_QC x d bf16)
 #ifndef V4_RPB_OVR
-#define V4_RPB_OVR 512
+#define V4_RPB_OVR 0
 #endif
-constexpr int V4_RPB = V4_RPB_OVR;   // table rows per block
+// table rows per block: few query blocks -> long blocks (the per-block
+// prologue and epilogue amortised; measured 69 vs 78 us at Q = 32), many ->
+// short ones (a wave's list fill grows with rows x queries)
+constexpr int v4_rpb(int nqb) { return V4_RPB_OVR ? V4_RPB_OVR : nqb <= 4 ? 2048 : 512; }
 #ifndef V4_MIN_Q
 #define V4_MIN_Q 16
 #endif
@@ -682,10 +688,13 @@ constexpr int V4_WL = V4_LIST / 4;   // ... per wave
 #endif
 #ifndef V4_LAB                   // lab ablations (tools/knn_lab.sh), 0 in the library:
 #define V4_LAB 0                 // 1 no admission checks, 2 B fragments not re-read
-#endif                           // from LDS, 4 no epilogue distances
+#endif                           // from LDS, 4 no epilogue distances, 8 only the
+                                 // per-block any-ballot (no per-row checks)
 
+// (NQB > 4: at least 3 waves per SIMD -- left alone the compiler unrolled
+// its way to 284 registers and one wave per SIMD, 1.7x slower)
 template <int KS, int NQB, bool PK>
-__global__ __launch_bounds__(256) void scan4_kernel(const float* __restrict__ tab,
+__global__ __launch_bounds__(256, NQB > 4 ? 3 : 1) void scan4_kernel(const float* __restrict__ tab,
                                                     const float* __restrict__ inv,
                                                     const bf16* __restrict__ tb, int64_t N, int rpb,
                                                     const bf16* __restrict__ qb,
@@ -714,7 +723,7 @@ __global__ __launch_bounds__(256) void scan4_kernel(const float* __restrict__ ta
   // ring, static indices): fp32 rows scaled and rounded here, or (PK) the
   // fit-time bf16 copy loaded as is.  The first PF loads go out before the
   // query fragments are staged.
-  constexpr int PF = PK ? V4_PF : 2;
+  constexpr int PF = PK && NQB <= 4 ? V4_PF : 2;
   using Frag = typename std::conditional<PK, bf16x8[KS], float4[KS][2]>::type;
   Frag x[PF];
   float iv[PF];
@@ -754,7 +763,9 @@ __global__ __launch_bounds__(256) void scan4_kernel(const float* __restrict__ ta
       }
     }
     const float t = thr0[qs];
-    th[b] = qi < nq ? t + V4_EPS : -1.f;
+    // a row passes iff its coarse cosine is >= 1 - bound; the 1e-6 below
+    // covers the rounding of 1 - bound (query slots past nq: 2, never)
+    th[b] = qi < nq ? (1.f - (t + V4_EPS)) - 1e-6f : 2.f;
   }
   if constexpr (BL) {
     constexpr int PER = NQB * KS * 64 / 256;
@@ -790,9 +801,11 @@ __global__ __launch_bounds__(256) void scan4_kernel(const float* __restrict__ ta
       // every query block's MFMAs first, back to back (interleaving each
       // block's admission checks serialised LDS read -> MFMA -> result ->
       // ballot per block: 146 us for 256 queries), then one ballot per block
-      // on the best of its 4 rows -- almost always empty -- before the
-      // per-row ones.  Query slots past nq have zero fragments and bound -1:
-      // never pass.
+      // on the best of its 4 rows -- usually empty -- before the per-row
+      // ones.  The accumulators start at bound - 1, so a check is a sign
+      // test: with |coarse - exact| <= 2^-8 + 2^-16 + fp32 accumulation error
+      // (< 1e-5 here) against V4_EPS = 0.004 the admitted set still contains
+      // every row whose exact distance is <= the bound.
       // (LDS fragments: block b + 1's read is issued before block b's MFMAs)
       f32x4 acc[NQB];
       bf16x8 nb[KS];
@@ -821,19 +834,28 @@ __global__ __launch_bounds__(256) void scan4_kernel(const float* __restrict__ ta
         for (int b = 0; b < NQB; ++b) labsink += acc[b][0] + acc[b][3];
         continue;
       }
+      const bool full = base + 16 <= r1;   // (wave-uniform) no row of the tile past r1
+      const int rb = (int)base + 4 * g;
 #pragma unroll
       for (int b = 0; b < NQB; ++b) {
-        // lane (c = r16, g): rows base + 4g + i, query 16 b + c
+        // lane (c = r16, g): rows rb + i, query 16 b + c
         const float mx = fmaxf(fmaxf(acc[b][0], acc[b][1]), fmaxf(acc[b][2], acc[b][3]));
-        if (!__ballot(1.f - mx <= th[b])) continue;   // 1 - x is monotone: min over the 4 rows
+        if (!__ballot(mx >= th[b])) continue;
+        if constexpr ((V4_LAB & 8) != 0) { ++wc; continue; }
+        // one block adds at most 256 entries: room is checked once here (a
+        // full list reads as overflowed, and the batch takes the exact path)
+        if (wc > V4_WL - 256) { wc = V4_WL + 1; continue; }
+        int* lqw = lq + w * V4_WL;
+        int* lrw = lr + w * V4_WL;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const bool pass = base + 4 * g + i < r1 && 1.f - acc[b][i] <= th[b];
+          const bool pass = acc[b][i] >= th[b] && (full || rb + i < r1);
           const uint64_t m = __ballot(pass);
           if (pass) {
             const int p = wc + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-            if (p < V4_WL) { lq[w * V4_WL + p] = 16 * b + r16; lr[w * V4_WL + p] = (int)(base + 4 * g + i); }
+            lqw[p] = 16 * b + r16;
+            lrw[p] = rb + i;
           }
           wc += __popcll(m);
         }
@@ -1375,11 +1397,12 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       // NQB * 16 queries)
       const int nqb = (int)std::min<int64_t>(cdiv(Q, 16), V4_QC / 16);
       const int NQ = nqb <= 2 ? 2 : nqb <= 4 ? 4 : nqb <= 8 ? 8 : 16;
-      const dim3 g4((unsigned)cdiv(N, V4_RPB), (unsigned)cdiv(Q, NQ * 16));
+      const int rpb = v4_rpb(NQ);
+      const dim3 g4((unsigned)cdiv(N, rpb), (unsigned)cdiv(Q, NQ * 16));
 #define CASE4(ks, nq)                                                 \
   if (d == 32 * ks && NQ == nq) {                                     \
-    if (tb) SCAN4(ks, nq, true, g4, N, V4_RPB);                       \
-    else SCAN4(ks, nq, false, g4, N, V4_RPB);                         \
+    if (tb) SCAN4(ks, nq, true, g4, N, rpb);                          \
+    else SCAN4(ks, nq, false, g4, N, rpb);                            \
   }
       CASE4(1, 2) CASE4(1, 4) CASE4(1, 8) CASE4(1, 16)
       CASE4(2, 2) CASE4(2, 4) CASE4(2, 8) CASE4(2, 16)

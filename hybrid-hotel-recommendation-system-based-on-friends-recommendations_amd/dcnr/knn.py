@@ -17,9 +17,9 @@ import torch
 from . import _lib
 
 # the batched scan (knn.hip scan v4) serves d = 32 / 64 over tables larger
-# than its 8192-row sample; only those get the fit-time bf16 copy
+# than its 32768-row sample; only those get the fit-time bf16 copy
 PACKED_D = (32, 64)
-PACKED_MIN_ROWS = 8192
+PACKED_MIN_ROWS = 32768
 
 
 class NearestNeighbors:

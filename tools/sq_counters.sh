@@ -4,6 +4,8 @@
 # short bench.py run (8 SQ + 1 GRBM counters each), then tools/sq_summary.py
 # reduces them per kernel.  On the GPU box, from the repo root:
 #   bash tools/sq_counters.sh r03a
+# SQ_PROG overrides the program (default: a short bench.py run), e.g.
+#   SQ_PROG="tools/knn_lab.py" bash tools/sq_counters.sh r03q
 set -o pipefail
 R=${1:-r03}
 OUT=gpurun_out/$R/sq
@@ -16,6 +18,6 @@ i=0
 for P in "$P1" "$P2"; do
   i=$((i+1))
   timeout -s KILL 240 rocprofv3 --pmc $P --kernel-trace --output-format csv -d $OUT/p$i -o run -- \
-      python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || exit 1
+      python3 ${SQ_PROG:-bench.py $ARGS} > $OUT/p$i.log 2>&1 || exit 1
 done
 python3 tools/sq_summary.py $OUT > gpurun_out/$R/sq_counters.txt

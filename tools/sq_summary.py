@@ -34,6 +34,10 @@ GROUPS = [
     ("gather_cross", r"gather_cross"),
     ("emb_runs", r"emb_runs"),
     ("adam", r"adam_kernel"),
+    ("knn scan4<2,16> (256 queries)", r"scan4_kernel<2, 16"),
+    ("knn scan4<2,2> (<= 32 queries)", r"scan4_kernel<2, 2,"),
+    ("knn rescore", r"rescore_kernel"),
+    ("knn scan3", r"scan3_kernel"),
 ]
 
 
