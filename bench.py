@@ -277,30 +277,24 @@ def bench_cfg5(dev, iters, cpu):
         t = ms / cnt / 1e3
         out[f"topk_q{Q}_us"] = t * 1e6
         out[f"topk_q{Q}_queries_per_sec"] = Q / t
-        if Q == 1:
-            out["roofline"] = {"bound": "hbm", "kernel": "scan2_kernel + merge (dcnr_cosine_topk, Q=1)",
-                               "achieved": table_bytes / t / 1e9, "peak": PEAK_HBM / 1e9,
-                               "unit": "GB/s", "frac": table_bytes / t / PEAK_HBM,
-                               "bytes_per_call": table_bytes}
-        else:
-            # the batched path streams the fit-time bf16 copy of the
-            # normalised table (2 B / element, dcnr_cosine_pack_rows) once per
-            # call; the scoring is 2 N Q d FLOP (bf16 MFMA coarse pass + exact
-            # fp32 rescoring of the few admitted rows -- their row gathers,
-            # ~Q x 1.3k x 260 B, are not counted as algorithmic bytes): the
-            # MFMA time is below the HBM time, so HBM bounds the call.
-            # fp32_mfma_floor_us: the same FLOP at the fp32 MFMA peak (the
-            # bound of an all-fp32 scan)
-            flop = 2.0 * n_items * Q * 64
-            packed = pipe.index._packed is not None
-            nbytes = n_items * 64 * 2 if packed else table_bytes
-            out[f"roofline_q{Q}"] = {
-                "bound": "hbm", "kernel": "kth_bound + scan4 (bf16 MFMA%s) + rescore (dcnr_cosine_topk)"
-                % (" over the fit-time bf16 copy" if packed else ""),
-                "achieved": nbytes / t / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
-                "frac": nbytes / t / PEAK_HBM, "bytes_per_call": nbytes,
-                "floor_us": max(nbytes / PEAK_HBM, flop / PEAK_BF16) * 1e6,
-                "flop_per_call": flop, "fp32_mfma_floor_us": flop / 157.3e12 * 1e6}
+        # the batched path (scan v4, every Q here) streams the fit-time bf16
+        # copy of the normalised table (2 B / element, dcnr_cosine_pack_rows)
+        # once per call; the scoring is 2 N Q d FLOP (bf16 MFMA coarse pass +
+        # exact fp32 rescoring of the few admitted rows -- their row gathers,
+        # ~Q x 400 x 260 B, are not counted as algorithmic bytes): the MFMA
+        # time is below the HBM time, so HBM bounds the call.
+        # fp32_mfma_floor_us: the same FLOP at the fp32 MFMA peak (the bound
+        # of an all-fp32 scan)
+        flop = 2.0 * n_items * Q * 64
+        packed = pipe.index._packed is not None
+        nbytes = n_items * 64 * 2 if packed else table_bytes
+        out["roofline" if Q == 1 else f"roofline_q{Q}"] = {
+            "bound": "hbm", "kernel": "kth_bound + scan4 (bf16 MFMA%s) + rescore (dcnr_cosine_topk, Q=%d)"
+            % (" over the fit-time bf16 copy" if packed else "", Q),
+            "achieved": nbytes / t / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
+            "frac": nbytes / t / PEAK_HBM, "bytes_per_call": nbytes,
+            "floor_us": max(nbytes / PEAK_HBM, flop / PEAK_BF16) * 1e6,
+            "flop_per_call": flop, "fp32_mfma_floor_us": flop / 157.3e12 * 1e6}
     users = torch.randint(0, 1_000_000, (iters,), generator=g, device=dev).tolist()
     pos = [torch.randint(0, n_items, (32,), generator=g, device=dev) for _ in range(iters)]
     for k in range(2):

@@ -552,7 +552,7 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------- scan v4
-// Batched queries (Q >= V4_MIN_Q, d = 32 or 64): bf16-MFMA coarse scoring of
+// Every query count (Q >= V4_MIN_Q; d = 32 or 64, N > V4_S): bf16-MFMA coarse scoring of
 // every (row, query) pair + exact fp32 re-scoring of the rows it admits.
 //
 // The coarse cosine is sum_i bf16(x_i * inv_r) * bf16(q_i / |q|), fp32
@@ -587,7 +587,7 @@ constexpr int V4_QC = 256;       // queries per block (LDS: V4_QC x d bf16)
 // short ones (a wave's list fill grows with rows x queries)
 constexpr int v4_rpb(int nqb) { return V4_RPB_OVR ? V4_RPB_OVR : nqb <= 4 ? 2048 : 512; }
 #ifndef V4_MIN_Q
-#define V4_MIN_Q 16
+#define V4_MIN_Q 1   // from Q = 1: 60-66 us for Q <= 8 against 65-98 on scan v2
 #endif
 
 // k-th smallest of n distances (>= 0) held in LDS, by a 2-pass radix select
@@ -1416,7 +1416,7 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       // bound on every query's k-th best -- the sample's, or the 512-row one
       // if pass 1 overflowed)
     }
-    if (Q >= MFMA_MIN_Q && d % 16 == 0) {
+    if (v4 || (Q >= MFMA_MIN_Q && d % 16 == 0)) {   // (v4: its gated exact fallback, any Q)
       const int qtiles = (int)cdiv(Q, K3_QT);
       const int64_t blocks = rup(ns, 8) * qtiles;
       switch (d / 16) {

@@ -437,10 +437,10 @@ def test_cosine_knn_vs_sklearn_golden(dev):
 
 @pytest.mark.parametrize("Q,d", [(1, 64), (3, 64), (8, 64), (32, 64), (256, 64), (64, 32)])
 def test_cosine_knn_full_size(dev, Q, d):
-    """configs[4] size: cosine top-11 over 1M x d (VALU scan for Q < 16; from
-    Q = 16 the bf16-MFMA coarse scan + exact fp32 rescoring of its admitted
-    rows, knn.hip scan v4) against a brute-force torch fp32 reference on the
-    device (random table: no ties)."""
+    """configs[4] size: cosine top-11 over 1M x d (the bf16-MFMA coarse scan
+    + exact fp32 rescoring of its admitted rows, knn.hip scan v4, for every Q)
+    against a brute-force torch fp32 reference on the device (random table:
+    no ties)."""
     import dcnr
     g = torch.Generator(device=dev).manual_seed(11 + Q + d)
     table = torch.randn(1_000_000, d, device=dev, generator=g)
