@@ -104,6 +104,15 @@ namespace {
     if (st_ != DCNR_OK) return st_;          \
   } while (0)
 
+// Flags of the fork/join events between the caller's stream and the side
+// stream (both on this device: a device-scope release/acquire orders them;
+// without the system-scope fence the step measured 4.019 vs 4.051 ms,
+// alternating A/B x3 on one box, profiles/lab/r03x_event_fence_ab.txt).
+#ifndef DCNR_EV_NOFENCE
+#define DCNR_EV_NOFENCE 1
+#endif
+constexpr unsigned SYNC_EV = hipEventDisableTiming | (DCNR_EV_NOFENCE ? hipEventDisableSystemFence : 0u);
+
 // One side stream per device (created on first use, never destroyed) for the
 // backward's work that does not depend on the deep tower; fork/join events
 // per call.
@@ -131,8 +140,8 @@ struct SideJoin {
   bool recorded = false, joined = false;
   dcnr_status fork(hipStream_t s) {
     TRY(side_stream(&side));
-    DCNR_HIP(hipEventCreateWithFlags(&fork_ev, hipEventDisableTiming));
-    DCNR_HIP(hipEventCreateWithFlags(&join_ev, hipEventDisableTiming));
+    DCNR_HIP(hipEventCreateWithFlags(&fork_ev, SYNC_EV));
+    DCNR_HIP(hipEventCreateWithFlags(&join_ev, SYNC_EV));
     DCNR_HIP(hipEventRecord(fork_ev, s));
     DCNR_HIP(hipStreamWaitEvent(side, fork_ev, 0));
     main = s;
@@ -150,7 +159,7 @@ struct SideJoin {
   }
   // an intermediate point of the side stream's work that `s` waits for alone
   dcnr_status mark() {
-    DCNR_HIP(hipEventCreateWithFlags(&mark_ev, hipEventDisableTiming));
+    DCNR_HIP(hipEventCreateWithFlags(&mark_ev, SYNC_EV));
     DCNR_HIP(hipEventRecord(mark_ev, side));
     return DCNR_OK;
   }
@@ -642,9 +651,9 @@ struct DwPipe {
   bool pending = false;   // side work enqueued since the last join
   dcnr_status init(hipStream_t side_stream) {
     side = side_stream;
-    DCNR_HIP(hipEventCreateWithFlags(&in_ev, hipEventDisableTiming));
-    DCNR_HIP(hipEventCreateWithFlags(&dw_ev, hipEventDisableTiming));
-    DCNR_HIP(hipEventCreateWithFlags(&done_ev, hipEventDisableTiming));
+    DCNR_HIP(hipEventCreateWithFlags(&in_ev, SYNC_EV));
+    DCNR_HIP(hipEventCreateWithFlags(&dw_ev, SYNC_EV));
+    DCNR_HIP(hipEventCreateWithFlags(&done_ev, SYNC_EV));
     return DCNR_OK;
   }
   // order the side stream after the main stream's work so far (and the main
