@@ -493,6 +493,56 @@ def test_cosine_pack_rows_and_packed_scan(dev, d):
                                      _lib.stream_ptr(dev)) != 0   # d % 8 != 0
 
 
+@pytest.mark.parametrize("d,k", [(64, 32), (32, 11), (64, 1), (64, 64)])
+def test_cosine_knn_v4_ties_zero_rows_and_kmax(dev, d, k):
+    """Scan v4 edge cases (ties, nulls, maximum k): 40 exact
+    copies of row 5 scattered over the table (one distance for all 41, so
+    ordered by row index), all-zero rows (sklearn's normalize leaves them
+    zero: distance 1 to every query), a zero query (distance 1 to every row:
+    the k lowest rows; its list overflows scan v4 and takes the exact path),
+    k up to v4's 32 and KMAX = 64 (the exact scan); the rest of every list
+    against a torch fp32 brute force."""
+    import dcnr
+    g = torch.Generator(device=dev).manual_seed(77 + d + k)
+    N = 120_000
+    table = torch.randn(N, d, device=dev, generator=g)
+    dup = torch.randperm(N, device=dev, generator=g)[:40]
+    dup = dup[dup != 5]
+    table[dup] = table[5].clone()
+    zero = torch.randperm(N, device=dev, generator=g)[:25]
+    zero = zero[(zero != 5) & ~torch.isin(zero, dup)]
+    table[zero] = 0.0
+    nn_ = dcnr.NearestNeighbors(metric="cosine").fit(table)
+    q = torch.cat([table[5:6] * 3.0, torch.randn(6, d, device=dev, generator=g)])
+    dist_, idx = nn_.kneighbors_device(q, k)
+    dist_, idx = dist_.cpu().numpy(), idx.cpu().numpy()
+    # query 0: the 41 rows on its direction first, ascending rows, one distance
+    ties = np.sort(np.concatenate([[5], dup.cpu().numpy()]))
+    m = min(k, ties.size)
+    assert idx[0][:m].tolist() == ties[:m].tolist()
+    assert np.all(dist_[0][:m] == dist_[0][0]) and dist_[0][0] <= 2e-6
+    # random queries: against torch fp32 (zero rows at distance 1)
+    tn = table / table.norm(dim=1, keepdim=True).clamp_min(1e-30)
+    qn = q[1:] / q[1:].norm(dim=1, keepdim=True)
+    ref_d, ref_i = torch.topk((1.0 - qn @ tn.T).clamp(0, 2), k, dim=1, largest=False)
+    ref_d, ref_i = ref_d.cpu().numpy(), ref_i.cpu().numpy()
+    np.testing.assert_allclose(dist_[1:], ref_d, rtol=0, atol=2e-6)
+    for r in range(ref_d.shape[0]):
+        near = np.diff(ref_d[r]) <= 2e-6
+        iso = np.ones(k, bool)
+        iso[1:] &= ~near
+        iso[:-1] &= ~near
+        np.testing.assert_array_equal(idx[1 + r][iso], ref_i[r][iso])
+    # every list sorted by (distance, row)
+    for r in range(idx.shape[0]):
+        key = list(zip(dist_[r].tolist(), idx[r].tolist()))
+        assert key == sorted(key)
+    # the zero query: every distance is 1 -> rows 0 .. k-1
+    dz, iz = nn_.kneighbors_device(torch.zeros(1, d, device=dev), k)
+    assert iz.cpu().numpy()[0].tolist() == list(range(k))
+    assert np.all(dz.cpu().numpy() == 1.0)
+
+
 def test_cosine_knn_v4_overflow_falls_back_exact(dev):
     """More than V4_CAP rows inside one query's admission bound (12000 rows
     on the query's own direction, every one at distance 0): scan v4's list
