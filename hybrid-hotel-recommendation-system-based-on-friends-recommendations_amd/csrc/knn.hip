@@ -576,6 +576,12 @@ constexpr float V4_EPS = 0.004f;
 #define V4_S_OVR 32768
 #endif
 constexpr int V4_S = V4_S_OVR;   // exact sample rows for the admission bound
+#ifndef V4_TH_S
+#define V4_TH_S 512              // rows of the first bound (kth_bound_kernel) on the v4 path
+#endif
+#ifndef V4_SNQ
+#define V4_SNQ 16                // query blocks per launch row of the sample pass (Q=256: 31 vs 43 us at 2)
+#endif
 constexpr int V4_CAP = 4096;     // admitted rows per query
 constexpr int V4_SCAP = 256;     // rows at or under the selected k-th bin
 constexpr int V4_QC = 256;       // queries per block (LDS: V4_QC x d bf16)
@@ -1360,7 +1366,15 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       rows = (int*)x;
       dists = (float*)(rows + Q * V4_CAP);
     }
-    {   // (v4: also its bf16 queries, zeroed list counts and gate)
+    if (v4 && V4_TH_S != TH_S) {   // v4's pass-1 bound from a larger first sample
+      if (d == 32)
+        hipLaunchKernelGGL((kth_bound_kernel<8, V4_TH_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, q, qn,
+                           k, thr0, qb, qcnt, gate);
+      else
+        hipLaunchKernelGGL((kth_bound_kernel<16, V4_TH_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, q,
+                           qn, k, thr0, qb, qcnt, gate);
+      DCNR_LAUNCH_CHECK();
+    } else {   // (v4: also its bf16 queries, zeroed list counts and gate)
       switch (d / 4) {
 #define CASEK(n)                                                                           \
   case n:                                                                                  \
@@ -1374,38 +1388,37 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       DCNR_LAUNCH_CHECK();
     }
     if (v4) {
+      // query blocks of 16: NQB per launch row (the table is read once per
+      // NQB * 16 queries); the sample pass takes at most V4_SNQ of them
+      const int nqb = (int)std::min<int64_t>(cdiv(Q, 16), V4_QC / 16);
+      const int NQ = nqb <= 2 ? 2 : nqb <= 4 ? 4 : nqb <= 8 ? 8 : 16;
+      const int NQS = std::min(NQ, V4_SNQ);
+      constexpr int RPB_S = 64;   // one row tile per wave: the sample pass is latency-bound
+      const dim3 gs((unsigned)cdiv(V4_S, RPB_S), (unsigned)cdiv(Q, NQS * 16));
+      const int rpb = v4_rpb(NQ);
+      const dim3 g4((unsigned)cdiv(N, rpb), (unsigned)cdiv(Q, NQ * 16));
+#define SCAN4(ks, nq, pk, g, n, rp)                                                                    \
+  hipLaunchKernelGGL((scan4_kernel<ks, nq, pk>), g, dim3(256), 0, s, t, inv, tb, n, rp, qb, thr0, qn, \
+                     Q, qcnt, rows, dists, gate)
+#define CASE4(ks, nq, sel, g, n, rp)                                  \
+  if (d == 32 * ks && sel == nq) {                                    \
+    if (tb) SCAN4(ks, nq, true, g, n, rp);                            \
+    else SCAN4(ks, nq, false, g, n, rp);                              \
+  }
+#define CASES4(sel, g, n, rp)                                                             \
+  CASE4(1, 2, sel, g, n, rp) CASE4(1, 4, sel, g, n, rp) CASE4(1, 8, sel, g, n, rp)         \
+  CASE4(1, 16, sel, g, n, rp) CASE4(2, 2, sel, g, n, rp) CASE4(2, 4, sel, g, n, rp)        \
+  CASE4(2, 8, sel, g, n, rp) CASE4(2, 16, sel, g, n, rp)
       // pass 1 over the first V4_S rows under the 512-row bound (~2% of them
       // admitted): their exact k-th distance -> thr0, the admission bound of
-      // pass 2 over the whole table (~k / V4_S of it admitted)
-      constexpr int RPB_S = 64;   // one row tile per wave: the sample pass is latency-bound
-      const dim3 gs((unsigned)cdiv(V4_S, RPB_S), (unsigned)cdiv(Q, 32));
-#define SCAN4(ks, nq, pk, g, n, rpb)                                                                    \
-  hipLaunchKernelGGL((scan4_kernel<ks, nq, pk>), g, dim3(256), 0, s, t, inv, tb, n, rpb, qb, thr0, qn, \
-                     Q, qcnt, rows, dists, gate)
-      if (d == 32) {
-        if (tb) SCAN4(1, 2, true, gs, (int64_t)V4_S, RPB_S);
-        else SCAN4(1, 2, false, gs, (int64_t)V4_S, RPB_S);
-      } else {
-        if (tb) SCAN4(2, 2, true, gs, (int64_t)V4_S, RPB_S);
-        else SCAN4(2, 2, false, gs, (int64_t)V4_S, RPB_S);
-      }
+      // pass 2 over the whole table
+      CASES4(NQS, gs, (int64_t)V4_S, RPB_S)
       DCNR_LAUNCH_CHECK();
       hipLaunchKernelGGL((rescore_kernel<true>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k,
                          nullptr, nullptr, gate, thr0);
       DCNR_LAUNCH_CHECK();
-      // query blocks of 16: NQB per launch row (the table is read once per
-      // NQB * 16 queries)
-      const int nqb = (int)std::min<int64_t>(cdiv(Q, 16), V4_QC / 16);
-      const int NQ = nqb <= 2 ? 2 : nqb <= 4 ? 4 : nqb <= 8 ? 8 : 16;
-      const int rpb = v4_rpb(NQ);
-      const dim3 g4((unsigned)cdiv(N, rpb), (unsigned)cdiv(Q, NQ * 16));
-#define CASE4(ks, nq)                                                 \
-  if (d == 32 * ks && NQ == nq) {                                     \
-    if (tb) SCAN4(ks, nq, true, g4, N, rpb);                          \
-    else SCAN4(ks, nq, false, g4, N, rpb);                            \
-  }
-      CASE4(1, 2) CASE4(1, 4) CASE4(1, 8) CASE4(1, 16)
-      CASE4(2, 2) CASE4(2, 4) CASE4(2, 8) CASE4(2, 16)
+      CASES4(NQ, g4, N, rpb)
+#undef CASES4
 #undef CASE4
 #undef SCAN4
       DCNR_LAUNCH_CHECK();
