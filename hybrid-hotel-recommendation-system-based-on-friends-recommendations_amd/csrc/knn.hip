@@ -579,6 +579,9 @@ constexpr int V4_S = V4_S_OVR;   // exact sample rows for the admission bound
 #ifndef V4_TH_S
 #define V4_TH_S 512              // rows of the first bound (kth_bound_kernel) on the v4 path
 #endif
+#ifndef V4_WPS
+#define V4_WPS 3                 // min waves per SIMD of scan4 for NQB > 4
+#endif
 #ifndef V4_SNQ
 #define V4_SNQ 16                // query blocks per launch row of the sample pass (Q=256: 31 vs 43 us at 2)
 #endif
@@ -700,7 +703,7 @@ constexpr int V4_WL = V4_LIST / 4;   // ... per wave
 // (NQB > 4: at least 3 waves per SIMD -- left alone the compiler unrolled
 // its way to 284 registers and one wave per SIMD, 1.7x slower)
 template <int KS, int NQB, bool PK>
-__global__ __launch_bounds__(256, NQB > 4 ? 3 : 1) void scan4_kernel(const float* __restrict__ tab,
+__global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const float* __restrict__ tab,
                                                     const float* __restrict__ inv,
                                                     const bf16* __restrict__ tb, int64_t N, int rpb,
                                                     const bf16* __restrict__ qb,
