@@ -70,13 +70,21 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 // and drains them (vmcnt(0)) before every ds_read, which would serialise a stage ring;
 // the caller's counted vmcnt waits are the only synchronisation.
 // M0 is saved and restored inside the statement (it is compiler-reserved).
+#ifndef DCNR_DMA_NT
+#define DCNR_DMA_NT 0
+#endif
+#if DCNR_DMA_NT
+#define DCNR_DMA_POLICY "nt "
+#else
+#define DCNR_DMA_POLICY ""
+#endif
 __device__ __forceinline__ void dma16(u32x4 rsrc, int off, uint32_t lds_dst) {
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen " DCNR_DMA_POLICY "lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(off), "s"(rsrc), "s"(lds_dst)
