@@ -5,13 +5,22 @@
 //   dist(q, x) = clip(1 - <q/|q|, x/|x|>, 0, 2)          (fp32)
 //   result: k smallest per query, ascending by (dist, row index)
 //
-// HBM-streaming design: the table is read exactly once per tile of QT queries.
-// Each workgroup scans one contiguous row slice; every thread owns one row per
-// step (16-B loads), computes QT dots against the LDS-resident normalised
-// queries, and appends rows that beat the query's running k-th-best threshold
-// into a per-query LDS candidate buffer.  A buffer that could overflow on the
-// next step is compacted by an in-LDS bitonic sort (ties by index -> fully
-// deterministic).  A second kernel merges the slices' k-lists per query.
+// Four scans, chosen per shape in cosine_topk():
+//  * scan v4 (d = 32 / 64, k <= 32, N > V4_S; every Q): a bf16-MFMA coarse
+//    cosine over a fit-time bf16 copy of the normalised rows, with an
+//    admission bound that provably keeps every true neighbour, then exact
+//    fp32 distances of the admitted rows and an exact selection -- the
+//    production path of configs[4] (section "scan v4" below);
+//  * scan v3 (Q >= 16, d % 16 == 0): exact fp32-MFMA scan into per-slice
+//    k-lists -- other shapes, and v4's gated fallback;
+//  * scan v2 (d <= 64, k <= 32): exact VALU scan with wave-register lists;
+//  * scan v1 (the rest, k <= 64): the original streaming scan below --
+//    each workgroup scans one contiguous row slice; every thread owns one
+//    row per step (16-B loads), computes QT dots against the LDS-resident
+//    normalised queries, and appends rows that beat the query's running
+//    k-th-best threshold into a per-query LDS candidate buffer, compacted
+//    by an in-LDS bitonic sort (ties by index: deterministic).
+// v1-v3 end in merge_kernel (the slices' k-lists per query).
 #include "dcnr_internal.h"
 
 #include <cfloat>
