@@ -25,6 +25,8 @@
 //    no cross-wave reduction) and write one partial row per workgroup.
 #include "dcnr_internal.h"
 
+#include <type_traits>
+
 #ifndef WS_LAB_MODE
 #define WS_LAB_MODE 0   // tools/ws_lab.hip: 1 no C stores, 2 no X DMAs, 4 no MFMAs, 8 no epilogue,
                         // 16 no fragment reads in the K loop
@@ -53,6 +55,15 @@
 #ifndef WS_STAGGER
 #define WS_STAGGER 0
 #endif
+// software-pipelined epilogue (epilogues without operand loads): each tile's
+// epilogue runs one row block at a time inside the NEXT tile's K loop, in the
+// MFMA shadow; two accumulator sets, 32-row tiles (the register budget)
+#ifndef WS_PIPE
+#define WS_PIPE 0
+#endif
+#ifndef WS_PIPE_MIX
+#define WS_PIPE_MIX 0   // lab: let the scheduler mix the pending epilogue into the MFMA steps
+#endif
 
 namespace dcnr {
 namespace {
@@ -64,8 +75,12 @@ namespace {
 // ahead, DROP_BN 104.7 vs 111.9 us at 64 rows); eval BN_RELU at 32 rows
 // (71.5 vs 75.4-77.2 us at 64).
 constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
+template <int EPI> constexpr bool ws_pipe() {
+  return WS_PIPE && (EPI == NT_EPI_BIAS || EPI == NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS || EPI == NT_EPI_BN_RELU);
+}
 template <int KTP, int EPI> constexpr int ws_tm() {
-  return WS_TM_OVR && KTP == 16 ? WS_TM_OVR : (EPI <= NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS ? 64 : 32);
+  return ws_pipe<EPI>() ? 32
+         : WS_TM_OVR && KTP == 16 ? WS_TM_OVR : (EPI <= NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS ? 64 : 32);
 }
 template <int EPI> constexpr bool ws_ops_early() {
   return EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN || EPI == NT_EPI_BN_RESID_RELU;
@@ -245,17 +260,11 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     }
   };
   f32x4 acc[WS_RB][2];
-  // ---- epilogue of the tile at row m0 (acc, and its operands in the slots)
-  auto epilogue = [&](const int64_t m0) {
+  // ---- epilogue of row block rb of the tile at row m0 (accumulators ac, its
+  // operands in the slots)
+  auto epi_rb = [&](const int64_t m0, const int rb, f32x4 (&ac)[WS_RB][2]) {
     // lane holds C[m][nw + 16cb + 4q .. +3], m = m0 + 16rb + l15
-    if constexpr (WS_LAB_MODE & 8) {   // lab: no epilogue (keep acc alive)
-      float t = 0.f;
-#pragma unroll
-      for (int rb = 0; rb < WS_RB; ++rb) t += acc[rb][0][0] + acc[rb][1][3];
-      if (t == 12345.f) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), cr, 0, 0, 0);
-    } else
-#pragma unroll
-    for (int rb = 0; rb < WS_RB; ++rb) {
+    {
       const int64_t m = m0 + rb * 16 + l15;
       const bool mok = m < a.M;
       if (!WS_OPS_EARLY && rb + 1 < WS_RB) load_ops(m0, rb + 1, (rb + 1) & 1);
@@ -267,7 +276,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
 #pragma unroll
       for (int cb = 0; cb < 2; ++cb) {
         const int cl = wave * WS_WC + cb * 16 + q * 4;   // column within the slice
-        f2v v[2] = {f2v{acc[rb][cb][0], acc[rb][cb][1]}, f2v{acc[rb][cb][2], acc[rb][cb][3]}};
+        f2v v[2] = {f2v{ac[rb][cb][0], ac[rb][cb][1]}, f2v{ac[rb][cb][2], ac[rb][cb][3]}};
         f2v bb[2];
         if constexpr (HAS_BIAS) {
           const float4 bj = *reinterpret_cast<const float4*>(bias_s + cl);
@@ -351,12 +360,118 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
         const int off = (mok && nst < a.N) ? (int)((m * a.ldc + nst) * 2) : OOR;
         if constexpr (!(WS_LAB_MODE & 1))
           __builtin_amdgcn_raw_buffer_store_b128(sv, cr, off, 0, 0);
-        else if (acc[rb][0][0] == 12345.f)
+        else if (ac[rb][0][0] == 12345.f)
           __builtin_amdgcn_raw_buffer_store_b128(sv, cr, off, 0, 0);
       }
     }
   };
+  // ---- epilogue of the whole tile at row m0
+  auto epilogue = [&](const int64_t m0, f32x4 (&ac)[WS_RB][2]) {
+    if constexpr (WS_LAB_MODE & 8) {   // lab: no epilogue (keep acc alive)
+      float t = 0.f;
+#pragma unroll
+      for (int rb = 0; rb < WS_RB; ++rb) t += ac[rb][0][0] + ac[rb][1][3];
+      if (t == 12345.f) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), cr, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int rb = 0; rb < WS_RB; ++rb) epi_rb(m0, rb, ac);
+    }
+  };
 
+  if constexpr (ws_pipe<EPI>()) {
+    static_assert(NB == 2, "pipelined epilogue: two X buffers");
+    f32x4 acc2[WS_RB][2];
+    // the K loop of the tile in X buffer bi into ac; row block rb of the
+    // pending tile (pm0 >= 0, accumulators pa) is finished after K step
+    // ((rb + 1) KTP) / RB - 1, beside this tile's MFMAs
+    auto kloop = [&](auto pend_c, f32x4 (&ac)[WS_RB][2], const int bi, const int64_t pm0,
+                     f32x4 (&pa)[WS_RB][2]) {
+      constexpr bool PEND = decltype(pend_c)::value;   // (compile-time: one basic block per K step)
+      const char* xb = lds + bi * C::TILE + rowoff;
+#pragma unroll
+      for (int rb = 0; rb < WS_RB; ++rb)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) ac[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      auto xrd = [&](int kt, int rb) {
+        return *reinterpret_cast<const bf16x8*>(xb + rb * 16 * C::P + (kt >> 2) * 256 + coff[kt & 3]);
+      };
+      constexpr int NXB = WS_PFD + 1;
+      bf16x8 xf[NXB][WS_RB];
+#pragma unroll
+      for (int p = 0; p < WS_PFD; ++p)
+#pragma unroll
+        for (int rb = 0; rb < WS_RB; ++rb) xf[p][rb] = xrd(p, rb);
+#pragma unroll
+      for (int kt = 0; kt < KTP; ++kt) {
+        const int cur = kt % NXB;
+        const bool rd = kt + WS_PFD < KTP;
+        if (rd) {
+#pragma unroll
+          for (int rb = 0; rb < WS_RB; ++rb) xf[(kt + WS_PFD) % NXB][rb] = xrd(kt + WS_PFD, rb);
+        }
+#pragma unroll
+        for (int rb = 0; rb < WS_RB; ++rb)
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+            ac[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][kt], xf[cur][rb], ac[rb][cb], 0, 0, 0);
+        bool piece = false;
+        if constexpr (PEND) {
+#pragma unroll
+          for (int rb = 0; rb < WS_RB; ++rb)
+            if (kt == ((rb + 1) * KTP) / WS_RB - 1) {
+              epi_rb(pm0, rb, pa);
+              piece = true;
+            }
+        }
+#if WS_PREFETCH_PIN
+        if (rd && !(WS_PIPE_MIX && piece)) {
+#pragma unroll
+          for (int rb = 0; rb < WS_RB; ++rb) {
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
+          }
+        }
+        if (!(WS_PIPE_MIX && (piece || (PEND && kt + 1 < KTP && kt % (KTP / WS_RB) != KTP / WS_RB - 1))))
+          __builtin_amdgcn_sched_barrier(0);
+#endif
+      }
+    };
+    constexpr int NSTORE = (EPI == NT_EPI_F32 ? 2 : 1) * WS_RB;
+    // one tile: next tile's DMA, K loop (+ the pending epilogue), then the
+    // tile's X buffer is free and the next one landed: the stores issued
+    // after that DMA are exactly the pending epilogue's
+    auto step = [&](auto pend_c, f32x4 (&ac)[WS_RB][2], f32x4 (&pa)[WS_RB][2], int64_t& mt, int& bi,
+                    int64_t& pm0) {
+      const int64_t mn = mt + groups;
+      if (mn < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + (bi ^ 1) * C::TILE, wave, lane);
+      kloop(pend_c, ac, bi, pm0, pa);
+      const bool stored = decltype(pend_c)::value;
+      pm0 = mt * WS_TM;
+      if (stored && mn < a.mtiles)
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NSTORE) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      bi ^= 1;
+      mt = mn;
+    };
+    int64_t mt = group, pm0 = -1;
+    int bi = 0;
+    bool last2 = false;   // the pending tile's accumulators are acc2
+    using Yes = std::integral_constant<bool, true>;
+    using No = std::integral_constant<bool, false>;
+    if (mt < a.mtiles) step(No{}, acc, acc2, mt, bi, pm0);   // the first tile: nothing pending
+    while (mt < a.mtiles) {
+      step(Yes{}, acc2, acc, mt, bi, pm0);
+      last2 = true;
+      if (mt >= a.mtiles) break;
+      step(Yes{}, acc, acc2, mt, bi, pm0);
+      last2 = false;
+    }
+    if (pm0 >= 0) {
+      if (last2) epilogue(pm0, acc2);
+      else epilogue(pm0, acc);
+    }
+  } else {
   if constexpr (WS_PRIO) {
     if (wave >= 4) __builtin_amdgcn_s_setprio(1);
   }
@@ -368,7 +483,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     const int nbuf = buf + NB - 1 >= NB ? buf - 1 : buf + NB - 1;   // (buf + NB - 1) % NB
     if (mn < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + nbuf * C::TILE, wave, lane);
     const int64_t m0 = mt * WS_TM;
-    if (late && pm0 >= 0) epilogue(pm0);   // the previous tile's, beside the partners' MFMAs
+    if (late && pm0 >= 0) epilogue(pm0, acc);   // the previous tile's, beside the partners' MFMAs
     if constexpr (WS_OPS_EARLY) {
 #pragma unroll
       for (int rb = 0; rb < WS_RB; ++rb) load_ops(m0, rb, rb);
@@ -423,7 +538,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     }
 
     if (late) pm0 = m0;
-    else epilogue(m0);
+    else epilogue(m0, acc);
     // next tile's X landed and every wave is done reading this buffer.  Younger
     // than the next tile's DMAs: the stores of the last NB-1 tiles and the
     // DMAs of the NB-2 tiles after it -- when all of those were issued (near
@@ -435,7 +550,8 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
   }
-  if (late && pm0 >= 0) epilogue(pm0);
+  if (late && pm0 >= 0) epilogue(pm0, acc);
+  }
   if constexpr (STATS) {
     // 16-lane butterfly: lane (q, m) ends with k = bit2(m), cb = bit3(m),
     // column pair element r = 2 bit0(m) + bit1(m) of columns nw + 16cb + 4q

@@ -78,8 +78,13 @@ int main(int argc, char** argv) {
   float ms;
   hipEventElapsedTime(&ms, e0, e1);
   const double us = ms * 1e3 / it;
-  printf("ws epi %d mode %d  M=%ld K=%d N=%d  %.1f us  %.0f TF/s  %s\n", epi, WS_LAB_MODE, (long)M, K,
-         N, us, 2.0 * M * N * K / us / 1e6,
+  // checksum of C (bit patterns): compares builds of different schedules
+  std::vector<uint32_t> hc(M * (size_t)N * (epi == dcnr::NT_EPI_F32 ? 4 : 2) / 4);
+  hipMemcpy(hc.data(), C, hc.size() * 4, hipMemcpyDeviceToHost);
+  uint64_t cks = 0;
+  for (size_t i = 0; i < hc.size(); ++i) cks = cks * 1099511628211ull + hc[i];
+  printf("ws epi %d mode %d  M=%ld K=%d N=%d  %.1f us  %.0f TF/s  C %016llx  %s\n", epi, WS_LAB_MODE, (long)M, K,
+         N, us, 2.0 * M * N * K / us / 1e6, (unsigned long long)cks,
          hipGetErrorString(hipGetLastError()));
   return 0;
 }
