@@ -522,7 +522,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         if instrumented:
-            _lib.profile_enable(True)
+            _lib.profile_enable(instrumented)
             _lib.profile_collect()
         t0 = time.perf_counter()
         for k in range(args.steps):
@@ -547,6 +547,10 @@ def main():
     # on its stream (per-kernel-class durations for the roofline); the events
     # serialise launches, so this pass is not the throughput number
     el_prof, prof, _ = timed(True)
+    # and once more timing only the weight-gradient GEMMs, in place on their
+    # side stream under the dX chain (profile mode 2): their concurrent wall
+    # time, the contention the alone-priced table above does not show
+    _, prof_dw, _ = timed(2) if args.precision == "bf16" else (None, None, None)
     trainer.check_indices()
     final_loss = float(loss.item())
     # N > 1: the same K steps with the other table exchange on the same
@@ -649,6 +653,12 @@ def main():
                 "frac": dt["frac"], "traffic": pmc_traffic(dom),
                 "bytes_per_launch": dt["bytes_per_launch"], "avg_launch_ms": dt["avg_launch_ms"]}
         roof["frac_of_measured_copy"] = dt["achieved_gbs"] / peaks["copy_gbs"]
+        if prof_dw and prof_dw.get("gemm_dw", (0, 0, 0))[1] and dom == "gemm_dw":
+            c_ms, c_cnt, _ = prof_dw["gemm_dw"]
+            roof["concurrent"] = {
+                "avg_launch_ms": c_ms / c_cnt, "ms_per_step": c_ms / args.steps,
+                "note": "the same launches timed in place on the side stream, overlapping the "
+                        "main stream's dX GEMMs and BN passes (profile mode 2)"}
         if dom in GEMM_FLOP:
             flop_launch = GEMM_FLOP[dom] * B * args.steps / prof[dom][1]
             roof["mfma_view"] = {"achieved_tflops": flop_launch / (dt["avg_launch_ms"] / 1e3) / 1e12,

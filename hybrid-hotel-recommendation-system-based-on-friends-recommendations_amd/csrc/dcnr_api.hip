@@ -55,6 +55,7 @@ dcnr_status set_max_dyn_lds(const void* kernel, size_t bytes) {
 struct ProfRec { int cat; double bytes; hipEvent_t a, b; };
 static std::mutex g_pm;
 static bool g_prof = false;
+static int g_prof_mode = 0;   // 1: every class, each launch alone; 2: gemm_dw only, concurrent
 static std::vector<ProfRec> g_recs;
 static std::vector<hipEvent_t> g_pool;
 
@@ -68,7 +69,7 @@ static hipEvent_t prof_event() {
 struct ProfScope {
   int cat; hipStream_t s; double bytes; hipEvent_t a = nullptr;
   ProfScope(int c, hipStream_t st, double nbytes = 0.0) : cat(c), s(st), bytes(nbytes) {
-    if (!g_prof) return;
+    if (!g_prof || (g_prof_mode == 2 && c != DCNR_K_GEMM_DW)) return;
     std::lock_guard<std::mutex> lk(g_pm);
     a = prof_event();
     (void)hipEventRecord(a, s);
@@ -1121,8 +1122,9 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   DwPipe dwp;
   DwPipe* pipe = nullptr;
   // (not while kernel classes are being timed: there every launch is priced
-  // alone, on the main stream, as before the overlap)
-  if (d.prec == DCNR_PREC_BF16 && !g_prof) {
+  // alone, on the main stream, as before the overlap -- except in profile
+  // mode 2, which times the side stream's gemm_dw launches in place)
+  if (d.prec == DCNR_PREC_BF16 && (!g_prof || g_prof_mode == 2)) {
     TRY(dwp.init(sj.side));
     pipe = &dwp;
   }
@@ -1477,6 +1479,7 @@ dcnr_status dcnr_linear_wgrad_bf16(const void* dY, int64_t ldy, const void* X, i
 void dcnr_profile_enable(int on) {
   std::lock_guard<std::mutex> lk(g_pm);
   g_prof = on != 0;
+  g_prof_mode = on;
 }
 
 dcnr_status dcnr_profile_collect(double* ms, int64_t* launches, int32_t n) {

@@ -111,8 +111,10 @@ KERNEL_CLASSES = ["gather_cross", "gemm_fwd", "gemm_dx", "gemm_dw", "rowwise", "
                   "cross_bwd", "head", "adam", "knn", "pack", "serve", "emb_sort", "emb_sum"]
 
 
-def profile_enable(on: bool):
-    load().dcnr_profile_enable(1 if on else 0)
+def profile_enable(on):
+    """False/True = off/every class alone; 2 = gemm_dw only, concurrent on
+    its side stream (dcnr_profile_enable)."""
+    load().dcnr_profile_enable(int(on))
 
 
 def profile_collect(with_bytes: bool = False):

@@ -366,6 +366,10 @@ typedef enum {
   DCNR_K_COUNT = 14
 } dcnr_kernel_class;
 
+/* on = 0: off; 1: every launch timed per class with HIP events on its
+ * stream (the backward's weight-gradient GEMMs then run on the caller's
+ * stream, each launch priced alone); 2: only DCNR_K_GEMM_DW timed, on the
+ * side stream where it overlaps the dX chain (its concurrent wall time). */
 void dcnr_profile_enable(int on);
 /* Synchronises the recorded events and returns, per class, the summed kernel
  * milliseconds and launch counts since the last collect (arrays of n). */
