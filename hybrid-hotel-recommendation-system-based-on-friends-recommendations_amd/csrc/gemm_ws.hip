@@ -74,12 +74,16 @@ namespace {
 // operand load before the MFMAs ("early": RESID 90.5 vs 96.4 us one row block
 // ahead, DROP_BN 104.7 vs 111.9 us at 64 rows); eval BN_RELU at 32 rows
 // (71.5 vs 75.4-77.2 us at 64).
-constexpr int WS_NT = 512, WS_WAVES = 8, WS_TN = 256, WS_WC = 32;
+#ifndef WS_SPLIT
+#define WS_SPLIT 0   // lab: two 4-wave workgroups per CU on 128-column slices
+#endif
+constexpr int WS_WAVES = WS_SPLIT ? 4 : 8, WS_NT = 64 * WS_WAVES, WS_WC = 32, WS_TN = WS_WAVES * WS_WC;
+constexpr int WS_WG_PER_CU = WS_SPLIT ? 2 : 1;
 template <int EPI> constexpr bool ws_pipe() {
   return WS_PIPE && (EPI == NT_EPI_BIAS || EPI == NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS || EPI == NT_EPI_BN_RELU);
 }
 template <int KTP, int EPI> constexpr int ws_tm() {
-  return ws_pipe<EPI>() ? 32
+  return ws_pipe<EPI>() || WS_SPLIT ? 32
          : WS_TM_OVR && KTP == 16 ? WS_TM_OVR : (EPI <= NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS ? 64 : 32);
 }
 template <int EPI> constexpr bool ws_ops_early() {
@@ -146,7 +150,7 @@ __device__ __forceinline__ void issue_tile(u32x4 xr, int64_t ldx, int K, uint32_
 }
 
 template <int KTP, int EPI>
-__global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
+__global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs a) {
   constexpr int WS_TM = ws_tm<KTP, EPI>();
   constexpr int NB = ws_nb<KTP, EPI>();
   using C = WsCfg<KTP, WS_TM, NB>;
@@ -603,7 +607,7 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   }
   a.mtiles = cdiv(a.M, WS_TM);
   const int unit = 8 * a.nslices;
-  int grid = std::max(unit, (256 / unit) * unit);
+  int grid = std::max(unit, (256 * WS_WG_PER_CU / unit) * unit);
   const int64_t need = a.mtiles * a.nslices;
   if (need < grid) grid = (int)(cdiv(need, unit) * unit);
   a.groups = grid / a.nslices;
