@@ -288,7 +288,13 @@ def bench_cfg5(dev, iters, cpu):
         flop = 2.0 * n_items * Q * 64
         packed = pipe.index._packed is not None
         nbytes = n_items * 64 * 2 if packed else table_bytes
+        knn_pmc = {}
+        try:
+            knn_pmc = json.load(open(os.path.join(ROOT, "profiles", "knn_pmc_traffic.json")))
+        except Exception:
+            pass
         out["roofline" if Q == 1 else f"roofline_q{Q}"] = {
+            "traffic": knn_pmc.get(f"topk_q{Q}"),   # PMC HBM bytes per call (whole chain)
             "bound": "hbm", "kernel": "kth_bound + scan4 (bf16 MFMA%s) + rescore (dcnr_cosine_topk, Q=%d)"
             % (" over the fit-time bf16 copy" if packed else "", Q),
             "achieved": nbytes / t / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
