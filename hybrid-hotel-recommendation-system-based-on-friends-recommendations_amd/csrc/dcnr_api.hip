@@ -114,6 +114,13 @@ namespace {
 #endif
 constexpr unsigned SYNC_EV = hipEventDisableTiming | (DCNR_EV_NOFENCE ? hipEventDisableSystemFence : 0u);
 
+// workgroups of the residual blocks' weight-gradient GEMMs, which overlap the
+// dX chain on the side stream (0: one per CU, as for the initial layer's, the
+// last one of the backward)
+#ifndef DW_WG_BLOCKS
+#define DW_WG_BLOCKS 0
+#endif
+
 // One side stream per device (created on first use, never destroyed) for the
 // backward's work that does not depend on the deep tower; fork/join events
 // per call.
@@ -668,13 +675,14 @@ struct DwPipe {
     return DCNR_OK;
   }
   dcnr_status wgrad(const Layout& L, const void* dY, int64_t ldy, int N, const void* X, int64_t ldx,
-                    int Kc, int64_t B, float* out, int Nr, int Kr, int accumulate, hipStream_t main_s) {
+                    int Kc, int64_t B, float* out, int Nr, int Kr, int accumulate, hipStream_t main_s,
+                    int wg_target) {
     TRY(enter(main_s));
     ++calls;
     hipStream_t s = side;   // TRYB launches and times on the side stream
     // (the full-chip split count: 32 / 16 splits, leaving CUs to the main
     // stream and halving the slab, measured 2 % / 21 % slower per step)
-    const int S = gemm_dw_splits(N, Kc, B);
+    const int S = gemm_dw_splits(N, Kc, B, wg_target);
     if ((int64_t)S * N * Kc > L.slab_elems) {
       set_error("wgrad: slab too small");
       return DCNR_WORKSPACE_TOO_SMALL;
@@ -710,9 +718,9 @@ struct DwPipe {
 
 dcnr_status linear_dw(const Dims& d, const Layout& L, const void* dY, int ldy, int N,
                       const void* X, int ldx, int Kc, int64_t B, float* out, int Nr, int Kr,
-                      int accumulate, hipStream_t s, DwPipe* pipe = nullptr) {
+                      int accumulate, hipStream_t s, DwPipe* pipe = nullptr, int wg_target = 0) {
   if (d.prec == DCNR_PREC_BF16 && gemm_dw_supported(N, Kc, ldy, ldx, B)) {
-    if (pipe) return pipe->wgrad(L, dY, ldy, N, X, ldx, Kc, B, out, Nr, Kr, accumulate, s);
+    if (pipe) return pipe->wgrad(L, dY, ldy, N, X, ldx, Kc, B, out, Nr, Kr, accumulate, s, wg_target);
     return wgrad_bf16(dY, ldy, N, X, ldx, Kc, B, L.slab, L.slab_elems, out, Nr, Kr, accumulate, s);
   }
   // the generic path below writes the slab on this stream: the side stream's
@@ -1157,7 +1165,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn2_apply2(d.prec, du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
                        dt2, L.part, &nc, s));
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
-    TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe));
+    TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
     if (fuse) {
       // dy1 = (dt2 W2) * [a1 != 0] / (1-p): relu and dropout masks from the
       // saved activation, BN1 partials (and, without SyncBN, its backward
@@ -1180,7 +1188,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_apply2(d.prec, da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, dt1,
                        L.part, &nc, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
-    TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe));
+    TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
     if (fuse && j > 0) {
       // G is only consumed by block j-1's BN2 backward: emit its du = G * [h_j > 0]
       // (in place over this block's du, the residual operand, unless

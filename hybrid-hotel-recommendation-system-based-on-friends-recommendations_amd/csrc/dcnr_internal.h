@@ -368,7 +368,8 @@ struct DwArgs {
   int tiles_n, tiles_k;            // filled by gemm_dw
 };
 bool gemm_dw_supported(int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t Btot);
-int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot);
+// split count for ~wg_target workgroups (0: the default, one per CU)
+int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot, int wg_target = 0);
 dcnr_status gemm_dw(const DwArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ elementwise

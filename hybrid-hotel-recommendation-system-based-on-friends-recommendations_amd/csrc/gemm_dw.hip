@@ -168,9 +168,9 @@ bool gemm_dw_supported(int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t B
 #ifndef DW_WG_TARGET
 #define DW_WG_TARGET 256   // workgroups per launch (lab override)
 #endif
-int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot) {
+int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot, int wg_target) {
   const int64_t tiles = cdiv(N, TNW) * cdiv(K, TKW);
-  int64_t s = std::max<int64_t>(8, (DW_WG_TARGET / tiles) / 8 * 8);
+  int64_t s = std::max<int64_t>(8, ((wg_target > 0 ? wg_target : DW_WG_TARGET) / tiles) / 8 * 8);
   while (s > 8 && cdiv(Btot, s) < 2 * BKW) s -= 8;   // at least two stages per split
   return (int)s;
 }
