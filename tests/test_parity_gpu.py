@@ -435,7 +435,7 @@ def test_cosine_knn_vs_sklearn_golden(dev):
             np.testing.assert_array_equal(i[r][isolated], ref_i[isolated])
 
 
-@pytest.mark.parametrize("Q,d", [(1, 64), (3, 64), (8, 64), (32, 64), (256, 64), (64, 32)])
+@pytest.mark.parametrize("Q,d", [(1, 64), (3, 64), (8, 64), (32, 64), (256, 64), (64, 32), (600, 64)])
 def test_cosine_knn_full_size(dev, Q, d):
     """configs[4] size: cosine top-11 over 1M x d (the bf16-MFMA coarse scan
     + exact fp32 rescoring of its admitted rows, knn.hip scan v4, for every Q)
