@@ -931,37 +931,56 @@ namespace {
 // bits as summing the untransposed slabs), transposes through LDS, writes
 // rows of out along k (16-B stores when out's rows allow).
 constexpr int RT_K = 64, RT_N = 16;
-__global__ __launch_bounds__(256) void splitk_reduce_t_kernel(const float* slab, int splits,
-                                                              int64_t stride, int ld, int N, int K,
-                                                              float* out, int accumulate, int vec_out) {
-  __shared__ float t[RT_K][RT_N + 1];
+// RT_ZG thread groups per output tile would each sum a contiguous share of
+// the splits and add the partials in group order (lab knob): measured 12-13
+// us alone either way per 512 x 512 call (the one-group kernel is not
+// latency-bound), 40-54 us median under the concurrent dX chain; one group
+// kept -- the summation order of the earlier rounds.
+#ifndef RT_ZG
+#define RT_ZG 1
+#endif
+__global__ __launch_bounds__(256 * RT_ZG) void splitk_reduce_t_kernel(const float* slab, int splits,
+                                                                      int64_t stride, int ld, int N, int K,
+                                                                      float* out, int accumulate, int vec_out) {
+  __shared__ float t[RT_ZG][RT_K][RT_N + 1];
   const int k0 = blockIdx.x * RT_K, n0 = blockIdx.y * RT_N;
+  const int zg = threadIdx.x >> 8, idx = threadIdx.x & 255;
   {
-    const int kk = threadIdx.x >> 2, nq = threadIdx.x & 3;
+    const int kk = idx >> 2, nq = idx & 3;
     const int k = k0 + kk, n = n0 + 4 * nq;
+    const int per = (splits + RT_ZG - 1) / RT_ZG;
+    const int z0 = zg * per, z1 = min(splits, z0 + per);
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if (k < K && n < N) {
       const float* base = slab + (int64_t)k * ld + n;
-      int z = 0;
-      for (; z + 16 <= splits; z += 16) {
+      int z = z0;
+      for (; z + 16 <= z1; z += 16) {
         float4 v[16];
 #pragma unroll
         for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const float4*>(base + (int64_t)(z + u) * stride);
 #pragma unroll
         for (int u = 0; u < 16; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
       }
-      for (; z < splits; ++z) {
+      for (; z < z1; ++z) {
         const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)z * stride);
         s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
       }
     }
-    t[kk][4 * nq] = s.x; t[kk][4 * nq + 1] = s.y; t[kk][4 * nq + 2] = s.z; t[kk][4 * nq + 3] = s.w;
+    t[zg][kk][4 * nq] = s.x; t[zg][kk][4 * nq + 1] = s.y; t[zg][kk][4 * nq + 2] = s.z; t[zg][kk][4 * nq + 3] = s.w;
   }
   __syncthreads();
-  const int nn = threadIdx.x >> 4, kq = threadIdx.x & 15;
+  if (zg) return;
+  const int nn = idx >> 4, kq = idx & 15;
   const int n = n0 + nn, k = k0 + 4 * kq;
   if (n >= N) return;
-  float v[4] = {t[4 * kq][nn], t[4 * kq + 1][nn], t[4 * kq + 2][nn], t[4 * kq + 3][nn]};
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float a = t[0][4 * kq + j][nn];
+#pragma unroll
+    for (int g = 1; g < RT_ZG; ++g) a += t[g][4 * kq + j][nn];
+    v[j] = a;
+  }
   float* o = out + (int64_t)n * K + k;
   if (vec_out && k + 3 < K) {
     float4 r = make_float4(v[0], v[1], v[2], v[3]);
@@ -987,7 +1006,7 @@ dcnr_status splitk_reduce_t(const float* slab, int splits, int64_t slab_stride, 
   }
   const int vec_out = K % 4 == 0 && (uintptr_t)out % 16 == 0;
   hipLaunchKernelGGL(splitk_reduce_t_kernel, dim3((unsigned)cdiv(K, RT_K), (unsigned)cdiv(N, RT_N)),
-                     dim3(256), 0, s, slab, splits, slab_stride, ld_slab, N, K, out, accumulate,
+                     dim3(256 * RT_ZG), 0, s, slab, splits, slab_stride, ld_slab, N, K, out, accumulate,
                      vec_out);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
