@@ -6,7 +6,7 @@
 //   result: k smallest per query, ascending by (dist, row index)
 //
 // Four scans, chosen per shape in cosine_topk():
-//  * scan v4 (d = 32 / 64, k <= 32, N > V4_S; every Q): a bf16-MFMA coarse
+//  * scan v4 (d = 32 / 64, k <= 32; every N and Q): a bf16-MFMA coarse
 //    cosine over a fit-time bf16 copy of the normalised rows, with an
 //    admission bound that provably keeps every true neighbour, then exact
 //    fp32 distances of the admitted rows and an exact selection -- the
@@ -561,7 +561,7 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------- scan v4
-// Every query count (Q >= V4_MIN_Q; d = 32 or 64, N > V4_S): bf16-MFMA coarse scoring of
+// Every table and query count (Q >= V4_MIN_Q; d = 32 or 64): bf16-MFMA coarse scoring of
 // every (row, query) pair + exact fp32 re-scoring of the rows it admits.
 //
 // The coarse cosine is sum_i bf16(x_i * inv_r) * bf16(q_i / |q|), fp32
@@ -1302,7 +1302,12 @@ void plan2(int64_t N, int* nslices, int64_t* rows_per_block) {
 }
 
 bool use_v4(int64_t N, int64_t Q, int d, int k) {
-  return use_v2(d, k) && Q >= V4_MIN_Q && d % 32 == 0 && N > V4_S;
+  // (every N: a table of at most V4_S rows is its own sample -- pass 1 then
+  // repeats pass 2, but one index and every row shard of it compute each
+  // distance with the same arithmetic, so a sharded index returns the single
+  // index's answer bit for bit)
+  (void)N;
+  return use_v2(d, k) && Q >= V4_MIN_Q && d % 32 == 0;
 }
 
 // v4 scratch after the v2 layout (cands | qn [Q][d] | thr0 [Q]): bf16
@@ -1406,7 +1411,8 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       const int NQ = nqb <= 2 ? 2 : nqb <= 4 ? 4 : nqb <= 8 ? 8 : 16;
       const int NQS = std::min(NQ, V4_SNQ);
       constexpr int RPB_S = 64;   // one row tile per wave: the sample pass is latency-bound
-      const dim3 gs((unsigned)cdiv(V4_S, RPB_S), (unsigned)cdiv(Q, NQS * 16));
+      const int64_t NS = std::min<int64_t>(N, V4_S);   // sample rows
+      const dim3 gs((unsigned)cdiv(NS, RPB_S), (unsigned)cdiv(Q, NQS * 16));
       const int rpb = v4_rpb(NQ);
       const dim3 g4((unsigned)cdiv(N, rpb), (unsigned)cdiv(Q, NQ * 16));
 #define SCAN4(ks, nq, pk, g, n, rp)                                                                    \
@@ -1424,7 +1430,7 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       // pass 1 over the first V4_S rows under the 512-row bound (~2% of them
       // admitted): their exact k-th distance -> thr0, the admission bound of
       // pass 2 over the whole table
-      CASES4(NQS, gs, (int64_t)V4_S, RPB_S)
+      CASES4(NQS, gs, NS, RPB_S)
       DCNR_LAUNCH_CHECK();
       hipLaunchKernelGGL((rescore_kernel<true>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k,
                          nullptr, nullptr, gate, thr0);

@@ -76,7 +76,10 @@ def _table(n, d, seed):
 
 
 def _cases():
-    return [(20000, 64, 1), (20000, 64, 7), (20000, 64, 40), (5003, 32, 33), (15, 16, 3)]
+    # (60000 and 70001 rows: the whole table above scan v4's 32768-row sample,
+    # each shard below it -- the same arithmetic either way)
+    return [(20000, 64, 1), (20000, 64, 7), (20000, 64, 40), (5003, 32, 33), (15, 16, 3),
+            (60000, 64, 40), (70001, 32, 1)]
 
 
 def _worker(rank, world, port, path):
