@@ -604,6 +604,12 @@ constexpr int V4_QC = 256;       // queries per block (LDS: V4_QC x d bf16)
 // prologue and epilogue amortised; measured 69 vs 78 us at Q = 32), many ->
 // short ones (a wave's list fill grows with rows x queries)
 constexpr int v4_rpb(int nqb) { return V4_RPB_OVR ? V4_RPB_OVR : nqb <= 4 ? 2048 : 512; }
+#ifndef V4_MIN_N
+#define V4_MIN_N 0   // lab: the smallest table scan v4 serves
+#endif
+#ifndef V4_Q1_N
+#define V4_Q1_N 800000   // a single query takes scan v2 below this many rows
+#endif
 #ifndef V4_MIN_Q
 #define V4_MIN_Q 1   // from Q = 1: 60-66 us for Q <= 8 against 65-98 on scan v2
 #endif
@@ -903,45 +909,38 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
   }
   __syncthreads();
   // exact fp32 distance of every admitted pair, here rather than in the
-  // per-query rescore: the row gathers (one round trip per EU x 16 pairs)
-  // then overlap the other blocks' streaming instead of forming a
-  // one-block-per-query latency chain.  16 lanes per pair: lane c takes
-  // float4 chunk c of the row and of the normalised query, a DPP butterfly
-  // sums the 16 dot4s.
-  constexpr int DV = KS * 8, EU = 4;
-  const int grp = threadIdx.x >> 4, c = threadIdx.x & 15;
+  // per-query rescore: the row gathers then overlap the other blocks'
+  // streaming instead of forming a one-block-per-query latency chain.  One
+  // lane per pair, the float4 chunks summed in order: scan v2's arithmetic,
+  // expression for expression, so v2 and v4 give a row the same distance
+  // bit for bit (a row-sharded index, whose small shards may take v2, then
+  // returns the single index's answer).
+  constexpr int DV = KS * 8;
   const float4* tab4 = reinterpret_cast<const float4*>(tab);
   const float4* qn4 = reinterpret_cast<const float4*>(qn);
-  for (int e0 = 0; e0 < ((V4_LAB & 4) ? 0 : n); e0 += 16 * EU) {
-    float4 xv[EU], qv[EU];
-    float ivv[EU];
-    int qe[EU], re[EU];
+  for (int e = threadIdx.x; e < ((V4_LAB & 4) ? 0 : n); e += 256) {
+    const int sl = slot(e);
+    const int qe = lq[sl], re = lr[sl];
+    const float4* rp = tab4 + (int64_t)re * DV;
+    const float4* qp = qn4 + (qc0 + qe) * DV;
+    float4 x[DV];
 #pragma unroll
-    for (int u = 0; u < EU; ++u) {
-      const int e = e0 + 16 * u + grp;
-      const bool ok = e < n;
-      const int sl = slot(min(e, n - 1));
-      qe[u] = ok ? lq[sl] : -1;
-      re[u] = ok ? lr[sl] : 0;
-      const bool ld = ok && c < DV;
-      xv[u] = ld ? tab4[(int64_t)re[u] * DV + c] : float4{0.f, 0.f, 0.f, 0.f};
-      qv[u] = ld ? qn4[(qc0 + qe[u]) * DV + c] : float4{0.f, 0.f, 0.f, 0.f};
-      ivv[u] = inv[re[u]];
+    for (int v = 0; v < DV; ++v) x[v] = rp[v];
+    const float ir = inv[re];
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < DV; ++v) {
+      const float4 q = qp[v];
+      s += x[v].x * q.x + x[v].y * q.y + x[v].z * q.z + x[v].w * q.w;
     }
-#pragma unroll
-    for (int u = 0; u < EU; ++u) {
-      float p = xv[u].x * qv[u].x + xv[u].y * qv[u].y + xv[u].z * qv[u].z + xv[u].w * qv[u].w;
-      p = row16_sum(p);
-      if (c == 0 && qe[u] >= 0) {
-        const int pos = atomicAdd(&qn_[qe[u]], 1);
-        if (pos < V4_CAP) {
-          const int64_t o = (qc0 + qe[u]) * V4_CAP + pos;
-          rows[o] = re[u];
-          dists[o] = fminf(fmaxf(1.f - p * ivv[u], 0.f), 2.f);
-        } else {
-          *flag = 1;
-        }
-      }
+    const float dist = fminf(fmaxf(1.f - s * ir, 0.f), 2.f);
+    const int pos = atomicAdd(&qn_[qe], 1);
+    if (pos < V4_CAP) {
+      const int64_t o = (qc0 + qe) * V4_CAP + pos;
+      rows[o] = re;
+      dists[o] = dist;
+    } else {
+      *flag = 1;
     }
   }
 }
@@ -1302,12 +1301,12 @@ void plan2(int64_t N, int* nslices, int64_t* rows_per_block) {
 }
 
 bool use_v4(int64_t N, int64_t Q, int d, int k) {
-  // (every N: a table of at most V4_S rows is its own sample -- pass 1 then
-  // repeats pass 2, but one index and every row shard of it compute each
-  // distance with the same arithmetic, so a sharded index returns the single
-  // index's answer bit for bit)
-  (void)N;
-  return use_v2(d, k) && Q >= V4_MIN_Q && d % 32 == 0;
+  // Any table size: one of at most V4_S rows is its own sample (pass 1 then
+  // repeats pass 2).  A single query over fewer than V4_Q1_N rows takes scan
+  // v2, whose one pass beats v4's fixed chain (29 vs 50 us at 20000 rows, 65
+  // vs 61 at 1M); v4's exact distances use v2's arithmetic, so the choice
+  // never changes an answer.
+  return use_v2(d, k) && Q >= V4_MIN_Q && d % 32 == 0 && N >= V4_MIN_N && (Q > 1 || N >= V4_Q1_N);
 }
 
 // v4 scratch after the v2 layout (cands | qn [Q][d] | thr0 [Q]): bf16

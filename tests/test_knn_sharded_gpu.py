@@ -78,8 +78,11 @@ def _table(n, d, seed):
 def _cases():
     # (60000 and 70001 rows: the whole table above scan v4's 32768-row sample,
     # each shard below it -- the same arithmetic either way)
+    # (60000 / 70001 rows: the table above scan v4's 32768-row sample, each
+    # shard below it; 1M rows at Q=1: the single index takes v4, its
+    # 500000-row shards scan v2 -- the same distances either way)
     return [(20000, 64, 1), (20000, 64, 7), (20000, 64, 40), (5003, 32, 33), (15, 16, 3),
-            (60000, 64, 40), (70001, 32, 1)]
+            (60000, 64, 40), (70001, 32, 1), (1_000_000, 64, 1)]
 
 
 def _worker(rank, world, port, path):

@@ -543,6 +543,26 @@ def test_cosine_knn_v4_ties_zero_rows_and_kmax(dev, d, k):
     assert np.all(dz.cpu().numpy() == 1.0)
 
 
+@pytest.mark.parametrize("N,d", [(100_000, 64), (50_000, 32)])
+def test_cosine_knn_v2_v4_same_answer(dev, N, d):
+    """One query alone takes scan v2 on these tables; the same query in a
+    batch of 2 / 40 takes scan v4 (coarse bf16 admission + exact rescoring):
+    rows and distances bit-identical (v4's exact distances use v2's
+    arithmetic), so the scan a shape happens to take never changes an
+    answer."""
+    import dcnr
+    g = torch.Generator(device=dev).manual_seed(9 + d)
+    table = torch.randn(N, d, device=dev, generator=g)
+    q = torch.randn(40, d, device=dev, generator=g)
+    nn_ = dcnr.NearestNeighbors(metric="cosine").fit(table)
+    for r in range(3):
+        d1, i1 = nn_.kneighbors_device(q[r:r + 1], 11)
+        d2, i2 = nn_.kneighbors_device(q[r:r + 2], 11)
+        d40, i40 = nn_.kneighbors_device(q, 11)
+        assert torch.equal(i1[0], i2[0]) and torch.equal(d1[0], d2[0]), r
+        assert torch.equal(i1[0], i40[r]) and torch.equal(d1[0], d40[r]), r
+
+
 def test_cosine_knn_v4_overflow_falls_back_exact(dev):
     """More than V4_CAP rows inside one query's admission bound (12000 rows
     on the query's own direction, every one at distance 0): scan v4's list
