@@ -6,14 +6,16 @@
 //   result: k smallest per query, ascending by (dist, row index)
 //
 // Four scans, chosen per shape in cosine_topk():
-//  * scan v4 (d = 32 / 64, k <= 32; every N and Q): a bf16-MFMA coarse
+//  * scan v4 (d = 32 / 64, k <= 32; every N and Q but single queries over
+//    small tables): a bf16-MFMA coarse
 //    cosine over a fit-time bf16 copy of the normalised rows, with an
 //    admission bound that provably keeps every true neighbour, then exact
 //    fp32 distances of the admitted rows and an exact selection -- the
 //    production path of configs[4] (section "scan v4" below);
-//  * scan v3 (Q >= 16, d % 16 == 0): exact fp32-MFMA scan into per-slice
-//    k-lists -- other shapes, and v4's gated fallback;
-//  * scan v2 (d <= 64, k <= 32): exact VALU scan with wave-register lists;
+//  * scan v3 (Q >= 16, d % 16 == 0, d not 32 / 64): exact fp32-MFMA scan
+//    into per-slice k-lists;
+//  * scan v2 (d <= 64, k <= 32): exact VALU scan with wave-register lists --
+//    small Q, and v4's gated fallback (the same distance arithmetic);
 //  * scan v1 (the rest, k <= 64): the original streaming scan below --
 //    each workgroup scans one contiguous row slice; every thread owns one
 //    row per step (16-B loads), computes QT dots against the LDS-resident
@@ -210,10 +212,12 @@ __global__ __launch_bounds__(K2_NT) void scan2_kernel(const float* __restrict__ 
                                                       const float* __restrict__ qn, int64_t Q,
                                                       int k, int64_t rows_per_block, int nslices,
                                                       int qtiles, Cand* out,
-                                                      const float* __restrict__ thr0) {
+                                                      const float* __restrict__ thr0,
+                                                      const int* gate = nullptr) {
   __shared__ float cd[K2_WPB][K2_QT][K2_CAP];
   __shared__ int ci[K2_WPB][K2_QT][K2_CAP];
   __shared__ int cntl[K2_WPB][K2_QT];
+  if (gate && *gate == 0) return;   // scan v4 fallback: only when v4 overflowed
   const int bid = blockIdx.x;
   const int tile = (bid / 8) % qtiles;
   const int slice = (bid % 8) + 8 * (bid / (8 * qtiles));
@@ -574,11 +578,11 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 // rows under that bound keeps every true neighbour, ties included.  T0 comes
 // from the same machinery run on the sample under the 512-row bound of
 // kth_bound_kernel (pass 1).  The admitted rows (~N k / V4_S per query) are
-// appended to a per-query list; rescore_kernel recomputes their distances in
-// fp32 (the products of scan v2, summed by a 16-lane butterfly) and selects
-// the k best by (distance, row).  A query whose
+// appended to a per-query list with their exact fp32 distances (scan v2's
+// arithmetic, computed in scan4's epilogue); rescore_kernel selects the k
+// best by (distance, row).  A query whose
 // list overflows V4_CAP (or whose k-th distance is shared by more than
-// V4_SCAP rows) raises a flag and the exact scan v3 + merge, launched behind
+// V4_SCAP rows) raises a flag and the exact scan v2 + merge, launched behind
 // it and gated on the flag, recomputes the batch.
 constexpr float V4_EPS = 0.004f;
 #ifndef V4_S_OVR
@@ -1446,7 +1450,7 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       // bound on every query's k-th best -- the sample's, or the 512-row one
       // if pass 1 overflowed)
     }
-    if (v4 || (Q >= MFMA_MIN_Q && d % 16 == 0)) {   // (v4: its gated exact fallback, any Q)
+    if (!v4 && Q >= MFMA_MIN_Q && d % 16 == 0) {
       const int qtiles = (int)cdiv(Q, K3_QT);
       const int64_t blocks = rup(ns, 8) * qtiles;
       switch (d / 16) {
@@ -1461,20 +1465,23 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       DCNR_LAUNCH_CHECK();
       return merge_lists(cands, Q, ns, k, idx, dist, s, gate);
     }
+    // scan v2: the exact VALU scan -- and, gated, v4's fallback when a list
+    // overflowed (the same distance arithmetic as v4's rescoring, so a batch
+    // that falls back still returns what v4 or v2 alone would)
     const int qtiles = (int)cdiv(Q, K2_QT);
     const int64_t blocks = rup(ns, 8) * qtiles;
     switch (d / 4) {
 #define CASE(n)                                                                                  \
   case n:                                                                                        \
     hipLaunchKernelGGL(scan2_kernel<n>, dim3((unsigned)blocks), dim3(K2_NT), 0, s, t, inv, N, qn, \
-                       Q, k, rps, ns, qtiles, cands, thr0);                                      \
+                       Q, k, rps, ns, qtiles, cands, thr0, gate);                                \
     break;
       CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
       CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
 #undef CASE
     }
     DCNR_LAUNCH_CHECK();
-    return merge_lists(cands, Q, ns, k, idx, dist, s);
+    return merge_lists(cands, Q, ns, k, idx, dist, s, gate);
   }
   plan(N, Q, k, &ns, &rps);
   dim3 grid(ns, (unsigned)cdiv(Q, QT));
