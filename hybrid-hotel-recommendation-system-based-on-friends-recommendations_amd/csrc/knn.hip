@@ -1305,8 +1305,8 @@ void plan2(int64_t N, int* nslices, int64_t* rows_per_block) {
 }
 
 bool use_v4(int64_t N, int64_t Q, int d, int k) {
-  // Any table size: one of at most V4_S rows is its own sample (pass 1 then
-  // repeats pass 2).  A single query over fewer than V4_Q1_N rows takes scan
+  // Any table size: one of at most V4_S rows is its own sample (pass 1 is
+  // then the whole search).  A single query over fewer than V4_Q1_N rows takes scan
   // v2, whose one pass beats v4's fixed chain (29 vs 50 us at 20000 rows, 65
   // vs 61 at 1M); v4's exact distances use v2's arithmetic, so the choice
   // never changes an answer.
@@ -1435,17 +1435,21 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       // pass 2 over the whole table
       CASES4(NQS, gs, NS, RPB_S)
       DCNR_LAUNCH_CHECK();
-      hipLaunchKernelGGL((rescore_kernel<true>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k,
-                         nullptr, nullptr, gate, thr0);
-      DCNR_LAUNCH_CHECK();
-      CASES4(NQ, g4, N, rpb)
-#undef CASES4
-#undef CASE4
-#undef SCAN4
-      DCNR_LAUNCH_CHECK();
+      if (NS < N) {
+        hipLaunchKernelGGL((rescore_kernel<true>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k,
+                           nullptr, nullptr, gate, thr0);
+        DCNR_LAUNCH_CHECK();
+        CASES4(NQ, g4, N, rpb)
+        DCNR_LAUNCH_CHECK();
+      }
+      // (a table of at most V4_S rows: pass 1 covered every row under a valid
+      // bound, so its lists already hold the answer)
       hipLaunchKernelGGL((rescore_kernel<false>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k,
                          idx, dist, gate, nullptr);
       DCNR_LAUNCH_CHECK();
+#undef CASES4
+#undef CASE4
+#undef SCAN4
       // (the exact fallback below admits rows under the same thr0: an upper
       // bound on every query's k-th best -- the sample's, or the 512-row one
       // if pass 1 overflowed)
