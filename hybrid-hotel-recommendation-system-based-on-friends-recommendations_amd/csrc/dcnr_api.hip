@@ -120,6 +120,19 @@ constexpr unsigned SYNC_EV = hipEventDisableTiming | (DCNR_EV_NOFENCE ? hipEvent
 #ifndef DW_WG_BLOCKS
 #define DW_WG_BLOCKS 0
 #endif
+// bf16 train: the backward's dt2 / dt1 buffers alternate between two sets by
+// block parity, so a main-stream writer of one never waits for the side
+// stream's weight-gradient GEMM of the block just before (lab knob: 0 = one
+// shared set, the round-2 pipe that waited on the previous call)
+#ifndef DW_DOUBLE_BUF
+#define DW_DOUBLE_BUF 1
+#endif
+// BN statistics reduced + finalised by the last workgroup of the producing
+// GEMM (no SyncBN hook): one launch less per BatchNorm layer (lab knob: 0 =
+// separate reduce launch)
+#ifndef WS_FUSE_RED
+#define WS_FUSE_RED 1
+#endif
 
 // One side stream per device (created on first use, never destroyed) for the
 // backward's work that does not depend on the deep tower; fork/join events
@@ -300,11 +313,13 @@ struct Layout {
   void* a1;                 // eval: BN1/ReLU output scratch; train: backward scratch (dt1)
   void* a1s[MAX_RES];       // train: each block's dropout(relu(BN1(t1))), saved for dW2
   float* zc; float* zdeep;
+  float* headp;             // eval: [head parts][B] deep-head partial dots (null: row_dot)
   BnBufs bn[2 * MAX_RES];
   float* part; double* sums; float* coef;
   double* red2; int* red_cnt;   // reduce_fused scratch (counters zeroed by pack_all)
   // backward
   void* G; void* dt2; void* du; void* da;
+  void* dt2b; void* dt1b;   // second dt2 / dt1 set (bf16 train, odd blocks); null: one set
   // per-block backward buffers: all alias G/dt2/du/da/a1 unless
   // DCNR_FLAG_KEEP_INTERMEDIATES gives each block its own
   void* duk[MAX_RES]; void* dt2k[MAX_RES]; void* dak[MAX_RES]; void* dt1k[MAX_RES];
@@ -328,6 +343,8 @@ bool masks_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && d.Hp % 32 == 0
 // embedding table's segment of a row is line-aligned for embed_bwd.hip
 int dq_of(const Dims& d) { return (int)rup(d.Dp, 32); }
 bool keep_of(const dcnr_model_desc* desc) { return (desc->flags & DCNR_FLAG_KEEP_INTERMEDIATES) != 0; }
+
+bool eval_fuse_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && gemm_ws_supported(d.Hp, d.Hp); }
 
 Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = false) {
   Layout L;
@@ -369,6 +386,8 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
   }
   L.zc = (float*)b.take(B * 4);
   L.zdeep = (float*)b.take(B * 4);
+  if (!train && !keep && eval_fuse_ok(d))   // the last eval GEMM's head partials
+    L.headp = (float*)b.take((size_t)B * gemm_ws_head_parts(d.Hp) * 4);
   for (int i = 0; i < 2 * d.R; ++i) {
     L.bn[i].scale = (float*)b.take(d.Hp * 4);
     L.bn[i].shift = (float*)b.take(d.Hp * 4);
@@ -407,11 +426,16 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
       L.emb.tmp_bytes = emb_sort_tmp_bytes(d.rows, d.widths, 2 + d.K, B);
       L.emb.tmp = b.take(L.emb.tmp_bytes);
     }
+    if (DW_DOUBLE_BUF && !keep && d.prec == DCNR_PREC_BF16 && d.R > 1) {
+      L.dt2b = b.take(act);
+      L.dt1b = b.take(act);
+    }
     for (int j = 0; j < d.R; ++j) {
+      const bool odd = (j & 1) && L.dt2b;
       L.duk[j] = keep ? b.take(act) : L.du;
-      L.dt2k[j] = keep ? b.take(act) : L.dt2;
+      L.dt2k[j] = keep ? b.take(act) : odd ? L.dt2b : L.dt2;
       L.dak[j] = keep ? b.take(act) : L.da;
-      L.dt1k[j] = keep ? b.take(act) : L.a1;
+      L.dt1k[j] = keep ? b.take(act) : odd ? L.dt1b : L.a1;
     }
 
   }
@@ -575,27 +599,35 @@ bool epi_stats_ok(const Dims& d) { return masks_ok(d) && gemm_ws_supported(d.Hp,
 // Eval forward with BatchNorm (running statistics) + ReLU (+ residual) in the
 // streaming GEMM's epilogue: no t1/t2 round trip through HBM and no rowwise
 // passes (bf16, gemm_ws shapes).
-bool eval_fuse_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && gemm_ws_supported(d.Hp, d.Hp); }
 
-// out = relu((A W^T + b) * bn.scale + bn.shift [+ R])
+// out = relu((A W^T + b) * bn.scale + bn.shift [+ R]); with rs (the layer's
+// gamma, beta, running mean, running var) the kernel makes scale / shift
+// itself; with headp (needs R) no out: the deep head's partial dots with wf
 dcnr_status linear_bn_relu(const Dims& d, const void* A, const void* W, const float* bias,
-                           const BnBufs& bn, const void* R, void* out, int64_t B, hipStream_t s) {
+                           const BnBufs& bn, const void* R, void* out, int64_t B, hipStream_t s,
+                           const float* const* rs = nullptr, const float* wf = nullptr,
+                           float* headp = nullptr) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
   a.X = (const bf16*)A; a.ldx = d.Hp; a.M = B; a.K = d.Hp;
-  a.W = (const bf16*)W; a.ldw = d.Hp; a.N = d.Hp;
+  a.W = (const bf16*)W; a.ldw = d.Hp; a.N = d.Hp; a.Nr = d.H;
   a.C = out; a.ldc = d.Hp; a.bias = bias;
   a.R = R; a.ldr = d.Hp;
   a.bn_scale = bn.scale; a.bn_shift = bn.shift;
-  return gemm_ws(R ? NT_EPI_BN_RESID_RELU : NT_EPI_BN_RELU, a, s);
+  if (rs) { a.bn_g = rs[0]; a.bn_b = rs[1]; a.bn_rm = rs[2]; a.bn_rv = rs[3]; }
+  a.wf = wf; a.headp = headp;
+  return gemm_ws(headp ? NT_EPI_BN_RESID_RELU_HEAD : R ? NT_EPI_BN_RESID_RELU : NT_EPI_BN_RELU, a, s);
 }
 
 // t = A W^T + b  and  part = BN column partials of t, shifted by b (nc rows)
+// (rf: reduce and finalise the partials in the same launch when it can; *nc
+// is then -1)
 dcnr_status linear_fwd_stats(const Dims& d, const Layout& L, const void* A, int lda, const void* W,
                              int K, const float* bias, void* out, int64_t B, int* nc,
-                             hipStream_t s) {
+                             hipStream_t s, const RedFinal* rf = nullptr) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
+  if (rf) { a.fuse_red = WS_FUSE_RED; a.rf = *rf; a.Nr = d.H; }
   a.X = (const bf16*)A; a.ldx = lda; a.M = B; a.K = K;
   a.W = (const bf16*)W; a.ldw = K; a.N = d.Hp;
   a.C = out; a.ldc = d.Hp; a.bias = bias;
@@ -606,9 +638,11 @@ dcnr_status linear_fwd_stats(const Dims& d, const Layout& L, const void* A, int 
 // C = mask(H) * (X W^T [+ R]) and part = [sum C, sum C*xhat(T)] (BN backward)
 dcnr_status linear_dx_bn(const Dims& d, const Layout& L, int epi, const void* X, const void* Wt,
                          const void* R, void* C, const uint8_t* Hbits, float hscale,
-                         const void* T, const BnBufs& bn, int64_t B, int* nc, hipStream_t s) {
+                         const void* T, const BnBufs& bn, int64_t B, int* nc, hipStream_t s,
+                         const RedFinal* rf = nullptr) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
+  if (rf) { a.fuse_red = WS_FUSE_RED; a.rf = *rf; a.Nr = d.H; }
   a.X = (const bf16*)X; a.ldx = d.Hp; a.M = B; a.K = d.Hp;
   a.W = (const bf16*)Wt; a.ldw = d.Hp; a.N = d.Hp;
   a.C = C; a.ldc = d.Hp;
@@ -647,27 +681,33 @@ dcnr_status wgrad_bf16(const void* dY, int64_t ldy, int N, const void* X, int64_
 // The backward's bf16 weight gradients run on the side stream: each call's
 // gemm_dw + split-K reduce are ordered after the main stream's work so far
 // (its dY is complete) and overlap the main stream's next dX GEMM and BN
-// passes. The main stream's next writer of a dY buffer comes after the next
-// call, which first waits for the previous call's GEMM, so the operands stay
-// alive; the reduces share one slab because they are serialised on the side
-// stream. join() orders the main stream after all of it. Same kernels, same
-// order per output: the gradients are unchanged (same-box A/B in DESIGN.md).
+// passes. The operands stay alive because call n's enter() orders the main
+// stream after call n-lag's GEMM: with one shared dt2 / dt1 set (lag 1) the
+// next writer of a call's dY comes after the next call; with the two
+// alternating sets (lag 3) it comes after call n+3 (the writer of call n's dt2
+// is block j-2's BN2 apply, which follows block j-1's dW1 call). The reduces
+// share one slab because they are serialised on the side stream. join()
+// orders the main stream after all of it. Same kernels, same order per
+// output: the gradients are unchanged.
 struct DwPipe {
+  static constexpr int RING = 4;
   hipStream_t side = nullptr, main = nullptr;
-  hipEvent_t in_ev = nullptr, dw_ev = nullptr, done_ev = nullptr;
-  int calls = 0;
+  hipEvent_t in_ev = nullptr, done_ev = nullptr;
+  hipEvent_t dw_ev[RING] = {};
+  int calls = 0, lag = 1;
   bool pending = false;   // side work enqueued since the last join
-  dcnr_status init(hipStream_t side_stream) {
+  dcnr_status init(hipStream_t side_stream, int lag_calls) {
     side = side_stream;
+    lag = lag_calls;
     DCNR_HIP(hipEventCreateWithFlags(&in_ev, SYNC_EV));
-    DCNR_HIP(hipEventCreateWithFlags(&dw_ev, SYNC_EV));
     DCNR_HIP(hipEventCreateWithFlags(&done_ev, SYNC_EV));
+    for (auto& e : dw_ev) DCNR_HIP(hipEventCreateWithFlags(&e, SYNC_EV));
     return DCNR_OK;
   }
   // order the side stream after the main stream's work so far (and the main
-  // stream after the previous call's GEMM, see above)
+  // stream after call (calls - lag)'s GEMM, see above)
   dcnr_status enter(hipStream_t main_s) {
-    if (calls) DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev, 0));
+    if (calls >= lag) DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev[(calls - lag) % RING], 0));
     DCNR_HIP(hipEventRecord(in_ev, main_s));
     DCNR_HIP(hipStreamWaitEvent(side, in_ev, 0));
     main = main_s;
@@ -678,7 +718,7 @@ struct DwPipe {
                     int Kc, int64_t B, float* out, int Nr, int Kr, int accumulate, hipStream_t main_s,
                     int wg_target) {
     TRY(enter(main_s));
-    ++calls;
+    const int call = calls++;
     hipStream_t s = side;   // TRYB launches and times on the side stream
     // (the full-chip split count: 32 / 16 splits, leaving CUs to the main
     // stream and halving the slab, measured 2 % / 21 % slower per step)
@@ -694,7 +734,7 @@ struct DwPipe {
     a.Btot = B; a.k_per_split = rup(cdiv(B, S), 64);
     a.N = N; a.K = Kc; a.splits = S;
     TRYB(DCNR_K_GEMM_DW, 2.0 * B * (N + Kc) + 4.0 * Nr * Kr * (accumulate ? 2 : 1), gemm_dw(a, s));
-    DCNR_HIP(hipEventRecord(dw_ev, s));
+    DCNR_HIP(hipEventRecord(dw_ev[call % RING], s));
     TRYB(DCNR_K_REDUCE, 4.0 * S * N * Kc + 4.0 * Nr * Kr * (accumulate ? 2 : 1),
          splitk_reduce_t(L.slab, S, (int64_t)N * Kc, N, Nr, Kr, out, accumulate, s));
     return DCNR_OK;
@@ -711,7 +751,9 @@ struct DwPipe {
       (void)hipEventRecord(done_ev, side);
       (void)hipStreamWaitEvent(main, done_ev, 0);
     }
-    for (auto e : {in_ev, dw_ev, done_ev})
+    for (auto e : {in_ev, done_ev})
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : dw_ev)
       if (e) (void)hipEventDestroy(e);
   }
 };
@@ -788,6 +830,7 @@ dcnr_status bn_layer_fwd(const dcnr_model_desc* desc, const Dims& d, const Layou
                          const BnBufs& bb, hipStream_t s, int nc_pre = 0,
                          const float* shiftf = nullptr) {
   BnFinal f{gamma, beta, rm, rv, nbt, bb.scale, bb.shift, bb.mean, bb.invstd};
+  if (train && nc_pre < 0) return DCNR_OK;   // reduced and finalised by the GEMM launch
   if (train) {
     int nc = nc_pre;
     const void* shift = nc_pre ? nullptr : t;
@@ -816,6 +859,7 @@ dcnr_status bn_bwd_reduce(const dcnr_model_desc* desc, const Dims& d, const Layo
                           float* dgamma, float* dbeta, float* dwf, float* dbias_pre,
                           int accumulate, hipStream_t s) {
   const int Hp = d.Hp, H = d.H;
+  if (nc < 0) return DCNR_OK;   // reduced and finalised by the dX GEMM launch
   if (!desc->bn_allreduce) {
     RedFinal rf = bn_bwd_rf(L, B, gamma, invstd, dgamma, dbeta, dwf, dbias_pre, accumulate);
     TRYP(DCNR_K_REDUCE, reduce_fused(DCNR_PREC_FP32, L.part, nc, NK, Hp, H, nullptr, rf, s));
@@ -999,6 +1043,24 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   TRYB(DCNR_K_GEMM_FWD, (double)B * d.Dp * d.es + act_b(d, B) + w_b(d, d.Dp),
        linear_fwd(d, L.x0, d.Dp, L.W0p, d.Dp, L.b0p, L.h[0], B, s));
   if (!train && eval_fuse_ok(d)) {
+    if (L.headp) {
+      // each GEMM makes its layer's running-stat affine itself; the last
+      // block's GEMM ends in the deep head dot (no h_R), summed with zc + bf
+      for (int j = 0; j < d.R; ++j) {
+        const auto& Bk = P.blk[j];
+        const float* rs1[4] = {Bk.g1, Bk.be1, Bk.rm1, Bk.rv1};
+        const float* rs2[4] = {Bk.g2, Bk.be2, Bk.rm2, Bk.rv2};
+        const bool last = j == d.R - 1;
+        TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
+             linear_bn_relu(d, L.h[j], L.W1p[j], L.b1p[j], L.bn[2 * j], nullptr, L.a1, B, s, rs1));
+        TRYB(DCNR_K_GEMM_FWD, (last ? 2 * act_b(d, B) + 4.0 * B * gemm_ws_head_parts(d.Hp) : 3 * act_b(d, B)) + w_b(d, d.Hp),
+             linear_bn_relu(d, L.a1, L.W2p[j], L.b2p[j], L.bn[2 * j + 1], L.h[j], last ? nullptr : L.h[j + 1],
+                            B, s, rs2, last ? P.wf : nullptr, last ? L.headp : nullptr));
+      }
+      const int np = gemm_ws_head_parts(d.Hp);
+      TRYB(DCNR_K_HEAD, (4.0 * np + 8.0) * B, head_parts(L.headp, np, L.zc, P.bf, B, logits, s));
+      return DCNR_OK;
+    }
     // every layer's running-stat affine in one launch
     BnEvalBatch eb;
     memset(&eb, 0, sizeof(eb));
@@ -1026,9 +1088,16 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     const auto& Bk = P.blk[j];
     const bool fuse = train && epi_stats_ok(d);   // BN partials from the GEMM epilogue
     int nc = 0;
+    // local BN: the GEMM's last workgroups reduce and finalise the statistics
+    RedFinal rf1 = bn_fwd_rf(L, B, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1, L.bn[2 * j]);
+    RedFinal rf2 = bn_fwd_rf(L, B, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2, L.bn[2 * j + 1]);
+    rf1.shiftf = L.b1p[j];
+    rf2.shiftf = L.b2p[j];
+    const bool local = !desc->bn_allreduce;
     if (fuse)
       TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
-           linear_fwd_stats(d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, &nc, s));
+           linear_fwd_stats(d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, &nc, s,
+                            local ? &rf1 : nullptr));
     else
       TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
            linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
@@ -1039,7 +1108,8 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
                      dropout_seed, j, s, train ? L.mask_a1[j] : nullptr));
     if (fuse)
       TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
-           linear_fwd_stats(d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, &nc, s));
+           linear_fwd_stats(d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, &nc, s,
+                            local ? &rf2 : nullptr));
     else
       TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
            linear_fwd(d, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
@@ -1133,13 +1203,15 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   // alone, on the main stream, as before the overlap -- except in profile
   // mode 2, which times the side stream's gemm_dw launches in place)
   if (d.prec == DCNR_PREC_BF16 && (!g_prof || g_prof_mode == 2)) {
-    TRY(dwp.init(sj.side));
+    // lag 3 needs the alternating dt2 / dt1 sets (or one set per block)
+    TRY(dwp.init(sj.side, L.dt2b || keep_of(desc) ? 3 : 1));
     pipe = &dwp;
   }
 
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   const bool fuse = epi_stats_ok(d);   // BN partials from the dX GEMM epilogues
-  int nc_du = 0;   // > 0: L.du and its BN2 partials were made by the previous dX GEMM
+  int nc_du = 0;   // != 0: L.du and its BN2 partials (> 0) or finalised BN2 backward (-1)
+                   // were made by the previous dX GEMM
   for (int j = d.R - 1; j >= 0; --j) {
     const auto& Bk = P.blk[j];
     auto& Gk = Gr.blk[j];
@@ -1170,9 +1242,10 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       // dy1 = (dt2 W2) * [a1 != 0] / (1-p): relu and dropout masks from the
       // saved activation, BN1 partials (and, without SyncBN, its backward
       // coefficients and dgamma/dbeta) in the same pass
+      const RedFinal rf = bn_bwd_rf(L, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1, accumulate);
       TRYB(DCNR_K_GEMM_DX, 3 * act_b(d, B) + mask_b(d, B) + w_b(d, d.Hp), linear_dx_bn(d, L, NT_EPI_DROP_BN, dt2, L.W2t[j], nullptr, da,
                                         L.mask_a1[j], p > 0.f ? 1.f / (1.f - p) : 1.f, L.t1[j],
-                                        bn1, B, &nc, s));
+                                        bn1, B, &nc, s, desc->bn_allreduce ? nullptr : &rf));
     } else {
       GemmArgs g;
       memset(&g, 0, sizeof(g));
@@ -1194,8 +1267,11 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       // (in place over this block's du, the residual operand, unless
       // KEEP_INTERMEDIATES) and the partials
       const BnBufs& bp = L.bn[2 * (j - 1) + 1];
+      const RedFinal rf = bn_bwd_rf(L, B, P.blk[j - 1].g2, bp.invstd, Gr.blk[j - 1].g2,
+                                    Gr.blk[j - 1].be2, nullptr, Gr.blk[j - 1].b2, accumulate);
       TRYB(DCNR_K_GEMM_DX, 4 * act_b(d, B) + mask_b(d, B) + w_b(d, d.Hp), linear_dx_bn(d, L, NT_EPI_RESID_BN, dt1, L.W1t[j], du, L.duk[j - 1],
-                                        L.mask_h[j], 1.f, L.t2[j - 1], bp, B, &nc_du, s));
+                                        L.mask_h[j], 1.f, L.t2[j - 1], bp, B, &nc_du, s,
+                                        desc->bn_allreduce ? nullptr : &rf));
       Gin = L.duk[j - 1];
     } else {
       GemmArgs g;

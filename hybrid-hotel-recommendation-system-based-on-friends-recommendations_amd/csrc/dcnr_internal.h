@@ -335,6 +335,10 @@ enum NtEpi : int {
   // bn_shift = the running-stat affine of bn_finalize2):
   NT_EPI_BN_RELU = 6,        // C = relu((acc + bias) * sc + sh)
   NT_EPI_BN_RESID_RELU = 7,  // C = relu((acc + bias) * sc + sh + R)
+  // the eval forward's last block: no C; the deep head dot of the bf16-rounded
+  // relu((acc + bias) * sc + sh + R) with wf, one partial per row per wave of
+  // each column slice: headp[slice * 8 + wave][m] (summed by head_parts)
+  NT_EPI_BN_RESID_RELU_HEAD = 8,
 };
 // (c is the stored bf16 value; xhat(T) = (T[m][n] - mean[n]) * invstd[n])
 struct NtArgs {
@@ -348,13 +352,29 @@ struct NtArgs {
                                                     // c%32 of word [m][c/32] = keep column c
   const bf16* T; int64_t ldt;                       // BN input for xhat
   const float* mean; const float* invstd;
-  const float* bn_scale; const float* bn_shift;     // BN_RELU, BN_RESID_RELU
+  const float* bn_scale; const float* bn_shift;     // BN_RELU, BN_RESID_RELU(_HEAD)
+  // eval BN from the running statistics (bn_rm != null): the kernel computes
+  // scale / shift itself (bn_eval_multi_kernel's arithmetic) instead of reading
+  // bn_scale / bn_shift
+  const float* bn_g; const float* bn_b; const float* bn_rm; const float* bn_rv;
+  const float* wf; float* headp;                    // BN_RESID_RELU_HEAD (wf: Nr entries)
   float* part;                                      // column partials (stats epilogues)
+  // stats epilogues: with fuse_red the launch's last workgroup per column
+  // slice also sums the partial rows (reduce_small's fixed order) and runs
+  // red_finalize(rf) on them (columns >= Nr are padding); gemm_ws then
+  // reports nparts = -1 (nothing left to reduce)
+  int fuse_red; int Nr; RedFinal rf;
   int nslices, groups; int64_t mtiles;   // filled by gemm_ws
 };
+// hand-off counter slots of gemm_ws's in-launch reductions (above the ones
+// reduce_fused uses)
+constexpr int CNT_WS_BASE = 256;
 bool gemm_ws_supported(int64_t K, int64_t N);
-// nparts (stats epilogues): rows of part written (the nchunks of reduce_fused)
+// nparts (stats epilogues): rows of part written (the nchunks of reduce_fused),
+// or -1 when a.fuse_red reduced and finalised them in the launch
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
+// head partials of NT_EPI_BN_RESID_RELU_HEAD: rows of headp written (0: unsupported shape)
+int gemm_ws_head_parts(int64_t N);
 inline bool nt_epi_stats(int epi) { return epi >= NT_EPI_BIAS_STATS && epi <= NT_EPI_DROP_BN; }
 
 // bf16 weight-gradient GEMM (gemm_dw.hip): slab[split][n][k] = sum over the
@@ -536,6 +556,9 @@ dcnr_status bn_add_relu_head(int precision, const void* t, const void* x, void* 
                              float* logits, hipStream_t s);
 dcnr_status row_dot(int precision, const void* X, int ld, int N, const float* w, int64_t B,
                     float* out, hipStream_t s);
+// logits[b] = sum_p part[p][b] (p = 0..np-1, fixed order) + zc[b] + bf
+dcnr_status head_parts(const float* part, int np, const float* zc, const float* bf, int64_t B,
+                       float* logits, hipStream_t s);
 dcnr_status head_logits(const float* zdeep, const float* zc, const float* bf, int64_t B,
                         float* logits, hipStream_t s);
 size_t bce_ws_bytes();

@@ -492,13 +492,21 @@ __global__ __launch_bounds__(NT) void pack_kernel(PackBatch pb) {
   T* dst = (T*)d.dst;
   const int cg = d.ld >> 3;
   const int tot = d.rows_p * cg;
+  const bool vec = d.src && d.cols % 4 == 0 && ((uintptr_t)d.src & 15) == 0;
   for (int i = blockIdx.x * NT + threadIdx.x; i < tot; i += gridDim.x * NT) {
     const int r = i / cg, c0 = (i - r * cg) * 8;
     float v[8];
+    if (vec && r < d.rows && c0 + 8 <= d.cols) {   // two 16-B loads
+      const f32x4* q = reinterpret_cast<const f32x4*>(d.src + (int64_t)r * d.cols + c0);
+      const f32x4 a = q[0], b = q[1];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const int c = c0 + k;
-      v[k] = (r < d.rows && c < d.cols) ? d.src[(int64_t)r * d.cols + c] : 0.f;
+      for (int k = 0; k < 4; ++k) { v[k] = a[k]; v[4 + k] = b[k]; }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int c = c0 + k;
+        v[k] = (r < d.rows && c < d.cols) ? d.src[(int64_t)r * d.cols + c] : 0.f;
+      }
     }
     T* p = dst + (int64_t)r * d.ld + c0;
     if constexpr (sizeof(T) == 2) {
@@ -698,7 +706,12 @@ dcnr_status pack_weights(int precision, const PackBatch& pb, hipStream_t s) {
       set_error("pack: leading dimension %d not a multiple of 8", pb.d[i].ld);
       return DCNR_UNSUPPORTED_SHAPE;
     }
-  dim3 grid(64, pb.n);
+  // one 8-column group per thread for a 512 x 512 matrix (the transposes'
+  // 64 x 64 tiles need 64 blocks)
+  int gx = 64;
+  for (int i = 0; i < pb.n; ++i)
+    gx = std::max<int>(gx, (int)std::min<int64_t>(256, cdiv((int64_t)pb.d[i].rows_p * (pb.d[i].ld >> 3), NT)));
+  dim3 grid(gx, pb.n);
   if (precision == DCNR_PREC_BF16) hipLaunchKernelGGL(pack_kernel<bf16>, grid, dim3(NT), 0, s, pb);
   else hipLaunchKernelGGL(pack_kernel<float>, grid, dim3(NT), 0, s, pb);
   DCNR_LAUNCH_CHECK();

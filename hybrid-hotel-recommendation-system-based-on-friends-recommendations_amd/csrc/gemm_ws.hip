@@ -87,7 +87,8 @@ template <int KTP, int EPI> constexpr int ws_tm() {
          : WS_TM_OVR && KTP == 16 ? WS_TM_OVR : (EPI <= NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS ? 64 : 32);
 }
 template <int EPI> constexpr bool ws_ops_early() {
-  return EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN || EPI == NT_EPI_BN_RESID_RELU;
+  return EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN || EPI == NT_EPI_BN_RESID_RELU ||
+         EPI == NT_EPI_BN_RESID_RELU_HEAD;
 }
 // X-tile buffers in the LDS ring: one tile in flight while one is consumed.
 template <int KTP, int EPI> constexpr int ws_nb() { return WS_NB_OVR && KTP == 16 ? WS_NB_OVR : 2; }
@@ -99,7 +100,7 @@ template <int KTP, int TM, int NB = 2> struct WsCfg {
   static constexpr int RPD = 1024 / P;                    // rows per DMA wave-instruction
   static constexpr int DPW = TM / RPD / WS_WAVES;         // DMAs per wave per tile
   static constexpr int RB = TM / 16;                      // 16-row blocks per tile
-  static constexpr size_t LDS_BYTES = NB * (size_t)TILE + 3 * WS_TN * 4 + 16;  // + hand-off flag
+  static constexpr size_t LDS_BYTES = NB * (size_t)TILE + 4 * WS_TN * 4 + 16;  // + hand-off flag
   static_assert(TM % (RPD * WS_WAVES) == 0 && TM % 16 == 0, "tile rows");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
@@ -149,6 +150,43 @@ __device__ __forceinline__ void issue_tile(u32x4 xr, int64_t ldx, int K, uint32_
   }
 }
 
+// In-launch BN reduction (stats epilogues with a.fuse_red): the last
+// workgroup of each column slice to store its partial row sums the slice's
+// partial rows in reduce_small_kernel's fixed order (8 row groups of 32 rows,
+// each summed in fp64 from 0, the groups added in order: the same bits as the
+// separate reduce launch) and hands the column sums to red_finalize -- one
+// launch less per BatchNorm layer.  Thread (c, k): column n0 + c, sum k.
+__device__ __forceinline__ void ws_reduce_tail(const NtArgs& a, int slice, int n0, char* lds) {
+  int* flag = reinterpret_cast<int*>(lds);
+  if (!last_arriver(&a.rf.counter[CNT_WS_BASE + slice], a.groups, flag)) return;
+  const int tid = threadIdx.x, c = tid % WS_TN, k = tid / WS_TN;
+  const int n = n0 + c;
+  const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.part, (int64_t)a.groups * 2 * a.N * 4);
+  constexpr int U = 32;
+  double tot = 0.0;
+#pragma unroll 1
+  for (int g = 0; g < 8; ++g) {
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = g * U + u;
+      const bool ok = n < a.N && row < a.groups;
+      v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, ok ? ((row * 2 + k) * a.N + n) * 4 : OOR, 0, 0));
+    }
+    double gs = 0.0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) gs += (double)v[u];
+    tot += gs;
+  }
+  double* red = reinterpret_cast<double*>(lds + 64);
+  red[tid] = tot;
+  __syncthreads();
+  if (k != 0 || n >= a.N) return;
+  const bool has_k = a.rf.shiftf != nullptr;
+  const double K = has_k ? (double)a.rf.shiftf[n] : 0.0;
+  red_finalize(a.rf, n, a.N, a.Nr, tot, red[WS_TN + c], 0.0, has_k, K);
+}
+
 template <int KTP, int EPI>
 __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs a) {
   constexpr int WS_TM = ws_tm<KTP, EPI>();
@@ -156,7 +194,8 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
   using C = WsCfg<KTP, WS_TM, NB>;
   constexpr int WS_RB = C::RB;
   constexpr bool STATS = EPI >= NT_EPI_BIAS_STATS && EPI <= NT_EPI_DROP_BN;
-  constexpr bool HAS_R = EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_BN_RESID_RELU;
+  constexpr bool HEAD = EPI == NT_EPI_BN_RESID_RELU_HEAD;
+  constexpr bool HAS_R = EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_BN_RESID_RELU || HEAD;
   constexpr bool HAS_HT = EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN;
   constexpr bool HAS_BIAS = EPI <= NT_EPI_BIAS_STATS || EPI >= NT_EPI_BN_RELU;
   constexpr bool HAS_SS = EPI >= NT_EPI_BN_RELU;   // eval BN affine + ReLU
@@ -205,6 +244,7 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
   float* bias_s = reinterpret_cast<float*>(lds + NB * C::TILE);
   float* nmi_s = bias_s + WS_TN;
   float* istd_s = bias_s + 2 * WS_TN;
+  float* wf_s = bias_s + 3 * WS_TN;   // HEAD: the slice's deep head weights
   for (int c = tid; c < WS_TN; c += WS_NT) {
     const int n = n0 + c;
     bias_s[c] = (HAS_BIAS && a.bias && n < a.N) ? a.bias[n] : 0.f;
@@ -213,9 +253,22 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
       istd_s[c] = n < a.N ? a.invstd[n] : 0.f;
     }
     if constexpr (HAS_SS) {
-      nmi_s[c] = n < a.N ? a.bn_scale[n] : 0.f;
-      istd_s[c] = n < a.N ? a.bn_shift[n] : 0.f;
+      if (a.bn_rm) {   // running-stat affine, as bn_eval_multi_kernel (pads: 0)
+        float sc = 0.f, sh = 0.f;
+        if (n < a.Nr) {
+          const double mean = a.bn_rm[n], var = a.bn_rv[n];
+          const float inv = (float)(1.0 / sqrt(var + (double)BN_EPS));
+          sc = a.bn_g[n] * inv;
+          sh = a.bn_b[n] - (float)mean * sc;
+        }
+        nmi_s[c] = sc;
+        istd_s[c] = sh;
+      } else {
+        nmi_s[c] = n < a.N ? a.bn_scale[n] : 0.f;
+        istd_s[c] = n < a.N ? a.bn_shift[n] : 0.f;
+      }
     }
+    if constexpr (HEAD) wf_s[c] = n < a.Nr ? a.wf[n] : 0.f;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -230,6 +283,8 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
       (void*)a.Hb, (short)0, HAS_HT ? (int)(a.M * a.ldhb * 4) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.T, (short)0, HAS_HT ? (int)(a.M * a.ldt * 2) : 0, 0x00020000);
+  const __amdgpu_buffer_rsrc_t hp_r = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.headp, (short)0, HEAD ? (int)(a.nslices * WS_WAVES * a.M * 4) : 0, 0x00020000);
 
   // per-lane column partials [sum, sum2][cb][column pair], over all tiles
   f2v st[2][2][2];
@@ -275,6 +330,7 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
       const int slot = WS_OPS_EARLY ? rb : rb & 1;
       u32x2 o[2], rf[2], tf[2];
       u32x4 of[2];
+      float hd = 0.f;   // HEAD: this lane's 8 columns of the row's dot
       if constexpr (HAS_R) to_acc_layout(rv[slot], rf);
       if constexpr (HAS_HT) to_acc_layout(tv[slot], tf);
 #pragma unroll
@@ -308,6 +364,11 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
           v[1] *= a.hscale;
         }
         o[cb] = u32x2{pack2(v[0][0], v[0][1]), pack2(v[1][0], v[1][1])};
+        if constexpr (HEAD) {   // the stored (bf16-rounded) activation, as row_dot reads it
+          const float4 w4 = *reinterpret_cast<const float4*>(wf_s + cl);
+          const f2v c0 = unpack2(o[cb][0]), c1 = unpack2(o[cb][1]);
+          hd += ((c0[0] * w4.x + c0[1] * w4.y) + c1[0] * w4.z) + c1[1] * w4.w;
+        }
         of[cb] = u32x4{__float_as_uint(v[0][0]), __float_as_uint(v[0][1]),
                        __float_as_uint(v[1][0]), __float_as_uint(v[1][1])};
         if constexpr (HAS_HT) {
@@ -346,7 +407,18 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
           }
         }
       }
-      if constexpr (EPI == NT_EPI_F32) {
+      if constexpr (HEAD) {
+        // the row's 4 lanes (q = 0..3, same l15): half-wave then row swap
+        const unsigned u = __float_as_uint(hd);
+        auto h2 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+        const float t = __uint_as_float(h2[0]) + __uint_as_float(h2[1]);
+        const unsigned ut = __float_as_uint(t);
+        auto h4 = __builtin_amdgcn_permlane16_swap(ut, ut, false, false);
+        const float r4 = __uint_as_float(h4[0]) + __uint_as_float(h4[1]);
+        if (q == 0)
+          __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4), hp_r,
+                                                mok ? (int)(((slice * WS_WAVES + wave) * a.M + m) * 4) : OOR, 0, 0);
+      } else if constexpr (EPI == NT_EPI_F32) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
           const int n = nw + cb * 16 + q * 4;
@@ -573,6 +645,7 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
     const int k = (lane >> 2) & 1, cb = (lane >> 3) & 1, r = 2 * (lane & 1) + ((lane >> 1) & 1);
     const int n = nw + cb * 16 + q * 4 + r;
     if (n < a.N) a.part[((int64_t)group * 2 + k) * a.N + n] = x[0];
+    if (a.fuse_red) ws_reduce_tail(a, slice, n0, lds);
   }
 }
 
@@ -587,6 +660,7 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
                                            a.T ? a.ldt : 0});
   const int64_t mchunk = std::max<int64_t>(WS_TM, ((int64_t(1) << 29) / (maxld * 2)) / WS_TM * WS_TM);
   if (a.M > mchunk) {
+    a.fuse_red = 0;   // partial rows of several launches: reduced by the caller
     int total = 0;
     for (int64_t m0 = 0; m0 < a.M; m0 += mchunk) {
       NtArgs b = a;
@@ -612,6 +686,9 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   if (need < grid) grid = (int)(cdiv(need, unit) * unit);
   a.groups = grid / a.nslices;
   if (nparts) *nparts = a.groups;
+  if (a.fuse_red && !(WS_NT == 2 * WS_TN && a.groups <= 256 && a.nslices <= CNT_SLOTS - CNT_WS_BASE))
+    a.fuse_red = 0;
+  if (a.fuse_red && nparts) *nparts = -1;
   hipLaunchKernelGGL((gemm_ws_kernel<KTP, EPI>), dim3(grid), dim3(WS_NT), C::LDS_BYTES, s, a);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
@@ -627,6 +704,7 @@ dcnr_status dispatch_ws(const NtArgs& a, hipStream_t s, int* nparts) {
 }  // namespace
 
 bool gemm_ws_supported(int64_t K, int64_t N) { return K <= 512 && K % 8 == 0 && N % 8 == 0; }
+int gemm_ws_head_parts(int64_t N) { return N % 8 == 0 && N <= 4096 ? (int)cdiv(N, WS_TN) * WS_WAVES : 0; }
 
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
   if (nparts) *nparts = 0;
@@ -634,7 +712,10 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
   const bool ht = epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN;
   if (!gemm_ws_supported(a.K, a.N) || a.ldx % 8 || a.ldw % 8 || a.ldc % 8 ||
       ((epi == NT_EPI_RESID || epi == NT_EPI_RESID_BN || epi == NT_EPI_BN_RESID_RELU) && (a.ldr % 8 || !a.R)) ||
-      (epi >= NT_EPI_BN_RELU && (!a.bn_scale || !a.bn_shift)) ||
+      (epi >= NT_EPI_BN_RELU && !a.bn_rm && (!a.bn_scale || !a.bn_shift)) ||
+      (epi >= NT_EPI_BN_RELU && a.bn_rm && (!a.bn_g || !a.bn_b || !a.bn_rv)) ||
+      (epi == NT_EPI_BN_RESID_RELU_HEAD &&
+       (!a.wf || !a.headp || !gemm_ws_head_parts(a.N) || a.M * gemm_ws_head_parts(a.N) * 4 >= (int64_t(1) << 31))) ||
       (ht && (!a.Hb || !a.T || !a.mean || !a.invstd || a.ldt % 8)) ||
       (nt_epi_stats(epi) && !a.part)) {
     set_error("gemm_ws: unsupported K=%d N=%d / missing epilogue operand", a.K, a.N);
@@ -649,6 +730,7 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
       return dispatch_ws<NT_EPI_RESID_BN>(a, s, nparts);
     case NT_EPI_BN_RELU: return dispatch_ws<NT_EPI_BN_RELU>(a, s, nparts);
     case NT_EPI_BN_RESID_RELU: return dispatch_ws<NT_EPI_BN_RESID_RELU>(a, s, nparts);
+    case NT_EPI_BN_RESID_RELU_HEAD: return dispatch_ws<NT_EPI_BN_RESID_RELU_HEAD>(a, s, nparts);
     case NT_EPI_DROP_BN:
       return dispatch_ws<NT_EPI_DROP_BN>(a, s, nparts);
   }

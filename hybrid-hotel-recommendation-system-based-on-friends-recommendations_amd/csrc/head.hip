@@ -72,6 +72,17 @@ __global__ void logits_kernel(const float* zdeep, const float* zc, const float* 
   if (i < B) z[i] = (zdeep[i] + zc[i]) + bf[0];
 }
 
+// eval head from the last GEMM's per-wave partial dots: z = sum_p part[p][b]
+// (fixed order) + zc + bf
+__global__ void head_parts_kernel(const float* part, int np, const float* zc, const float* bf,
+                                  int64_t B, float* z) {
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  float d = 0.f;
+  for (int p = 0; p < np; ++p) d += part[p * B + i];
+  z[i] = (d + zc[i]) + bf[0];
+}
+
 // stage 1: per block partial sum of the BCE terms (+ dz); stage 2: fixed-order sum
 __global__ __launch_bounds__(NT) void bce_kernel(const float* z, const float* y, int64_t B,
                                                  float* dz, float scale, double* part) {
@@ -173,6 +184,15 @@ dcnr_status head_logits(const float* zdeep, const float* zc, const float* bf, in
   if (B <= 0) return DCNR_OK;
   hipLaunchKernelGGL(logits_kernel, dim3((unsigned)cdiv(B, NT)), dim3(NT), 0, s, zdeep, zc, bf, B,
                      logits);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status head_parts(const float* part, int np, const float* zc, const float* bf, int64_t B,
+                       float* logits, hipStream_t s) {
+  if (B <= 0) return DCNR_OK;
+  hipLaunchKernelGGL(head_parts_kernel, dim3((unsigned)cdiv(B, NT)), dim3(NT), 0, s, part, np, zc, bf,
+                     B, logits);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
