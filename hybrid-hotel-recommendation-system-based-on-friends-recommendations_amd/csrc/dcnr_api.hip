@@ -131,7 +131,7 @@ constexpr unsigned SYNC_EV = hipEventDisableTiming | (DCNR_EV_NOFENCE ? hipEvent
 // GEMM (no SyncBN hook): one launch less per BatchNorm layer (lab knob: 0 =
 // separate reduce launch)
 #ifndef WS_FUSE_RED
-#define WS_FUSE_RED 1
+#define WS_FUSE_RED 0
 #endif
 
 // One side stream per device (created on first use, never destroyed) for the

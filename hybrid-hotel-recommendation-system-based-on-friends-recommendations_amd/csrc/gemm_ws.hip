@@ -162,21 +162,41 @@ __device__ __forceinline__ void ws_reduce_tail(const NtArgs& a, int slice, int n
   const int tid = threadIdx.x, c = tid % WS_TN, k = tid / WS_TN;
   const int n = n0 + c;
   const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.part, (int64_t)a.groups * 2 * a.N * 4);
-  constexpr int U = 32;
+  // every row's load in flight at once (one memory round trip: the tail of
+  // the launch), summed in reduce_small's order
+  constexpr int U = 32, NG = 8;
   double tot = 0.0;
-#pragma unroll 1
-  for (int g = 0; g < 8; ++g) {
-    float v[U];
+  if (a.groups <= 4 * U) {
+    float v[4 * U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int row = g * U + u;
-      const bool ok = n < a.N && row < a.groups;
-      v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, ok ? ((row * 2 + k) * a.N + n) * 4 : OOR, 0, 0));
+    for (int u = 0; u < 4 * U; ++u) {
+      const bool ok = n < a.N && u < a.groups;
+      v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, ok ? ((u * 2 + k) * a.N + n) * 4 : OOR, 0, 0));
     }
-    double gs = 0.0;
 #pragma unroll
-    for (int u = 0; u < U; ++u) gs += (double)v[u];
-    tot += gs;
+    for (int g = 0; g < NG; ++g) {
+      double gs = 0.0;
+      if (g < 4) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) gs += (double)v[g * U + u];
+      }
+      tot += gs;
+    }
+  } else {
+#pragma unroll 1
+    for (int g = 0; g < NG; ++g) {
+      float v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int row = g * U + u;
+        const bool ok = n < a.N && row < a.groups;
+        v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, ok ? ((row * 2 + k) * a.N + n) * 4 : OOR, 0, 0));
+      }
+      double gs = 0.0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) gs += (double)v[u];
+      tot += gs;
+    }
   }
   double* red = reinterpret_cast<double*>(lds + 64);
   red[tid] = tot;

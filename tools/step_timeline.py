@@ -9,6 +9,7 @@ queue adam runs on) -- where the step waits on cross-stream events.
 """
 import argparse
 import csv
+import re
 
 
 def main():
@@ -31,7 +32,7 @@ def main():
     gaps, last_end = [], base
     print(f"step {a.step}: {(end['t1'] - base) / 1e3:.1f} us, {len(step)} kernels, main queue {main_q}")
     for r in step:
-        name = r["Kernel_Name"].split("(")[0][:70]
+        name = re.sub(r"\(anonymous namespace\)::|dcnr::|void ", "", r["Kernel_Name"]).split("(")[0][:60]
         on_main = r[qkey] == main_q
         if on_main:
             g = (r["t0"] - last_end) / 1e3
