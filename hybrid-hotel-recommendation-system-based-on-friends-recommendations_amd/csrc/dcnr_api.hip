@@ -130,6 +130,13 @@ constexpr unsigned SYNC_EV = hipEventDisableTiming | (DCNR_EV_NOFENCE ? hipEvent
 // BN statistics reduced + finalised by the last workgroup of the producing
 // GEMM (no SyncBN hook): one launch less per BatchNorm layer (lab knob: 0 =
 // separate reduce launch)
+// the side-stream pipe's dependency on the main stream's BN apply pass is
+// that launch's own completion event (hipExtLaunchKernel stop event) instead
+// of a marker recorded after it, and with the alternating dt sets the main
+// stream waits for the side once per block (lab knob: 0 = marker per call)
+#ifndef DW_EXT_EV
+#define DW_EXT_EV 0
+#endif
 #ifndef WS_FUSE_RED
 #define WS_FUSE_RED 0
 #endif
@@ -383,6 +390,8 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
     const size_t mb = (size_t)B * d.Hp / 8;
     for (int j = 0; j < d.R; ++j) L.mask_a1[j] = (uint8_t*)b.take(mb);
     for (int j = 1; j < d.R; ++j) L.mask_h[j] = (uint8_t*)b.take(mb);
+    if (bn_add_relu_head_supported(d.prec, d.Hp))   // [h_R > 0] for the last block's BN2 apply
+      L.mask_h[d.R] = (uint8_t*)b.take(mb);
   }
   L.zc = (float*)b.take(B * 4);
   L.zdeep = (float*)b.take(B * 4);
@@ -529,11 +538,12 @@ CrossParams make_cross(const Dims& d, const Params& P) {
 }
 
 dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train, hipStream_t s) {
-  // weights -> padded T copies (+ transposes for backward); biases -> padded f32
+  // weights -> padded T copies (+ transposes for backward); biases -> padded
+  // f32; one launch per MAX_PACK descriptors
   std::vector<PackDesc> v;
   auto add = [&](const float* src, void* dst, void* dst_t, int rows, int cols, int ld, int ld_t,
                  int rows_p, int cols_p) {
-    PackDesc p{src, dst, dst_t, rows, cols, ld, ld_t, rows_p, cols_p};
+    PackDesc p{src, dst, dst_t, rows, cols, ld, ld_t, rows_p, cols_p, 0};   // T = the precision
     v.push_back(p);
   };
   add(P.W0, L.W0p, train ? L.W0t : nullptr, d.H, d.D, d.Dp, d.Hp, d.Hp, d.Dp);
@@ -541,26 +551,19 @@ dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train
     add(P.blk[j].w1, L.W1p[j], train ? L.W1t[j] : nullptr, d.H, d.H, d.Hp, d.Hp, d.Hp, d.Hp);
     add(P.blk[j].w2, L.W2p[j], train ? L.W2t[j] : nullptr, d.H, d.H, d.Hp, d.Hp, d.Hp, d.Hp);
   }
-  std::vector<PackDesc> vb;
   auto addb = [&](const float* src, float* dst) {
-    PackDesc p{src, dst, nullptr, 1, d.H, d.Hp, 0, 1, 0};
-    vb.push_back(p);
+    PackDesc p{src, dst, nullptr, 1, d.H, d.Hp, 0, 1, 0, 1};
+    v.push_back(p);
   };
   addb(P.b0, L.b0p);
   // reduce_fused's column-group counters start at zero (a 1-row pack of 0 columns)
-  vb.push_back(PackDesc{P.b0, L.red_cnt, nullptr, 0, 0, CNT_SLOTS, 0, 1, 0});
+  v.push_back(PackDesc{P.b0, L.red_cnt, nullptr, 0, 0, CNT_SLOTS, 0, 1, 0, 1});
   for (int j = 0; j < d.R; ++j) { addb(P.blk[j].b1, L.b1p[j]); addb(P.blk[j].b2, L.b2p[j]); }
   for (size_t o = 0; o < v.size(); o += MAX_PACK) {
     PackBatch pb;
     pb.n = (int)std::min<size_t>(MAX_PACK, v.size() - o);
     for (int i = 0; i < pb.n; ++i) pb.d[i] = v[o + i];
     TRYP(DCNR_K_PACK, pack_weights(d.prec, pb, s));
-  }
-  for (size_t o = 0; o < vb.size(); o += MAX_PACK) {
-    PackBatch pb;
-    pb.n = (int)std::min<size_t>(MAX_PACK, vb.size() - o);
-    for (int i = 0; i < pb.n; ++i) pb.d[i] = vb[o + i];
-    TRYP(DCNR_K_PACK, pack_weights(DCNR_PREC_FP32, pb, s));
   }
   return DCNR_OK;
 }
@@ -696,6 +699,7 @@ struct DwPipe {
   hipEvent_t dw_ev[RING] = {};
   int calls = 0, lag = 1;
   bool pending = false;   // side work enqueued since the last join
+  bool primed = false;    // in_ev is the completion event of the last apply launch
   dcnr_status init(hipStream_t side_stream, int lag_calls) {
     side = side_stream;
     lag = lag_calls;
@@ -706,9 +710,20 @@ struct DwPipe {
   }
   // order the side stream after the main stream's work so far (and the main
   // stream after call (calls - lag)'s GEMM, see above)
+  // (lag 3 with DW_EXT_EV: odd calls wait for call n-2, the block-before's
+  // dW1 -- the side stream is in order, so that covers calls n-3 and n-2,
+  // whose dY the next two apply passes overwrite -- even calls wait for none)
   dcnr_status enter(hipStream_t main_s) {
-    if (calls >= lag) DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev[(calls - lag) % RING], 0));
-    DCNR_HIP(hipEventRecord(in_ev, main_s));
+    if (DW_EXT_EV && lag == 3) {
+      if ((calls & 1) && calls >= 3) DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev[(calls - 2) % RING], 0));
+    } else if (calls >= lag) {
+      DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev[(calls - lag) % RING], 0));
+    }
+    if (!primed || g_stop_ev) {   // no apply launch took the event: record it here
+      g_stop_ev = nullptr;
+      DCNR_HIP(hipEventRecord(in_ev, main_s));
+    }
+    primed = false;
     DCNR_HIP(hipStreamWaitEvent(side, in_ev, 0));
     main = main_s;
     pending = true;
@@ -739,6 +754,12 @@ struct DwPipe {
          splitk_reduce_t(L.slab, S, (int64_t)N * Kc, N, Nr, Kr, out, accumulate, s));
     return DCNR_OK;
   }
+  // the next row-pass launch on the main stream signals in_ev when it completes
+  void prime() {
+    if (!DW_EXT_EV) return;
+    g_stop_ev = in_ev;
+    primed = true;
+  }
   dcnr_status join(hipStream_t main_s) {
     if (!pending) return DCNR_OK;
     DCNR_HIP(hipEventRecord(done_ev, side));
@@ -747,6 +768,7 @@ struct DwPipe {
     return DCNR_OK;
   }
   ~DwPipe() {
+    g_stop_ev = nullptr;
     if (pending && main) {   // error path: order the side work before the caller's stream
       (void)hipEventRecord(done_ev, side);
       (void)hipStreamWaitEvent(main, done_ev, 0);
@@ -1119,7 +1141,7 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     if (head)   // last block: residual + ReLU + deep head dot + logits in one pass
       TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B) + 12.0 * B, bn_add_relu_head(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
                                             L.bn[2 * j + 1].scale, L.bn[2 * j + 1].shift, P.wf,
-                                            d.H, L.zc, P.bf, logits, s));
+                                            d.H, L.zc, P.bf, logits, s, train ? L.mask_h[d.R] : nullptr));
     else
       TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B) + (train && j + 1 < d.R ? mask_b(d, B) : 0), bn_add_relu2(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
                                         L.bn[2 * j + 1].scale, L.bn[2 * j + 1].shift, s,
@@ -1234,8 +1256,14 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRY(bn_bwd_reduce(desc, d, L, nc, 3, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2,
                         Gin ? nullptr : Gr.wf, Gk.b2, accumulate, s));
     }
-    TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn2_apply2(d.prec, du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
-                       dt2, L.part, &nc, s));
+    if (pipe) pipe->prime();   // the apply pass below signals the dW2 call's dependency
+    if (!Gin && j == d.R - 1 && L.mask_h[d.R] && d.prec == DCNR_PREC_BF16)
+      TRYB(DCNR_K_ROWWISE, 2 * act_b(d, B) + mask_b(d, B) + 4.0 * B,
+           bwd_bn2_apply_rank1(L.mask_h[d.R], dz, P.wf, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
+                               dt2, s));
+    else
+      TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn2_apply2(d.prec, du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
+                         dt2, L.part, &nc, s));
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
     TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
     if (fuse) {
@@ -1258,6 +1286,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     }
     TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
                         accumulate, s));
+    if (pipe) pipe->prime();
     TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_apply2(d.prec, da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, dt1,
                        L.part, &nc, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du

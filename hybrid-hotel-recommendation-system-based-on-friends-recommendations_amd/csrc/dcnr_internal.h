@@ -2,12 +2,19 @@
 // gfx950 (MI355X / CDNA4) only: 64-lane waves, MFMA, 160 KiB LDS per CU.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <stdint.h>
 #include <stddef.h>
 
 #include "../../include/dcnr.h"
 
 namespace dcnr {
+
+// When set, the next row-pass launch (run_rowcol) records this event as its
+// completion (hipExtLaunchKernel's stop event: no separate marker packet on
+// the stream) and clears it.  The backward's side-stream weight-gradient
+// pipe uses it to depend on the BN apply pass that wrote its dY.
+extern thread_local hipEvent_t g_stop_ev;
 
 typedef __bf16 bf16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -397,6 +404,7 @@ struct PackDesc {            // W [rows][cols] f32 -> dst T [rows_p][ld] (+ opti
   const float* src; void* dst; void* dst_t;
   int rows, cols, ld, ld_t;  // dst ld >= cols (pad 0), dst_t is [cols_p][ld_t] with ld_t >= rows
   int rows_p, cols_p;
+  int f32;                   // 1: dst is f32 whatever the batch's precision (no transpose)
 };
 constexpr int MAX_PACK = 20;
 struct PackBatch { PackDesc d[MAX_PACK]; int n; };
@@ -528,6 +536,11 @@ dcnr_status bwd_bn2_stats3(int precision, const void* G, const float* dz, const 
 dcnr_status bwd_bn2_apply2(int precision, const void* du, const void* t, const float* mean,
                            const float* invstd, const float* coef, int64_t B, int N, int ld,
                            void* dt, float* part, int* nchunks, hipStream_t s);
+// the same for the last block (g = dz (x) wf), bf16, du from the 1-bit
+// [out > 0] image of the forward's head pass (bits [B][ld/8])
+dcnr_status bwd_bn2_apply_rank1(const uint8_t* bits, const float* dz, const float* wf, const void* t,
+                                const float* mean, const float* invstd, const float* coef,
+                                int64_t B, int N, int ld, void* dt, hipStream_t s);
 // dr = da * keep/(1-p) * [t*scale+shift > 0] (in place); NK=2 partials [dr, dr*xhat]
 dcnr_status bwd_bn1_stats(int precision, void* da_dr, const void* t, const float* scale,
                           const float* shift, const float* mean, const float* invstd, int64_t B,
@@ -553,7 +566,7 @@ bool bn_add_relu_head_supported(int precision, int N);
 dcnr_status bn_add_relu_head(int precision, const void* t, const void* x, void* out, int64_t B,
                              int N, int ld, const float* scale, const float* shift,
                              const float* wf, int Nr, const float* zc, const float* bf,
-                             float* logits, hipStream_t s);
+                             float* logits, hipStream_t s, uint8_t* bits = nullptr);
 dcnr_status row_dot(int precision, const void* X, int ld, int N, const float* w, int64_t B,
                     float* out, hipStream_t s);
 // logits[b] = sum_p part[p][b] (p = 0..np-1, fixed order) + zc[b] + bf

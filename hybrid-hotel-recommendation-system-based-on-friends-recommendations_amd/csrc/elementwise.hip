@@ -144,7 +144,13 @@ dcnr_status run_rowcol(const Op& op, int64_t B, int N, float* part, int* nchunks
   int nc = (int)cdiv(B, rows);
   if (nchunks) *nchunks = nc;
   if (B <= 0) return DCNR_OK;
-  hipLaunchKernelGGL((rowcol_kernel<T, NK, Op>), dim3(nc), dim3(NT), 0, s, op, B, N, rows, part);
+  if (g_stop_ev) {
+    hipExtLaunchKernelGGL((rowcol_kernel<T, NK, Op>), dim3(nc), dim3(NT), 0, s, nullptr, g_stop_ev, 0,
+                          op, B, N, rows, part);
+    g_stop_ev = nullptr;
+  } else {
+    hipLaunchKernelGGL((rowcol_kernel<T, NK, Op>), dim3(nc), dim3(NT), 0, s, op, B, N, rows, part);
+  }
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
@@ -249,6 +255,7 @@ template <typename T> struct BnAddReluOp {   // out = relu(t*sc+sh + x)
 template <typename T> struct BnAddReluHeadOp {
   const T* t; const T* x; T* out; int ld; const float* sc; const float* sh;
   const float* wf; int Nr; const float* zc; const float* bf; float* logits;
+  uint8_t* bits;   // train: 1-bit [out > 0] for the backward (null: none)
   struct Cst { float sc[VE<T>], sh[VE<T>], wf[VE<T>]; float bf; };
   struct Reg { float a[VE<T>], b[VE<T>]; };
   __device__ void prep(int c, Cst& q) const {
@@ -269,6 +276,7 @@ template <typename T> struct BnAddReluHeadOp {
       d += (float)(T)q.a[v] * k.wf[v];   // the stored (rounded) activation, as row_dot reads it
     }
     stv<T, true>(out + r * ld + c, q.a);
+    if (bits) store_pos_bits<T>(bits, r, ld >> 3, c, q.a);
     d = wave_sum_dpp(d);
     if ((threadIdx.x & 63) == 0) logits[r] = (d + zc[r]) + k.bf;
   }
@@ -329,6 +337,35 @@ template <typename T> struct Bwd2ApplyOp {
     stv<T>(dt + r * ld + c, q.u);
   }
 };
+// last block (g = dz (x) wf, rank 1): dt2 = k0*du - k1*xhat - k2 with du
+// rebuilt from dz, wf and the forward's 1-bit [out > 0] image (bf16), so the
+// pass reads neither du nor out; du is the value Bwd2StatsOp stores, bit for bit
+template <typename T> struct Bwd2ApplyRank1Op {
+  const uint8_t* bits; const float* dz; const float* wf; const T* t; const float* mean;
+  const float* invstd; const float* coef; int ld, N; T* dt;
+  struct Cst { float mu[VE<T>], is[VE<T>], k0[VE<T>], k1[VE<T>], k2[VE<T>], wf[VE<T>]; };
+  struct Reg { float t[VE<T>]; float d; uint32_t b; };
+  __device__ void prep(int c, Cst& q) const {
+    ldc(mean + c, q.mu); ldc(invstd + c, q.is); ldc(wf + c, q.wf);
+    ldc(coef + c, q.k0); ldc(coef + N + c, q.k1); ldc(coef + 2 * N + c, q.k2);
+  }
+  __device__ void load(int64_t r, int c, Reg& q) const {
+    ldv<T>(t + r * ld + c, q.t);
+    q.d = dz[r];
+    q.b = bits[r * (ld >> 3) + (c >> 3)];
+  }
+  __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&)[1][VE<T>]) const {
+    float o[VE<T>];
+#pragma unroll
+    for (int v = 0; v < VE<T>; ++v) {
+      const float du = (q.b >> v) & 1u ? (float)(T)(q.d * k.wf[v]) : 0.f;
+      const float xh = (q.t[v] - k.mu[v]) * k.is[v];
+      o[v] = k.k0[v] * du - k.k1[v] * xh - k.k2[v];
+    }
+    stv<T>(dt + r * ld + c, o);
+  }
+};
+
 template <typename T> struct Bwd1StatsOp {
   T* da; const T* t; const float* sc; const float* sh; const float* mean; const float* invstd;
   int ld; float inv_keep; uint32_t thresh; uint64_t seed; int layer; int drop;
@@ -388,6 +425,7 @@ template <typename T, bool G> struct RowUnroll<Bwd2StatsOp<T, G>> { static const
 template <typename T> struct RowUnroll<BnAddReluHeadOp<T>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<Bwd1ApplyOp<T>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<Bwd2ApplyOp<T>> { static constexpr int v = 2; };
+template <typename T> struct RowUnroll<Bwd2ApplyRank1Op<T>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<BnAddReluOp<T>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<BnReluDropOp<T>> { static constexpr int v = 2; };
 
@@ -487,8 +525,7 @@ __global__ void splitk_reduce_kernel(const float* slab, int splits, int64_t stri
 // or two 16-B (fp32) stores per thread) and, for the backward, transposes
 // [cols_p][ld_t] through 64x64 LDS tiles (coalesced reads and writes).
 template <typename T>
-__global__ __launch_bounds__(NT) void pack_kernel(PackBatch pb) {
-  const PackDesc& d = pb.d[blockIdx.y];
+__device__ __forceinline__ void pack_rows(const PackDesc& d) {
   T* dst = (T*)d.dst;
   const int cg = d.ld >> 3;
   const int tot = d.rows_p * cg;
@@ -519,6 +556,14 @@ __global__ __launch_bounds__(NT) void pack_kernel(PackBatch pb) {
       *reinterpret_cast<f32x4*>(p + 4) = f32x4{v[4], v[5], v[6], v[7]};
     }
   }
+}
+
+// (d.f32: an fp32 copy -- biases, counters -- in the same launch as T weights)
+template <typename T>
+__global__ __launch_bounds__(NT) void pack_kernel(PackBatch pb) {
+  const PackDesc& d = pb.d[blockIdx.y];
+  if (d.f32) pack_rows<float>(d);
+  else pack_rows<T>(d);
   if (!d.dst_t) return;
   __shared__ float tile[64][65];
   T* dt = (T*)d.dst_t;
@@ -699,6 +744,8 @@ dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, 
 }
 
 // ================================================================== API
+thread_local hipEvent_t g_stop_ev = nullptr;
+
 dcnr_status pack_weights(int precision, const PackBatch& pb, hipStream_t s) {
   if (pb.n == 0) return DCNR_OK;
   for (int i = 0; i < pb.n; ++i)
@@ -823,8 +870,8 @@ template <typename T>
 static dcnr_status bn_add_relu_head_impl(const void* t, const void* x, void* out, int64_t B, int N,
                                          int ld, const float* sc, const float* sh, const float* wf,
                                          int Nr, const float* zc, const float* bf, float* logits,
-                                         hipStream_t s) {
-  BnAddReluHeadOp<T> op{(const T*)t, (const T*)x, (T*)out, ld, sc, sh, wf, Nr, zc, bf, logits};
+                                         uint8_t* bits, hipStream_t s) {
+  BnAddReluHeadOp<T> op{(const T*)t, (const T*)x, (T*)out, ld, sc, sh, wf, Nr, zc, bf, logits, bits};
   return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
 }
 bool bn_add_relu_head_supported(int precision, int N) {
@@ -833,14 +880,14 @@ bool bn_add_relu_head_supported(int precision, int N) {
 dcnr_status bn_add_relu_head(int precision, const void* t, const void* x, void* out, int64_t B,
                              int N, int ld, const float* scale, const float* shift,
                              const float* wf, int Nr, const float* zc, const float* bf,
-                             float* logits, hipStream_t s) {
+                             float* logits, hipStream_t s, uint8_t* bits) {
   if (!bn_add_relu_head_supported(precision, N)) {
     set_error("bn_add_relu_head: needs a wave per row (N=%d)", N);
     return DCNR_UNSUPPORTED_SHAPE;
   }
   return precision == DCNR_PREC_BF16
-             ? bn_add_relu_head_impl<bf16>(t, x, out, B, N, ld, scale, shift, wf, Nr, zc, bf, logits, s)
-             : bn_add_relu_head_impl<float>(t, x, out, B, N, ld, scale, shift, wf, Nr, zc, bf, logits, s);
+             ? bn_add_relu_head_impl<bf16>(t, x, out, B, N, ld, scale, shift, wf, Nr, zc, bf, logits, bits, s)
+             : bn_add_relu_head_impl<float>(t, x, out, B, N, ld, scale, shift, wf, Nr, zc, bf, logits, nullptr, s);
 }
 
 template <typename T>
@@ -872,6 +919,12 @@ static dcnr_status bwd2_apply_impl(const void* du, const void* t, const float* m
                                    int ld, void* dt, float* part, int* nc, hipStream_t s) {
   Bwd2ApplyOp<T> op{(const T*)du, (const T*)t, mean, invstd, coef, ld, N, (T*)dt};
   return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
+}
+dcnr_status bwd_bn2_apply_rank1(const uint8_t* bits, const float* dz, const float* wf, const void* t,
+                                const float* mean, const float* invstd, const float* coef,
+                                int64_t B, int N, int ld, void* dt, hipStream_t s) {
+  Bwd2ApplyRank1Op<bf16> op{bits, dz, wf, (const bf16*)t, mean, invstd, coef, ld, N, (bf16*)dt};
+  return run_rowcol<bf16, 0>(op, B, N, nullptr, nullptr, s);
 }
 dcnr_status bwd_bn2_apply2(int precision, const void* du, const void* t, const float* mean,
                            const float* invstd, const float* coef, int64_t B, int N, int ld,
