@@ -93,7 +93,10 @@ typedef enum { DCNR_EVAL = 0, DCNR_TRAIN = 1 } dcnr_mode;
 /* Train workspace keeps every residual block's backward intermediates (du,
  * dt2, da, dt1) in buffers of their own instead of reusing one set: the
  * stage-by-stage parity tests read them (dcnr_workspace_offset).  Same
- * kernels, same results; more workspace. */
+ * kernels, same results; more workspace.  In eval mode it keeps the
+ * unfused tail (BN affine finalize launch, the last block's output h_R in
+ * the workspace, separate head dot); without it the bf16 eval forward ends
+ * in the last GEMM's head epilogue and never stores h_R. */
 #define DCNR_FLAG_KEEP_INTERMEDIATES 2u
 
 /* Optional collective hook for SyncBN across data-parallel ranks: called
