@@ -418,6 +418,7 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
     // split count depends on the tile count (narrow H -> more splits)
     L.slab_elems = std::max<int64_t>({(int64_t)64 * d.Hp * std::max(d.Hp, d.Dp),
                                       (int64_t)gemm_dw_splits(d.Hp, d.Hp, B) * d.Hp * d.Hp,
+                                      (int64_t)gemm_dw_splits(d.Hp, d.Hp, B, DW_WG_BLOCKS) * d.Hp * d.Hp,
                                       (int64_t)gemm_dw_splits(d.Hp, d.Dp, B) * d.Hp * d.Dp});
     L.slab = (float*)b.take((size_t)L.slab_elems * 4);
     L.sc = (float*)b.take((size_t)B * (2 * d.L + 1) * 4);
