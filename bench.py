@@ -67,7 +67,7 @@ CLASS_KERNELS = {
     "cross_bwd": "cross_coef / x0_alpha / cross_final kernels (low-rank cross backward)",
     "emb_sort": "emb_ids/hist/scan/scatter/bucket_sort kernels (stable id sort)",
     "emb_sum": "emb_runs_short/long_kernel (fixed-order embedding-gradient sums)",
-    "head": "row_dot / logits / bce kernels",
+    "head": "row_dot / head_parts / logits / bce kernels",
     "adam": "adam_kernel (fused AdamW)",
     "pack": "pack / zero-fill kernels",
 }

@@ -33,17 +33,31 @@
 namespace dcnr {
 namespace {
 
-constexpr int TNW = 256, TKW = 256, BKW = 32, NTW = 512, NSTAGE = 4;
-constexpr int ROWB = TNW * 2;                 // bytes per LDS row (256 bf16)
-constexpr int OPB = BKW * ROWB;               // bytes per operand per stage (16 KiB)
-constexpr int STAGEB = 2 * OPB;               // A + B per stage (32 KiB)
-constexpr int LDS_DW = NSTAGE * STAGEB;       // ring of 4 stages (128 KiB)
+// DW_TK: the tile's k width (lab: 128 halves the split count, so the fp32
+// slab, at 1.5x the L2->LDS operand bytes and 0.625 instead of 0.375
+// fragment reads per MFMA)
+#ifndef DW_TK
+#define DW_TK 256
+#endif
+constexpr int TNW = 256, TKW = DW_TK, BKW = 32, NTW = 512, NSTAGE = 4;
+constexpr int ROWB = TNW * 2;                 // bytes per A row in LDS (256 bf16)
+constexpr int ROWBB = TKW * 2;                // bytes per B row in LDS
+constexpr int OPB = BKW * ROWB;               // A bytes per stage (16 KiB)
+constexpr int OPBB = BKW * ROWBB;             // B bytes per stage
+constexpr int STAGEB = OPB + OPBB;            // A + B per stage
+constexpr int LDS_DW = NSTAGE * STAGEB;       // ring of 4 stages
+constexpr int WKC = TKW / 4;                  // k columns per wave (4 waves across k)
+constexpr int NJ = WKC / 16;                  // 16-column MFMA blocks per wave in k
+constexpr int DMAW = 2 + (TKW == 256 ? 2 : 1);   // DMA instructions per wave per stage
+static_assert(TKW == 256 || TKW == 128, "DW_TK");
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 // physical byte offset of logical (row, byte x) inside one operand image
+// with RB bytes per row
+template <int RB = ROWB>
 __device__ __forceinline__ int swz(int row, int x) {
-  return row * ROWB + ((((x >> 5) ^ (row & 7)) << 5) | (x & 31));
+  return row * RB + ((((x >> 5) ^ (row & 7)) << 5) | (x & 31));
 }
 
 // One stage: rows kb..kb+31 of A (cols n0..n0+255) and B (cols c0..c0+255).
@@ -61,23 +75,32 @@ __device__ __forceinline__ void stage_load(u32x4 ar, u32x4 br, int64_t lda, int6
     const int na = n0 + chunk * 8, ka = c0 + chunk * 8;
     const bool okr = b < kend;
     const int offa = (okr && na < N) ? (int)((b * lda + na) * 2) : OOR;
-    const int offb = (okr && ka < K) ? (int)((b * ldb + ka) * 2) : OOR;
     const uint32_t dsta = lds_addr(lds_stage) + (wave * 2 + i) * 1024;
-    if constexpr (!(DW_LAB_MODE & 2)) {
-      dma16(ar, offa, dsta);
-      dma16(br, offb, dsta + OPB);
+    if constexpr (!(DW_LAB_MODE & 2)) dma16(ar, offa, dsta);
+    if constexpr (TKW == 256) {
+      const int offb = (okr && ka < K) ? (int)((b * ldb + ka) * 2) : OOR;
+      if constexpr (!(DW_LAB_MODE & 2)) dma16(br, offb, dsta + OPB);
     }
+  }
+  if constexpr (TKW == 128) {   // 256-B rows: one instruction fills 4 rows, one per wave
+    const int row = wave * 4 + (lane >> 4), q = lane & 15;
+    const int chunk = ((q >> 1) ^ (row & 7)) * 2 + (q & 1);
+    const int64_t b = kb + row;
+    const int ka = c0 + chunk * 8;
+    const int offb = (b < kend && ka < K) ? (int)((b * ldb + ka) * 2) : OOR;
+    if constexpr (!(DW_LAB_MODE & 2)) dma16(br, offb, lds_addr(lds_stage) + OPB + wave * 1024);
   }
 }
 
 // A-operand fragment (16 columns starting at cb, batch rows kk..kk+31):
 // lane l gets X[kk + 8*(l>>4) + j][cb + (l&15)], j = 0..7, from the
 // batch-major image via two transposed 4x16 block reads.
+template <int RB = ROWB>
 __device__ __forceinline__ bf16x8 frag_t(const char* img, int cb, int kk, int lane) {
   const int rk = kk + 8 * (lane >> 4) + ((lane & 15) >> 2);
   const int x = (cb + 4 * (lane & 3)) * 2;
-  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + swz(rk, x)));
-  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + swz(rk + 4, x)));
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + swz<RB>(rk, x)));
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + swz<RB>(rk + 4, x)));
   typedef __attribute__((ext_vector_type(8))) short s16x8;
   s16x8 c = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
   return __builtin_bit_cast(bf16x8, c);
@@ -94,16 +117,16 @@ __global__ __launch_bounds__(NTW, 1) void gemm_dw_kernel(DwArgs g) {
   const int64_t kend = min(g.Btot, kbeg + g.k_per_split);
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wn = wave >> 2, wk = wave & 3;    // wave tile: n wn*128.., k wk*64..
+  const int wn = wave >> 2, wk = wave & 3;    // wave tile: n wn*128.., k wk*WKC..
 
   const u32x4 ar = rsrc_words(g.A, g.Btot * g.lda * 2);
   const u32x4 br = rsrc_words(g.B, g.Btot * g.ldb * 2);
 
-  f32x4 acc[8][4];
+  f32x4 acc[8][NJ];
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nst = kend > kbeg ? (int)((kend - kbeg + BKW - 1) / BKW) : 0;
 #pragma unroll
@@ -115,8 +138,8 @@ __global__ __launch_bounds__(NTW, 1) void gemm_dw_kernel(DwArgs g) {
     // this wave's DMAs of stage st are done (the younger stages stay in
     // flight), then the barrier makes every wave's part visible and retires
     // stage st-1's reads, so its buffer can be refilled with stage st+3
-    if (st + 2 < nst) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    if (st + 2 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * DMAW) : "memory");
+    else if (st + 1 < nst) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(DMAW) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (st + NSTAGE - 1 < nst)
@@ -124,15 +147,15 @@ __global__ __launch_bounds__(NTW, 1) void gemm_dw_kernel(DwArgs g) {
                  g.K, lds + ((st + NSTAGE - 1) % NSTAGE) * STAGEB, wave, lane);
     const char* ai = lds + (st % NSTAGE) * STAGEB;
     const char* bi = ai + OPB;
-    bf16x8 af[8], bf[4];
+    bf16x8 af[8], bf[NJ];
 #pragma unroll
     for (int i = 0; i < 8; ++i) af[i] = frag_t(ai, wn * 128 + i * 16, 0, lane);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bf[j] = frag_t(bi, wk * 64 + j * 16, 0, lane);
+    for (int j = 0; j < NJ; ++j) bf[j] = frag_t<ROWBB>(bi, wk * WKC + j * 16, 0, lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < NJ; ++j)
         if constexpr (!(DW_LAB_MODE & 1))
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
         else
@@ -148,8 +171,8 @@ __global__ __launch_bounds__(NTW, 1) void gemm_dw_kernel(DwArgs g) {
 #pragma unroll
   for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int k = c0 + wk * 64 + j * 16 + (lane & 15);
+    for (int j = 0; j < NJ; ++j) {
+      const int k = c0 + wk * WKC + j * 16 + (lane & 15);
       const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4;   // N % 8 == 0: all 4 or none
       const bool ok = n < g.N && k < g.K;
       if (!(DW_LAB_MODE & 4) || acc[i][j][0] == 1234.5f)
