@@ -395,7 +395,7 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
   }
   L.zc = (float*)b.take(B * 4);
   L.zdeep = (float*)b.take(B * 4);
-  if (!train && !keep && eval_fuse_ok(d))   // the last eval GEMM's head partials
+  if (!train && !keep && eval_fuse_ok(d) && d.R >= 1)   // the last eval GEMM's head partials
     L.headp = (float*)b.take((size_t)B * gemm_ws_head_parts(d.Hp) * 4);
   for (int i = 0; i < 2 * d.R; ++i) {
     L.bn[i].scale = (float*)b.take(d.Hp * 4);
@@ -619,7 +619,7 @@ dcnr_status linear_bn_relu(const Dims& d, const void* A, const void* W, const fl
   a.R = R; a.ldr = d.Hp;
   a.bn_scale = bn.scale; a.bn_shift = bn.shift;
   if (rs) { a.bn_g = rs[0]; a.bn_b = rs[1]; a.bn_rm = rs[2]; a.bn_rv = rs[3]; }
-  a.wf = wf; a.headp = headp;
+  a.wf = wf; a.headp = headp; a.ldh = B;
   return gemm_ws(headp ? NT_EPI_BN_RESID_RELU_HEAD : R ? NT_EPI_BN_RESID_RELU : NT_EPI_BN_RELU, a, s);
 }
 

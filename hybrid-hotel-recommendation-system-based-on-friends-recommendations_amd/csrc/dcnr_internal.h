@@ -364,7 +364,8 @@ struct NtArgs {
   // scale / shift itself (bn_eval_multi_kernel's arithmetic) instead of reading
   // bn_scale / bn_shift
   const float* bn_g; const float* bn_b; const float* bn_rm; const float* bn_rv;
-  const float* wf; float* headp;                    // BN_RESID_RELU_HEAD (wf: Nr entries)
+  const float* wf; float* headp; int64_t ldh;      // BN_RESID_RELU_HEAD (wf: Nr entries;
+                                                    // headp rows ldh apart, ldh >= M)
   float* part;                                      // column partials (stats epilogues)
   // stats epilogues: with fuse_red the launch's last workgroup per column
   // slice also sums the partial rows (reduce_small's fixed order) and runs

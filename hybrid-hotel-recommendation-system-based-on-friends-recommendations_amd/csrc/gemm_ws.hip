@@ -304,7 +304,7 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
   const __amdgpu_buffer_rsrc_t tr = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.T, (short)0, HAS_HT ? (int)(a.M * a.ldt * 2) : 0, 0x00020000);
   const __amdgpu_buffer_rsrc_t hp_r = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)a.headp, (short)0, HEAD ? (int)(a.nslices * WS_WAVES * a.M * 4) : 0, 0x00020000);
+      (void*)a.headp, (short)0, HEAD ? (int)(((a.nslices * WS_WAVES - 1) * a.ldh + a.M) * 4) : 0, 0x00020000);
 
   // per-lane column partials [sum, sum2][cb][column pair], over all tiles
   f2v st[2][2][2];
@@ -437,7 +437,7 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
         const float r4 = __uint_as_float(h4[0]) + __uint_as_float(h4[1]);
         if (q == 0)
           __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(r4), hp_r,
-                                                mok ? (int)(((slice * WS_WAVES + wave) * a.M + m) * 4) : OOR, 0, 0);
+                                                mok ? (int)(((slice * WS_WAVES + wave) * a.ldh + m) * 4) : OOR, 0, 0);
       } else if constexpr (EPI == NT_EPI_F32) {
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb) {
@@ -689,6 +689,7 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
       b.C = (char*)a.C + m0 * a.ldc * (EPI == NT_EPI_F32 ? 4 : 2);
       if (a.R) b.R = (const char*)a.R + m0 * a.ldr * 2;
       if (a.Hb) b.Hb = a.Hb + m0 * a.ldhb;
+      if (a.headp) b.headp = a.headp + m0;   // same row stride ldh
       if (a.T) b.T = a.T + m0 * a.ldt;
       if (a.part) b.part = a.part + (int64_t)total * 2 * a.N;
       int np = 0;
@@ -735,7 +736,8 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
       (epi >= NT_EPI_BN_RELU && !a.bn_rm && (!a.bn_scale || !a.bn_shift)) ||
       (epi >= NT_EPI_BN_RELU && a.bn_rm && (!a.bn_g || !a.bn_b || !a.bn_rv)) ||
       (epi == NT_EPI_BN_RESID_RELU_HEAD &&
-       (!a.wf || !a.headp || !gemm_ws_head_parts(a.N) || a.M * gemm_ws_head_parts(a.N) * 4 >= (int64_t(1) << 31))) ||
+       (!a.wf || !a.headp || !gemm_ws_head_parts(a.N) || a.ldh < a.M ||
+        a.ldh * gemm_ws_head_parts(a.N) * 4 >= (int64_t(1) << 31))) ||
       (ht && (!a.Hb || !a.T || !a.mean || !a.invstd || a.ldt % 8)) ||
       (nt_epi_stats(epi) && !a.part)) {
     set_error("gemm_ws: unsupported K=%d N=%d / missing epilogue operand", a.K, a.N);

@@ -33,8 +33,10 @@ def _eval_logits(m, inp, dev, keep):
     return z.double().cpu().numpy()
 
 
-@pytest.mark.parametrize("cfg,B", [(gc.CFG3R, 131072), (gc.CFG3R, 4099), (gc.CFG1, 777),
-                                   (gc.CFG_ODD, 1000)])
+# (600000 rows of 512 bf16 columns: the GEMM runs in two M-chunks of 32-bit
+# buffer offsets, each writing its rows of the head partials)
+@pytest.mark.parametrize("cfg,B", [(gc.CFG3R, 131072), (gc.CFG3R, 4099), (gc.CFG3R, 600000),
+                                   (gc.CFG1, 777), (gc.CFG_ODD, 1000)])
 def test_eval_fused_head_matches_unfused(dev, cfg, B):
     import dcnr
     import dcnr_oracle as orc  # checker only
