@@ -137,6 +137,13 @@ constexpr unsigned SYNC_EV = hipEventDisableTiming | (DCNR_EV_NOFENCE ? hipEvent
 #ifndef DW_EXT_EV
 #define DW_EXT_EV 0
 #endif
+// lab: each block's weight-gradient call enqueued after the dX GEMM that
+// follows its apply pass, so the side stream's gemm_dw overlaps the next BN
+// apply pass (a row pass that can share a CU with it) rather than the dX
+// GEMM (which cannot: both need most of a CU's LDS)
+#ifndef DW_AFTER_DX
+#define DW_AFTER_DX 0
+#endif
 #ifndef WS_FUSE_RED
 #define WS_FUSE_RED 0
 #endif
@@ -1266,7 +1273,8 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn2_apply2(d.prec, du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
                          dt2, L.part, &nc, s));
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
-    TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
+    if (!DW_AFTER_DX)
+      TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
     if (fuse) {
       // dy1 = (dt2 W2) * [a1 != 0] / (1-p): relu and dropout masks from the
       // saved activation, BN1 partials (and, without SyncBN, its backward
@@ -1285,13 +1293,16 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_stats(d.prec, da, L.t1[j], bn1.scale, bn1.shift, bn1.mean,
                                          bn1.invstd, B, Hp, Hp, p, dropout_seed, j, L.part, &nc, s));
     }
+    if (DW_AFTER_DX)
+      TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
     TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
                         accumulate, s));
     if (pipe) pipe->prime();
     TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_apply2(d.prec, da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, dt1,
                        L.part, &nc, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
-    TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
+    if (!DW_AFTER_DX)
+      TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
     if (fuse && j > 0) {
       // G is only consumed by block j-1's BN2 backward: emit its du = G * [h_j > 0]
       // (in place over this block's du, the residual operand, unless
@@ -1313,6 +1324,8 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       Gin = L.G;
       nc_du = 0;
     }
+    if (DW_AFTER_DX)
+      TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
   }
   // ---- initial layer
   // its bias gradient (column sums of G) also goes under the dx0 GEMM and
