@@ -545,7 +545,8 @@ CrossParams make_cross(const Dims& d, const Params& P) {
   return c;
 }
 
-dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train, hipStream_t s) {
+dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train, hipStream_t s,
+                     bool zero_err = false) {
   // weights -> padded T copies (+ transposes for backward); biases -> padded
   // f32; one launch per MAX_PACK descriptors
   std::vector<PackDesc> v;
@@ -566,6 +567,8 @@ dcnr_status pack_all(const Dims& d, const Params& P, const Layout& L, bool train
   addb(P.b0, L.b0p);
   // reduce_fused's column-group counters start at zero (a 1-row pack of 0 columns)
   v.push_back(PackDesc{P.b0, L.red_cnt, nullptr, 0, 0, CNT_SLOTS, 0, 1, 0, 1});
+  // (eval, index check on: the gather's error word, in the same launch)
+  if (zero_err) v.push_back(PackDesc{P.b0, L.err, nullptr, 0, 0, 8, 0, 1, 0, 1});
   for (int j = 0; j < d.R; ++j) { addb(P.blk[j].b1, L.b1p[j]); addb(P.blk[j].b2, L.b2p[j]); }
   for (size_t o = 0; o < v.size(); o += MAX_PACK) {
     PackBatch pb;
@@ -1050,9 +1053,11 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     TRY(pack_all(d, P, L, train, s));
     TRY(sj.mark());
   } else {
-    TRY(pack_all(d, P, L, train, s));
+    TRY(pack_all(d, P, L, train, s, check != 0));
   }
-  if (check) TRYP(DCNR_K_PACK, fill_zero(L.err, 4, s));
+  // (train: the pack runs on the side stream beside the gather, so the
+  // error word is zeroed here, before it)
+  if (check && train) TRYP(DCNR_K_PACK, fill_zero(L.err, 4, s));
   if (train) {
     EmbBwdDesc eb;
     memset(&eb, 0, sizeof(eb));
