@@ -22,7 +22,11 @@
 //    stores (and loads its operands the same way);
 //  * the BatchNorm-statistics epilogues keep per-lane column partials in
 //    registers over all of the workgroup's tiles (each wave owns its columns:
-//    no cross-wave reduction) and write one partial row per workgroup.
+//    no cross-wave reduction) and write one partial row per workgroup;
+//  * eval: BN (from the running statistics, computed per column at launch)
+//    + ReLU (+ residual) in the epilogue, and for the last residual block the
+//    deep head dot (NT_EPI_BN_RESID_RELU_HEAD: one partial per row and wave,
+//    no C store).
 #include "dcnr_internal.h"
 
 #include <type_traits>
