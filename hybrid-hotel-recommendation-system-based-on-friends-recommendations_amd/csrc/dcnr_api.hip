@@ -144,6 +144,12 @@ constexpr unsigned SYNC_EV = hipEventDisableTiming | (DCNR_EV_NOFENCE ? hipEvent
 #ifndef DW_AFTER_DX
 #define DW_AFTER_DX 0
 #endif
+// bf16 train: the last block's head pass does not store h_R; the backward's
+// BN2 statistics pass rebuilds it from t2, h_{R-1} and the BN2 affine
+// (KEEP_INTERMEDIATES still stores it for the stage tests)
+#ifndef TRAIN_HEAD_REBUILD
+#define TRAIN_HEAD_REBUILD 1
+#endif
 #ifndef WS_FUSE_RED
 #define WS_FUSE_RED 0
 #endif
@@ -358,6 +364,9 @@ bool masks_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && d.Hp % 32 == 0
 int dq_of(const Dims& d) { return (int)rup(d.Dp, 32); }
 bool keep_of(const dcnr_model_desc* desc) { return (desc->flags & DCNR_FLAG_KEEP_INTERMEDIATES) != 0; }
 
+bool head_rebuild(const Dims& d, bool train) {
+  return TRAIN_HEAD_REBUILD && train && d.prec == DCNR_PREC_BF16 && bn_add_relu_head_supported(d.prec, d.Hp);
+}
 bool eval_fuse_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && gemm_ws_supported(d.Hp, d.Hp); }
 
 Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = false) {
@@ -1152,7 +1161,9 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
                      L.bn[2 * j + 1], s, nc, fuse ? L.b2p[j] : nullptr));
     const bool head = j == d.R - 1 && bn_add_relu_head_supported(d.prec, d.Hp);
     if (head)   // last block: residual + ReLU + deep head dot + logits in one pass
-      TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B) + 12.0 * B, bn_add_relu_head(d.prec, L.t2[j], L.h[j], L.h[j + 1], B, d.Hp, d.Hp,
+      TRYB(DCNR_K_ROWWISE, (head_rebuild(d, train) && !keep_of(desc) ? 2 : 3) * act_b(d, B) + 12.0 * B,
+           bn_add_relu_head(d.prec, L.t2[j], L.h[j],
+                            head_rebuild(d, train) && !keep_of(desc) ? nullptr : L.h[j + 1], B, d.Hp, d.Hp,
                                             L.bn[2 * j + 1].scale, L.bn[2 * j + 1].shift, P.wf,
                                             d.H, L.zc, P.bf, logits, s, train ? L.mask_h[d.R] : nullptr));
     else
@@ -1263,8 +1274,10 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRY(bn_bwd_reduce(desc, d, L, nc_du, 2, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2, nullptr,
                         Gk.b2, accumulate, s));
     } else {
+      const bool rebuild = !Gin && j == d.R - 1 && head_rebuild(d, true);
       TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B) + (Gin ? act_b(d, B) : 4.0 * B), bwd_bn2_stats3(d.prec, Gin, dz, P.wf, L.h[j + 1], L.t2[j], bn2.mean,
-                                          bn2.invstd, B, Hp, Hp, du, L.part, &nc, s));
+                                          bn2.invstd, B, Hp, Hp, du, L.part, &nc, s,
+                                          rebuild ? L.h[j] : nullptr, bn2.scale, bn2.shift));
       // dbeta2, dgamma2 and (last block only) dW_f[:H]
       TRY(bn_bwd_reduce(desc, d, L, nc, 3, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2,
                         Gin ? nullptr : Gr.wf, Gk.b2, accumulate, s));

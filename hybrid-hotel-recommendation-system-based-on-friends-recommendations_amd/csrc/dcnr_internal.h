@@ -529,10 +529,13 @@ dcnr_status bn_add_relu2(int precision, const void* t, const void* x, void* out,
 // du = g*[out>0], g = G[b,n] (G != null) or dz[b]*wf[n]; NK=3 partials:
 // [du, du*xhat, dz*out] (xhat = (t-mean)*invstd; the 3rd only when G == null)
 // (also writes du = g*[out>0] in the storage type)
+// (G null and x non-null: the last block's out is rebuilt from t, x = the
+// block input and the BN scale / shift sc, sh -- out is not read)
 dcnr_status bwd_bn2_stats3(int precision, const void* G, const float* dz, const float* wf,
                            const void* out, const void* t, const float* mean, const float* invstd,
                            int64_t B, int N, int ld, void* du, float* part, int* nchunks,
-                           hipStream_t s);
+                           hipStream_t s, const void* x = nullptr, const float* sc = nullptr,
+                           const float* sh = nullptr);
 // dt = coef0*du - coef1*xhat - coef2 (part/nchunks unused)
 dcnr_status bwd_bn2_apply2(int precision, const void* du, const void* t, const float* mean,
                            const float* invstd, const float* coef, int64_t B, int N, int ld,

@@ -275,22 +275,27 @@ template <typename T> struct BnAddReluHeadOp {
       q.a[v] = fmaxf(q.a[v] * k.sc[v] + k.sh[v] + q.b[v], 0.f);
       d += (float)(T)q.a[v] * k.wf[v];   // the stored (rounded) activation, as row_dot reads it
     }
-    stv<T, true>(out + r * ld + c, q.a);
+    if (out) stv<T, true>(out + r * ld + c, q.a);   // (train: null, the backward rebuilds it)
     if (bits) store_pos_bits<T>(bits, r, ld >> 3, c, q.a);
     d = wave_sum_dpp(d);
     if ((threadIdx.x & 63) == 0) logits[r] = (d + zc[r]) + k.bf;
   }
 };
 
-// backward of out = relu(BN2(t2) + x): du = g*[out>0]; g = G or dz (x) wf
-template <typename T, bool HAS_G> struct Bwd2StatsOp {
+// backward of out = relu(BN2(t2) + x): du = g*[out>0]; g = G or dz (x) wf.
+// REBUILD (last block, g = dz (x) wf): `out` is the block input x and out is
+// rebuilt as the head pass computed it, bf16(relu(t2*sc + sh + x)), so the
+// forward never stores h_R
+template <typename T, bool HAS_G, bool REBUILD = false> struct Bwd2StatsOp {
   const T* G; const float* dz; const float* wf; const T* out; const T* t;
   const float* mean; const float* invstd; int ld; T* du_out;
-  struct Cst { float wf[VE<T>], mu[VE<T>], is[VE<T>]; };
+  const float* sc = nullptr; const float* sh = nullptr;
+  struct Cst { float wf[VE<T>], mu[VE<T>], is[VE<T>], sc[REBUILD ? VE<T> : 1], sh[REBUILD ? VE<T> : 1]; };
   struct Reg { float o[VE<T>], t[VE<T>], g[VE<T>]; float d = 0.f; };
   __device__ void prep(int c, Cst& q) const {
     if (!HAS_G) ldc(wf + c, q.wf);
     ldc(mean + c, q.mu); ldc(invstd + c, q.is);
+    if constexpr (REBUILD) { ldc(sc + c, q.sc); ldc(sh + c, q.sh); }
   }
   __device__ void load(int64_t r, int c, Reg& q) const {
     ldv<T>(out + r * ld + c, q.o);
@@ -301,6 +306,10 @@ template <typename T, bool HAS_G> struct Bwd2StatsOp {
   // du = g * [out > 0] is stored (storage type) and the sums use the stored
   // value, so the apply pass needs only du and t
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[3][VE<T>]) const {
+    if constexpr (REBUILD) {
+#pragma unroll
+      for (int v = 0; v < VE<T>; ++v) q.o[v] = (float)(T)fmaxf(q.t[v] * k.sc[v] + k.sh[v] + q.o[v], 0.f);
+    }
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
       float g = HAS_G ? q.g[v] : q.d * k.wf[v];
@@ -421,7 +430,7 @@ template <typename T> struct Bwd1ApplyOp {
 #ifndef BWD2_STATS_UNROLL
 #define BWD2_STATS_UNROLL 2
 #endif
-template <typename T, bool G> struct RowUnroll<Bwd2StatsOp<T, G>> { static constexpr int v = BWD2_STATS_UNROLL; };
+template <typename T, bool G, bool R> struct RowUnroll<Bwd2StatsOp<T, G, R>> { static constexpr int v = BWD2_STATS_UNROLL; };
 template <typename T> struct RowUnroll<BnAddReluHeadOp<T>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<Bwd1ApplyOp<T>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<Bwd2ApplyOp<T>> { static constexpr int v = 2; };
@@ -894,7 +903,12 @@ template <typename T>
 static dcnr_status bwd2_stats_impl(const void* G, const float* dz, const float* wf, const void* out,
                                    const void* t, const float* mean, const float* invstd,
                                    int64_t B, int N, int ld, void* du, float* part, int* nc,
-                                   hipStream_t s) {
+                                   hipStream_t s, const void* x, const float* sc, const float* sh) {
+  if (!G && x) {
+    Bwd2StatsOp<T, false, true> op{nullptr, dz, wf, (const T*)x, (const T*)t, mean, invstd, ld,
+                                   (T*)du, sc, sh};
+    return run_rowcol<T, 3>(op, B, N, part, nc, s);
+  }
   if (G) {
     Bwd2StatsOp<T, true> op{(const T*)G, dz, wf, (const T*)out, (const T*)t, mean, invstd, ld,
                             (T*)du};
@@ -907,10 +921,10 @@ static dcnr_status bwd2_stats_impl(const void* G, const float* dz, const float* 
 dcnr_status bwd_bn2_stats3(int precision, const void* G, const float* dz, const float* wf,
                            const void* out, const void* t, const float* mean, const float* invstd,
                            int64_t B, int N, int ld, void* du, float* part, int* nchunks,
-                           hipStream_t s) {
+                           hipStream_t s, const void* x, const float* sc, const float* sh) {
   return precision == DCNR_PREC_BF16
-             ? bwd2_stats_impl<bf16>(G, dz, wf, out, t, mean, invstd, B, N, ld, du, part, nchunks, s)
-             : bwd2_stats_impl<float>(G, dz, wf, out, t, mean, invstd, B, N, ld, du, part, nchunks, s);
+             ? bwd2_stats_impl<bf16>(G, dz, wf, out, t, mean, invstd, B, N, ld, du, part, nchunks, s, x, sc, sh)
+             : bwd2_stats_impl<float>(G, dz, wf, out, t, mean, invstd, B, N, ld, du, part, nchunks, s, x, sc, sh);
 }
 
 template <typename T>
