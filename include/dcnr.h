@@ -96,7 +96,9 @@ typedef enum { DCNR_EVAL = 0, DCNR_TRAIN = 1 } dcnr_mode;
  * kernels, same results; more workspace.  In eval mode it keeps the
  * unfused tail (BN affine finalize launch, the last block's output h_R in
  * the workspace, separate head dot); without it the bf16 eval forward ends
- * in the last GEMM's head epilogue and never stores h_R. */
+ * in the last GEMM's head epilogue and never stores h_R; likewise the bf16
+ * train forward does not store h_R (the backward rebuilds it from t2 and
+ * h_{R-1}), so DCNR_WS_H at index R is only meaningful with this flag. */
 #define DCNR_FLAG_KEEP_INTERMEDIATES 2u
 
 /* Optional collective hook for SyncBN across data-parallel ranks: called
