@@ -109,50 +109,13 @@ namespace {
 // stream (both on this device: a device-scope release/acquire orders them;
 // without the system-scope fence the step measured 4.019 vs 4.051 ms,
 // alternating A/B x3 on one box, profiles/lab/r03x_event_fence_ab.txt).
-#ifndef DCNR_EV_NOFENCE
-#define DCNR_EV_NOFENCE 1
-#endif
-constexpr unsigned SYNC_EV = hipEventDisableTiming | (DCNR_EV_NOFENCE ? hipEventDisableSystemFence : 0u);
+constexpr unsigned SYNC_EV = hipEventDisableTiming | hipEventDisableSystemFence;
 
-// workgroups of the residual blocks' weight-gradient GEMMs, which overlap the
-// dX chain on the side stream (0: one per CU, as for the initial layer's, the
-// last one of the backward)
-#ifndef DW_WG_BLOCKS
-#define DW_WG_BLOCKS 0
-#endif
-// bf16 train: the backward's dt2 / dt1 buffers alternate between two sets by
-// block parity, so a main-stream writer of one never waits for the side
-// stream's weight-gradient GEMM of the block just before (lab knob: 0 = one
-// shared set, the round-2 pipe that waited on the previous call)
-#ifndef DW_DOUBLE_BUF
-#define DW_DOUBLE_BUF 1
-#endif
-// BN statistics reduced + finalised by the last workgroup of the producing
-// GEMM (no SyncBN hook): one launch less per BatchNorm layer (lab knob: 0 =
-// separate reduce launch)
-// the side-stream pipe's dependency on the main stream's BN apply pass is
-// that launch's own completion event (hipExtLaunchKernel stop event) instead
-// of a marker recorded after it, and with the alternating dt sets the main
-// stream waits for the side once per block (lab knob: 0 = marker per call)
-#ifndef DW_EXT_EV
-#define DW_EXT_EV 0
-#endif
-// lab: each block's weight-gradient call enqueued after the dX GEMM that
-// follows its apply pass, so the side stream's gemm_dw overlaps the next BN
-// apply pass (a row pass that can share a CU with it) rather than the dX
-// GEMM (which cannot: both need most of a CU's LDS)
-#ifndef DW_AFTER_DX
-#define DW_AFTER_DX 0
-#endif
-// bf16 train: the last block's head pass does not store h_R; the backward's
-// BN2 statistics pass rebuilds it from t2, h_{R-1} and the BN2 affine
-// (KEEP_INTERMEDIATES still stores it for the stage tests)
-#ifndef TRAIN_HEAD_REBUILD
-#define TRAIN_HEAD_REBUILD 1
-#endif
-#ifndef WS_FUSE_RED
-#define WS_FUSE_RED 0
-#endif
+// Measured and rejected side-stream pipe variants:
+// the apply pass's own completion event as the dependency (+1.4 %), the
+// weight-gradient call after the dX GEMM (+3.5 %), fewer workgroups for the
+// overlapped weight-gradient GEMMs, BN statistics reduced by the producing
+// GEMM's last workgroup (+2.3-3.7 %).
 
 // One side stream per device (created on first use, never destroyed) for the
 // backward's work that does not depend on the deep tower; fork/join events
@@ -364,8 +327,11 @@ bool masks_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && d.Hp % 32 == 0
 int dq_of(const Dims& d) { return (int)rup(d.Dp, 32); }
 bool keep_of(const dcnr_model_desc* desc) { return (desc->flags & DCNR_FLAG_KEEP_INTERMEDIATES) != 0; }
 
+// bf16 train: the last block's head pass does not store h_R; the backward's
+// BN2 statistics pass rebuilds it from t2, h_{R-1} and the BN2 affine
+// (KEEP_INTERMEDIATES still stores it for the stage tests)
 bool head_rebuild(const Dims& d, bool train) {
-  return TRAIN_HEAD_REBUILD && train && d.prec == DCNR_PREC_BF16 && bn_add_relu_head_supported(d.prec, d.Hp);
+  return train && d.prec == DCNR_PREC_BF16 && bn_add_relu_head_supported(d.prec, d.Hp);
 }
 bool eval_fuse_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && gemm_ws_supported(d.Hp, d.Hp); }
 
@@ -411,7 +377,10 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
   }
   L.zc = (float*)b.take(B * 4);
   L.zdeep = (float*)b.take(B * 4);
-  if (!train && !keep && eval_fuse_ok(d) && d.R >= 1)   // the last eval GEMM's head partials
+  // the last eval GEMM's head partials (32-bit buffer offsets: at Hp = 512
+  // up to ~33M rows; larger batches take the unfused, M-chunked tail)
+  if (!train && !keep && eval_fuse_ok(d) && d.R >= 1 &&
+      (int64_t)B * gemm_ws_head_parts(d.Hp) * 4 < (int64_t(1) << 31))
     L.headp = (float*)b.take((size_t)B * gemm_ws_head_parts(d.Hp) * 4);
   for (int i = 0; i < 2 * d.R; ++i) {
     L.bn[i].scale = (float*)b.take(d.Hp * 4);
@@ -434,7 +403,6 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
     // split count depends on the tile count (narrow H -> more splits)
     L.slab_elems = std::max<int64_t>({(int64_t)64 * d.Hp * std::max(d.Hp, d.Dp),
                                       (int64_t)gemm_dw_splits(d.Hp, d.Hp, B) * d.Hp * d.Hp,
-                                      (int64_t)gemm_dw_splits(d.Hp, d.Hp, B, DW_WG_BLOCKS) * d.Hp * d.Hp,
                                       (int64_t)gemm_dw_splits(d.Hp, d.Dp, B) * d.Hp * d.Dp});
     L.slab = (float*)b.take((size_t)L.slab_elems * 4);
     L.sc = (float*)b.take((size_t)B * (2 * d.L + 1) * 4);
@@ -452,7 +420,10 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
       L.emb.tmp_bytes = emb_sort_tmp_bytes(d.rows, d.widths, 2 + d.K, B);
       L.emb.tmp = b.take(L.emb.tmp_bytes);
     }
-    if (DW_DOUBLE_BUF && !keep && d.prec == DCNR_PREC_BF16 && d.R > 1) {
+    // the backward's dt2 / dt1 buffers alternate between two sets by block
+    // parity, so a main-stream writer of one never waits for the side
+    // stream's weight-gradient GEMM of the block just before
+    if (!keep && d.prec == DCNR_PREC_BF16 && d.R > 1) {
       L.dt2b = b.take(act);
       L.dt1b = b.take(act);
     }
@@ -643,14 +614,11 @@ dcnr_status linear_bn_relu(const Dims& d, const void* A, const void* W, const fl
 }
 
 // t = A W^T + b  and  part = BN column partials of t, shifted by b (nc rows)
-// (rf: reduce and finalise the partials in the same launch when it can; *nc
-// is then -1)
 dcnr_status linear_fwd_stats(const Dims& d, const Layout& L, const void* A, int lda, const void* W,
                              int K, const float* bias, void* out, int64_t B, int* nc,
-                             hipStream_t s, const RedFinal* rf = nullptr) {
+                             hipStream_t s) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
-  if (rf) { a.fuse_red = WS_FUSE_RED; a.rf = *rf; a.Nr = d.H; }
   a.X = (const bf16*)A; a.ldx = lda; a.M = B; a.K = K;
   a.W = (const bf16*)W; a.ldw = K; a.N = d.Hp;
   a.C = out; a.ldc = d.Hp; a.bias = bias;
@@ -661,11 +629,9 @@ dcnr_status linear_fwd_stats(const Dims& d, const Layout& L, const void* A, int 
 // C = mask(H) * (X W^T [+ R]) and part = [sum C, sum C*xhat(T)] (BN backward)
 dcnr_status linear_dx_bn(const Dims& d, const Layout& L, int epi, const void* X, const void* Wt,
                          const void* R, void* C, const uint8_t* Hbits, float hscale,
-                         const void* T, const BnBufs& bn, int64_t B, int* nc, hipStream_t s,
-                         const RedFinal* rf = nullptr) {
+                         const void* T, const BnBufs& bn, int64_t B, int* nc, hipStream_t s) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
-  if (rf) { a.fuse_red = WS_FUSE_RED; a.rf = *rf; a.Nr = d.H; }
   a.X = (const bf16*)X; a.ldx = d.Hp; a.M = B; a.K = d.Hp;
   a.W = (const bf16*)Wt; a.ldw = d.Hp; a.N = d.Hp;
   a.C = C; a.ldc = d.Hp;
@@ -719,7 +685,6 @@ struct DwPipe {
   hipEvent_t dw_ev[RING] = {};
   int calls = 0, lag = 1;
   bool pending = false;   // side work enqueued since the last join
-  bool primed = false;    // in_ev is the completion event of the last apply launch
   dcnr_status init(hipStream_t side_stream, int lag_calls) {
     side = side_stream;
     lag = lag_calls;
@@ -730,34 +695,22 @@ struct DwPipe {
   }
   // order the side stream after the main stream's work so far (and the main
   // stream after call (calls - lag)'s GEMM, see above)
-  // (lag 3 with DW_EXT_EV: odd calls wait for call n-2, the block-before's
-  // dW1 -- the side stream is in order, so that covers calls n-3 and n-2,
-  // whose dY the next two apply passes overwrite -- even calls wait for none)
   dcnr_status enter(hipStream_t main_s) {
-    if (DW_EXT_EV && lag == 3) {
-      if ((calls & 1) && calls >= 3) DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev[(calls - 2) % RING], 0));
-    } else if (calls >= lag) {
-      DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev[(calls - lag) % RING], 0));
-    }
-    if (!primed || g_stop_ev) {   // no apply launch took the event: record it here
-      g_stop_ev = nullptr;
-      DCNR_HIP(hipEventRecord(in_ev, main_s));
-    }
-    primed = false;
+    if (calls >= lag) DCNR_HIP(hipStreamWaitEvent(main_s, dw_ev[(calls - lag) % RING], 0));
+    DCNR_HIP(hipEventRecord(in_ev, main_s));
     DCNR_HIP(hipStreamWaitEvent(side, in_ev, 0));
     main = main_s;
     pending = true;
     return DCNR_OK;
   }
   dcnr_status wgrad(const Layout& L, const void* dY, int64_t ldy, int N, const void* X, int64_t ldx,
-                    int Kc, int64_t B, float* out, int Nr, int Kr, int accumulate, hipStream_t main_s,
-                    int wg_target) {
+                    int Kc, int64_t B, float* out, int Nr, int Kr, int accumulate, hipStream_t main_s) {
     TRY(enter(main_s));
     const int call = calls++;
     hipStream_t s = side;   // TRYB launches and times on the side stream
     // (the full-chip split count: 32 / 16 splits, leaving CUs to the main
     // stream and halving the slab, measured 2 % / 21 % slower per step)
-    const int S = gemm_dw_splits(N, Kc, B, wg_target);
+    const int S = gemm_dw_splits(N, Kc, B);
     if ((int64_t)S * N * Kc > L.slab_elems) {
       set_error("wgrad: slab too small");
       return DCNR_WORKSPACE_TOO_SMALL;
@@ -774,12 +727,6 @@ struct DwPipe {
          splitk_reduce_t(L.slab, S, (int64_t)N * Kc, N, Nr, Kr, out, accumulate, s));
     return DCNR_OK;
   }
-  // the next row-pass launch on the main stream signals in_ev when it completes
-  void prime() {
-    if (!DW_EXT_EV) return;
-    g_stop_ev = in_ev;
-    primed = true;
-  }
   dcnr_status join(hipStream_t main_s) {
     if (!pending) return DCNR_OK;
     DCNR_HIP(hipEventRecord(done_ev, side));
@@ -788,7 +735,6 @@ struct DwPipe {
     return DCNR_OK;
   }
   ~DwPipe() {
-    g_stop_ev = nullptr;
     if (pending && main) {   // error path: order the side work before the caller's stream
       (void)hipEventRecord(done_ev, side);
       (void)hipStreamWaitEvent(main, done_ev, 0);
@@ -802,9 +748,9 @@ struct DwPipe {
 
 dcnr_status linear_dw(const Dims& d, const Layout& L, const void* dY, int ldy, int N,
                       const void* X, int ldx, int Kc, int64_t B, float* out, int Nr, int Kr,
-                      int accumulate, hipStream_t s, DwPipe* pipe = nullptr, int wg_target = 0) {
+                      int accumulate, hipStream_t s, DwPipe* pipe = nullptr) {
   if (d.prec == DCNR_PREC_BF16 && gemm_dw_supported(N, Kc, ldy, ldx, B)) {
-    if (pipe) return pipe->wgrad(L, dY, ldy, N, X, ldx, Kc, B, out, Nr, Kr, accumulate, s, wg_target);
+    if (pipe) return pipe->wgrad(L, dY, ldy, N, X, ldx, Kc, B, out, Nr, Kr, accumulate, s);
     return wgrad_bf16(dY, ldy, N, X, ldx, Kc, B, L.slab, L.slab_elems, out, Nr, Kr, accumulate, s);
   }
   // the generic path below writes the slab on this stream: the side stream's
@@ -848,14 +794,6 @@ RedFinal red_init(const Layout& L, int mode, double count, int accumulate) {
   return rf;
 }
 
-// nc_pre > 0: the partials of t are already in L.part (from the GEMM epilogue),
-// shifted by shiftf (the Linear bias); otherwise a stats pass over t makes them.
-RedFinal bn_fwd_rf(const Layout& L, int64_t B, const float* gamma, const float* beta, float* rm,
-                   float* rv, int64_t* nbt, const BnBufs& bb) {
-  RedFinal rf = red_init(L, RED_BN_FWD, (double)B, 0);
-  rf.f = BnFinal{gamma, beta, rm, rv, nbt, bb.scale, bb.shift, bb.mean, bb.invstd};
-  return rf;
-}
 
 RedFinal bn_bwd_rf(const Layout& L, int64_t B, const float* gamma, const float* invstd,
                    float* dgamma, float* dbeta, float* dwf, float* dbias_pre, int accumulate) {
@@ -866,13 +804,14 @@ RedFinal bn_bwd_rf(const Layout& L, int64_t B, const float* gamma, const float* 
   return rf;
 }
 
+// nc_pre > 0: the partials of t are already in L.part (from the GEMM epilogue),
+// shifted by shiftf (the Linear bias); otherwise a stats pass over t makes them.
 dcnr_status bn_layer_fwd(const dcnr_model_desc* desc, const Dims& d, const Layout& L,
                          const void* t, int64_t B, bool train, const float* gamma,
                          const float* beta, float* rm, float* rv, int64_t* nbt,
                          const BnBufs& bb, hipStream_t s, int nc_pre = 0,
                          const float* shiftf = nullptr) {
   BnFinal f{gamma, beta, rm, rv, nbt, bb.scale, bb.shift, bb.mean, bb.invstd};
-  if (train && nc_pre < 0) return DCNR_OK;   // reduced and finalised by the GEMM launch
   if (train) {
     int nc = nc_pre;
     const void* shift = nc_pre ? nullptr : t;
@@ -901,7 +840,6 @@ dcnr_status bn_bwd_reduce(const dcnr_model_desc* desc, const Dims& d, const Layo
                           float* dgamma, float* dbeta, float* dwf, float* dbias_pre,
                           int accumulate, hipStream_t s) {
   const int Hp = d.Hp, H = d.H;
-  if (nc < 0) return DCNR_OK;   // reduced and finalised by the dX GEMM launch
   if (!desc->bn_allreduce) {
     RedFinal rf = bn_bwd_rf(L, B, gamma, invstd, dgamma, dbeta, dwf, dbias_pre, accumulate);
     TRYP(DCNR_K_REDUCE, reduce_fused(DCNR_PREC_FP32, L.part, nc, NK, Hp, H, nullptr, rf, s));
@@ -1132,16 +1070,9 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     const auto& Bk = P.blk[j];
     const bool fuse = train && epi_stats_ok(d);   // BN partials from the GEMM epilogue
     int nc = 0;
-    // local BN: the GEMM's last workgroups reduce and finalise the statistics
-    RedFinal rf1 = bn_fwd_rf(L, B, Bk.g1, Bk.be1, Bk.rm1, Bk.rv1, Bk.nbt1, L.bn[2 * j]);
-    RedFinal rf2 = bn_fwd_rf(L, B, Bk.g2, Bk.be2, Bk.rm2, Bk.rv2, Bk.nbt2, L.bn[2 * j + 1]);
-    rf1.shiftf = L.b1p[j];
-    rf2.shiftf = L.b2p[j];
-    const bool local = !desc->bn_allreduce;
     if (fuse)
       TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
-           linear_fwd_stats(d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, &nc, s,
-                            local ? &rf1 : nullptr));
+           linear_fwd_stats(d, L, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, &nc, s));
     else
       TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
            linear_fwd(d, L.h[j], d.Hp, L.W1p[j], d.Hp, L.b1p[j], L.t1[j], B, s));
@@ -1152,8 +1083,7 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
                      dropout_seed, j, s, train ? L.mask_a1[j] : nullptr));
     if (fuse)
       TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
-           linear_fwd_stats(d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, &nc, s,
-                            local ? &rf2 : nullptr));
+           linear_fwd_stats(d, L, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, &nc, s));
     else
       TRYB(DCNR_K_GEMM_FWD, 2 * act_b(d, B) + w_b(d, d.Hp),
            linear_fwd(d, a1, d.Hp, L.W2p[j], d.Hp, L.b2p[j], L.t2[j], B, s));
@@ -1256,8 +1186,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
 
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   const bool fuse = epi_stats_ok(d);   // BN partials from the dX GEMM epilogues
-  int nc_du = 0;   // != 0: L.du and its BN2 partials (> 0) or finalised BN2 backward (-1)
-                   // were made by the previous dX GEMM
+  int nc_du = 0;   // > 0: L.du and its BN2 partials were made by the previous dX GEMM
   for (int j = d.R - 1; j >= 0; --j) {
     const auto& Bk = P.blk[j];
     auto& Gk = Gr.blk[j];
@@ -1282,7 +1211,6 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRY(bn_bwd_reduce(desc, d, L, nc, 3, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2,
                         Gin ? nullptr : Gr.wf, Gk.b2, accumulate, s));
     }
-    if (pipe) pipe->prime();   // the apply pass below signals the dW2 call's dependency
     if (!Gin && j == d.R - 1 && L.mask_h[d.R] && d.prec == DCNR_PREC_BF16)
       TRYB(DCNR_K_ROWWISE, 2 * act_b(d, B) + mask_b(d, B) + 4.0 * B,
            bwd_bn2_apply_rank1(L.mask_h[d.R], dz, P.wf, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
@@ -1291,16 +1219,13 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn2_apply2(d.prec, du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
                          dt2, L.part, &nc, s));
     // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
-    if (!DW_AFTER_DX)
-      TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
+    TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe));
     if (fuse) {
       // dy1 = (dt2 W2) * [a1 != 0] / (1-p): relu and dropout masks from the
-      // saved activation, BN1 partials (and, without SyncBN, its backward
-      // coefficients and dgamma/dbeta) in the same pass
-      const RedFinal rf = bn_bwd_rf(L, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1, accumulate);
+      // saved activation, BN1 partials in the same pass
       TRYB(DCNR_K_GEMM_DX, 3 * act_b(d, B) + mask_b(d, B) + w_b(d, d.Hp), linear_dx_bn(d, L, NT_EPI_DROP_BN, dt2, L.W2t[j], nullptr, da,
                                         L.mask_a1[j], p > 0.f ? 1.f / (1.f - p) : 1.f, L.t1[j],
-                                        bn1, B, &nc, s, desc->bn_allreduce ? nullptr : &rf));
+                                        bn1, B, &nc, s));
     } else {
       GemmArgs g;
       memset(&g, 0, sizeof(g));
@@ -1311,26 +1236,19 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_stats(d.prec, da, L.t1[j], bn1.scale, bn1.shift, bn1.mean,
                                          bn1.invstd, B, Hp, Hp, p, dropout_seed, j, L.part, &nc, s));
     }
-    if (DW_AFTER_DX)
-      TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
     TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
                         accumulate, s));
-    if (pipe) pipe->prime();
     TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_apply2(d.prec, da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, dt1,
                        L.part, &nc, s));
     // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
-    if (!DW_AFTER_DX)
-      TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
+    TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe));
     if (fuse && j > 0) {
       // G is only consumed by block j-1's BN2 backward: emit its du = G * [h_j > 0]
       // (in place over this block's du, the residual operand, unless
       // KEEP_INTERMEDIATES) and the partials
       const BnBufs& bp = L.bn[2 * (j - 1) + 1];
-      const RedFinal rf = bn_bwd_rf(L, B, P.blk[j - 1].g2, bp.invstd, Gr.blk[j - 1].g2,
-                                    Gr.blk[j - 1].be2, nullptr, Gr.blk[j - 1].b2, accumulate);
       TRYB(DCNR_K_GEMM_DX, 4 * act_b(d, B) + mask_b(d, B) + w_b(d, d.Hp), linear_dx_bn(d, L, NT_EPI_RESID_BN, dt1, L.W1t[j], du, L.duk[j - 1],
-                                        L.mask_h[j], 1.f, L.t2[j - 1], bp, B, &nc_du, s,
-                                        desc->bn_allreduce ? nullptr : &rf));
+                                        L.mask_h[j], 1.f, L.t2[j - 1], bp, B, &nc_du, s));
       Gin = L.duk[j - 1];
     } else {
       GemmArgs g;
@@ -1342,8 +1260,6 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       Gin = L.G;
       nc_du = 0;
     }
-    if (DW_AFTER_DX)
-      TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe, DW_WG_BLOCKS));
   }
   // ---- initial layer
   // its bias gradient (column sums of G) also goes under the dx0 GEMM and

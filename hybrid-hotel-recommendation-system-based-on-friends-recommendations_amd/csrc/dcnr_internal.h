@@ -14,7 +14,6 @@ namespace dcnr {
 // completion (hipExtLaunchKernel's stop event: no separate marker packet on
 // the stream) and clears it.  The backward's side-stream weight-gradient
 // pipe uses it to depend on the BN apply pass that wrote its dY.
-extern thread_local hipEvent_t g_stop_ev;
 
 typedef __bf16 bf16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -77,21 +76,15 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 // and drains them (vmcnt(0)) before every ds_read, which would serialise a stage ring;
 // the caller's counted vmcnt waits are the only synchronisation.
 // M0 is saved and restored inside the statement (it is compiler-reserved).
-#ifndef DCNR_DMA_NT
-#define DCNR_DMA_NT 0
-#endif
-#if DCNR_DMA_NT
-#define DCNR_DMA_POLICY "nt "
-#else
-#define DCNR_DMA_POLICY ""
-#endif
+// (Default cache policy: the nt policy measured 4.06 -> 4.17 ms per step,
+// profiles/lab/r03ae_dma_nt_ab.txt.)
 __device__ __forceinline__ void dma16(u32x4 rsrc, int off, uint32_t lds_dst) {
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen " DCNR_DMA_POLICY "lds\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
       : "v"(off), "s"(rsrc), "s"(lds_dst)
@@ -367,19 +360,11 @@ struct NtArgs {
   const float* wf; float* headp; int64_t ldh;      // BN_RESID_RELU_HEAD (wf: Nr entries;
                                                     // headp rows ldh apart, ldh >= M)
   float* part;                                      // column partials (stats epilogues)
-  // stats epilogues: with fuse_red the launch's last workgroup per column
-  // slice also sums the partial rows (reduce_small's fixed order) and runs
-  // red_finalize(rf) on them (columns >= Nr are padding); gemm_ws then
-  // reports nparts = -1 (nothing left to reduce)
-  int fuse_red; int Nr; RedFinal rf;
+  int Nr;                                           // real columns (eval BN / head: N pads to 8)
   int nslices, groups; int64_t mtiles;   // filled by gemm_ws
 };
-// hand-off counter slots of gemm_ws's in-launch reductions (above the ones
-// reduce_fused uses)
-constexpr int CNT_WS_BASE = 256;
 bool gemm_ws_supported(int64_t K, int64_t N);
-// nparts (stats epilogues): rows of part written (the nchunks of reduce_fused),
-// or -1 when a.fuse_red reduced and finalised them in the launch
+// nparts (stats epilogues): rows of part written (the nchunks of reduce_fused)
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
 // head partials of NT_EPI_BN_RESID_RELU_HEAD: rows of headp written (0: unsupported shape)
 int gemm_ws_head_parts(int64_t N);
@@ -397,7 +382,7 @@ struct DwArgs {
 };
 bool gemm_dw_supported(int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t Btot);
 // split count for ~wg_target workgroups (0: the default, one per CU)
-int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot, int wg_target = 0);
+int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot);
 dcnr_status gemm_dw(const DwArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ elementwise

@@ -20,13 +20,11 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int UNROLL = 4;
-#ifndef ROWWISE_RED_CHUNKS
-#define ROWWISE_RED_CHUNKS 2048
-#endif
-constexpr int TARGET_CHUNKS = ROWWISE_RED_CHUNKS;  // 8 blocks/CU in flight for HBM latency hiding
-#ifndef ROWWISE_APPLY_CHUNKS
-#define ROWWISE_APPLY_CHUNKS 8192
-#endif
+// reduction passes: 2048 partial rows (8 blocks/CU in flight for HBM latency
+// hiding); apply passes: 8192 short blocks (4096 / 16384 measured the same,
+// 1024 / 512 reduction chunks slower: DESIGN.md section 8, round 2)
+constexpr int TARGET_CHUNKS = 2048;
+constexpr int APPLY_CHUNKS = 8192;
 
 template <typename T> constexpr int VE = 16 / (int)sizeof(T);
 
@@ -139,18 +137,12 @@ dcnr_status run_rowcol(const Op& op, int64_t B, int N, float* part, int* nchunks
   }
   // apply-only passes (no partials) take one short block per 16 rows (one
   // load round per thread); reduction passes keep TARGET_CHUNKS partial rows
-  int rows = NK == 0 ? (int)std::max<int64_t>(16, cdiv(B, ROWWISE_APPLY_CHUNKS))
+  int rows = NK == 0 ? (int)std::max<int64_t>(16, cdiv(B, APPLY_CHUNKS))
                      : (int)std::max<int64_t>(32, cdiv(B, TARGET_CHUNKS));
   int nc = (int)cdiv(B, rows);
   if (nchunks) *nchunks = nc;
   if (B <= 0) return DCNR_OK;
-  if (g_stop_ev) {
-    hipExtLaunchKernelGGL((rowcol_kernel<T, NK, Op>), dim3(nc), dim3(NT), 0, s, nullptr, g_stop_ev, 0,
-                          op, B, N, rows, part);
-    g_stop_ev = nullptr;
-  } else {
-    hipLaunchKernelGGL((rowcol_kernel<T, NK, Op>), dim3(nc), dim3(NT), 0, s, op, B, N, rows, part);
-  }
+  hipLaunchKernelGGL((rowcol_kernel<T, NK, Op>), dim3(nc), dim3(NT), 0, s, op, B, N, rows, part);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
@@ -427,10 +419,8 @@ template <typename T> struct Bwd1ApplyOp {
   }
 };
 
-#ifndef BWD2_STATS_UNROLL
-#define BWD2_STATS_UNROLL 2
-#endif
-template <typename T, bool G, bool R> struct RowUnroll<Bwd2StatsOp<T, G, R>> { static constexpr int v = BWD2_STATS_UNROLL; };
+// (1 / 4 rows in flight measured the same / slower: DESIGN.md section 8)
+template <typename T, bool G, bool R> struct RowUnroll<Bwd2StatsOp<T, G, R>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<BnAddReluHeadOp<T>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<Bwd1ApplyOp<T>> { static constexpr int v = 2; };
 template <typename T> struct RowUnroll<Bwd2ApplyOp<T>> { static constexpr int v = 2; };
@@ -753,8 +743,6 @@ dcnr_status reduce_fused(int precision, const float* part, int nchunks, int NK, 
 }
 
 // ================================================================== API
-thread_local hipEvent_t g_stop_ev = nullptr;
-
 dcnr_status pack_weights(int precision, const PackBatch& pb, hipStream_t s) {
   if (pb.n == 0) return DCNR_OK;
   for (int i = 0; i < pb.n; ++i)
@@ -1011,25 +999,20 @@ namespace {
 // bits as summing the untransposed slabs), transposes through LDS, writes
 // rows of out along k (16-B stores when out's rows allow).
 constexpr int RT_K = 64, RT_N = 16;
-// RT_ZG thread groups per output tile would each sum a contiguous share of
-// the splits and add the partials in group order (lab knob): measured 12-13
-// us alone either way per 512 x 512 call (the one-group kernel is not
-// latency-bound), 40-54 us median under the concurrent dX chain; one group
-// kept -- the summation order of the earlier rounds.
-#ifndef RT_ZG
-#define RT_ZG 1
-#endif
-__global__ __launch_bounds__(256 * RT_ZG) void splitk_reduce_t_kernel(const float* slab, int splits,
-                                                                      int64_t stride, int ld, int N, int K,
-                                                                      float* out, int accumulate, int vec_out) {
-  __shared__ float t[RT_ZG][RT_K][RT_N + 1];
+// (Several thread groups per output tile, each summing a contiguous share of
+// the splits, measured 12-13 us alone either way per 512 x 512 call and
+// 40-54 us under the concurrent dX chain; one group kept -- the summation
+// order of the earlier rounds.)
+__global__ __launch_bounds__(256) void splitk_reduce_t_kernel(const float* slab, int splits,
+                                                              int64_t stride, int ld, int N, int K,
+                                                              float* out, int accumulate, int vec_out) {
+  __shared__ float t[RT_K][RT_N + 1];
   const int k0 = blockIdx.x * RT_K, n0 = blockIdx.y * RT_N;
-  const int zg = threadIdx.x >> 8, idx = threadIdx.x & 255;
+  const int idx = threadIdx.x;
   {
     const int kk = idx >> 2, nq = idx & 3;
     const int k = k0 + kk, n = n0 + 4 * nq;
-    const int per = (splits + RT_ZG - 1) / RT_ZG;
-    const int z0 = zg * per, z1 = min(splits, z0 + per);
+    const int z0 = 0, z1 = splits;
     float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     if (k < K && n < N) {
       const float* base = slab + (int64_t)k * ld + n;
@@ -1046,21 +1029,15 @@ __global__ __launch_bounds__(256 * RT_ZG) void splitk_reduce_t_kernel(const floa
         s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
       }
     }
-    t[zg][kk][4 * nq] = s.x; t[zg][kk][4 * nq + 1] = s.y; t[zg][kk][4 * nq + 2] = s.z; t[zg][kk][4 * nq + 3] = s.w;
+    t[kk][4 * nq] = s.x; t[kk][4 * nq + 1] = s.y; t[kk][4 * nq + 2] = s.z; t[kk][4 * nq + 3] = s.w;
   }
   __syncthreads();
-  if (zg) return;
   const int nn = idx >> 4, kq = idx & 15;
   const int n = n0 + nn, k = k0 + 4 * kq;
   if (n >= N) return;
   float v[4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float a = t[0][4 * kq + j][nn];
-#pragma unroll
-    for (int g = 1; g < RT_ZG; ++g) a += t[g][4 * kq + j][nn];
-    v[j] = a;
-  }
+  for (int j = 0; j < 4; ++j) v[j] = t[4 * kq + j][nn];
   float* o = out + (int64_t)n * K + k;
   if (vec_out && k + 3 < K) {
     float4 r = make_float4(v[0], v[1], v[2], v[3]);
@@ -1086,7 +1063,7 @@ dcnr_status splitk_reduce_t(const float* slab, int splits, int64_t slab_stride, 
   }
   const int vec_out = K % 4 == 0 && (uintptr_t)out % 16 == 0;
   hipLaunchKernelGGL(splitk_reduce_t_kernel, dim3((unsigned)cdiv(K, RT_K), (unsigned)cdiv(N, RT_N)),
-                     dim3(256 * RT_ZG), 0, s, slab, splits, slab_stride, ld_slab, N, K, out, accumulate,
+                     dim3(256), 0, s, slab, splits, slab_stride, ld_slab, N, K, out, accumulate,
                      vec_out);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;

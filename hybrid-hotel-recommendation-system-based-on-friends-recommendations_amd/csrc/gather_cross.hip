@@ -22,13 +22,6 @@
 
 #include <cstring>
 
-// tools/gather_lab.hip rebuilds this file with GC_LAB_MODE bits set to time
-// parts of the kernels in isolation (forward 1: no x0 stores, 2: no cross
-// compute, 4: no row loads).  The library always builds mode 0.
-#ifndef GC_LAB_MODE
-#define GC_LAB_MODE 0
-#endif
-
 namespace dcnr {
 namespace {
 
@@ -166,10 +159,7 @@ __global__ __launch_bounds__(NT) void gather_cross_fwd_kernel(GatherDesc g, Cros
     for (int u = 0; u < SPW; ++u) {
       const int s = w * SPW + u;
       const int64_t b = b0 + s;
-      if constexpr (!(GC_LAB_MODE & 4))
-        load_row<RM>(m, ids + s * g.n_tab, b < B ? b : B - 1, x[u]);
-      else
-        for (int r = 0; r < RM; ++r) x[u][r] = (float)ids[s * g.n_tab + (r & 1)];
+      load_row<RM>(m, ids + s * g.n_tab, b < B ? b : B - 1, x[u]);
     }
     // x0 in the deep tower's storage type.  bf16: staged through this wave's
     // LDS row so every lane stores 16 contiguous bytes (8 columns)
@@ -177,26 +167,24 @@ __global__ __launch_bounds__(NT) void gather_cross_fwd_kernel(GatherDesc g, Cros
     for (int u = 0; u < SPW; ++u) {
       const int64_t b = b0 + w * SPW + u;
       if (x0 == nullptr) continue;
-      if constexpr (!(GC_LAB_MODE & 1)) {
-        if constexpr (sizeof(T) == 2) {
+      if constexpr (sizeof(T) == 2) {
 #pragma unroll
-          for (int r = 0; r < RM; ++r) {
-            const int e = lane + WAVE * r;
-            if (e < ldx) stage[e] = (bf16)x[u][r];   // pad columns get 0
-          }
-          if (b < B && lane * 8 < ldx)
-            *reinterpret_cast<uint4*>(x0 + b * ldx + lane * 8) =
-                *reinterpret_cast<const uint4*>(stage + lane * 8);
-          if constexpr (RM > 8)
-            if (b < B && (lane + 64) * 8 < ldx)
-              *reinterpret_cast<uint4*>(x0 + b * ldx + (lane + 64) * 8) =
-                  *reinterpret_cast<const uint4*>(stage + (lane + 64) * 8);
-        } else {
+        for (int r = 0; r < RM; ++r) {
+          const int e = lane + WAVE * r;
+          if (e < ldx) stage[e] = (bf16)x[u][r];   // pad columns get 0
+        }
+        if (b < B && lane * 8 < ldx)
+          *reinterpret_cast<uint4*>(x0 + b * ldx + lane * 8) =
+              *reinterpret_cast<const uint4*>(stage + lane * 8);
+        if constexpr (RM > 8)
+          if (b < B && (lane + 64) * 8 < ldx)
+            *reinterpret_cast<uint4*>(x0 + b * ldx + (lane + 64) * 8) =
+                *reinterpret_cast<const uint4*>(stage + (lane + 64) * 8);
+      } else {
 #pragma unroll
-          for (int r = 0; r < RM; ++r) {
-            const int e = lane + WAVE * r;
-            if (b < B && e < ldx) St<T>::st(x0 + b * ldx + e, x[u][r]);
-          }
+        for (int r = 0; r < RM; ++r) {
+          const int e = lane + WAVE * r;
+          if (b < B && e < ldx) St<T>::st(x0 + b * ldx + e, x[u][r]);
         }
       }
     }
@@ -223,7 +211,7 @@ __global__ __launch_bounds__(NT) void gather_cross_fwd_kernel(GatherDesc g, Cros
       }
     }
     // cross stack: the SPW (=4) samples' dot products are reduced together
-    if constexpr (!(GC_LAB_MODE & 2)) {
+    {
       for (int l = 0; l < L; ++l) {
         float d[SPW];
 #pragma unroll
@@ -534,18 +522,11 @@ dcnr_status launch_fwd(const GatherDesc& g, const CrossParams& cp, const int64_t
   return DCNR_OK;
 }
 
-#ifndef GC_V4_SPW
-#define GC_V4_SPW 4
-#endif
+constexpr int GC_V4_SPW = 4;   // samples per wave-tile
 // waves per launch (measured, same box, tools/ab_variants.sh): writing x0
 // (train / eval forward) 3072 (2048: +20 %, 6144: +12 % kernel time); the
 // gather + cross front alone (configs[1]) 2048 (+6 % pairs/s over 3072)
-#ifndef GC_V4_WAVES
-#define GC_V4_WAVES 3072
-#endif
-#ifndef GC_V4_WAVES_NOX0
-#define GC_V4_WAVES_NOX0 2048
-#endif
+constexpr int GC_V4_WAVES = 3072, GC_V4_WAVES_NOX0 = 2048;
 
 template <int R4, int X0BF16>
 dcnr_status launch_v4(const GatherDesc& g, const CrossParams& cp, const int64_t* user,

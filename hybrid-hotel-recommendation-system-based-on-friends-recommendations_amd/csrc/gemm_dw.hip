@@ -24,22 +24,13 @@
 //    4 consecutive n; summed and transposed back by splitk_reduce_t).
 #include "dcnr_internal.h"
 
-// tools/dw_lab.hip rebuilds this file with DW_LAB_MODE bits (1: no MFMA,
-// 2: no stage loads, 4: no epilogue stores); the library builds mode 0.
-#ifndef DW_LAB_MODE
-#define DW_LAB_MODE 0
-#endif
-
 namespace dcnr {
 namespace {
 
-// DW_TK: the tile's k width (lab: 128 halves the split count, so the fp32
-// slab, at 1.5x the L2->LDS operand bytes and 0.625 instead of 0.375
-// fragment reads per MFMA)
-#ifndef DW_TK
-#define DW_TK 256
-#endif
-constexpr int TNW = 256, TKW = DW_TK, BKW = 32, NTW = 512, NSTAGE = 4;
+// (256 x 128 tiles -- half the split count and so half the fp32 slab, at
+// 1.5x the L2->LDS operand bytes and 0.625 instead of 0.375 fragment reads
+// per MFMA -- measured +0.5 % per step, profiles/lab/r03at_dw_tiles_ab.txt)
+constexpr int TNW = 256, TKW = 256, BKW = 32, NTW = 512, NSTAGE = 4;
 constexpr int ROWB = TNW * 2;                 // bytes per A row in LDS (256 bf16)
 constexpr int ROWBB = TKW * 2;                // bytes per B row in LDS
 constexpr int OPB = BKW * ROWB;               // A bytes per stage (16 KiB)
@@ -48,8 +39,7 @@ constexpr int STAGEB = OPB + OPBB;            // A + B per stage
 constexpr int LDS_DW = NSTAGE * STAGEB;       // ring of 4 stages
 constexpr int WKC = TKW / 4;                  // k columns per wave (4 waves across k)
 constexpr int NJ = WKC / 16;                  // 16-column MFMA blocks per wave in k
-constexpr int DMAW = 2 + (TKW == 256 ? 2 : 1);   // DMA instructions per wave per stage
-static_assert(TKW == 256 || TKW == 128, "DW_TK");
+constexpr int DMAW = 4;                       // DMA instructions per wave per stage
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -76,19 +66,9 @@ __device__ __forceinline__ void stage_load(u32x4 ar, u32x4 br, int64_t lda, int6
     const bool okr = b < kend;
     const int offa = (okr && na < N) ? (int)((b * lda + na) * 2) : OOR;
     const uint32_t dsta = lds_addr(lds_stage) + (wave * 2 + i) * 1024;
-    if constexpr (!(DW_LAB_MODE & 2)) dma16(ar, offa, dsta);
-    if constexpr (TKW == 256) {
-      const int offb = (okr && ka < K) ? (int)((b * ldb + ka) * 2) : OOR;
-      if constexpr (!(DW_LAB_MODE & 2)) dma16(br, offb, dsta + OPB);
-    }
-  }
-  if constexpr (TKW == 128) {   // 256-B rows: one instruction fills 4 rows, one per wave
-    const int row = wave * 4 + (lane >> 4), q = lane & 15;
-    const int chunk = ((q >> 1) ^ (row & 7)) * 2 + (q & 1);
-    const int64_t b = kb + row;
-    const int ka = c0 + chunk * 8;
-    const int offb = (b < kend && ka < K) ? (int)((b * ldb + ka) * 2) : OOR;
-    if constexpr (!(DW_LAB_MODE & 2)) dma16(br, offb, lds_addr(lds_stage) + OPB + wave * 1024);
+    dma16(ar, offa, dsta);
+    const int offb = (okr && ka < K) ? (int)((b * ldb + ka) * 2) : OOR;
+    dma16(br, offb, dsta + OPB);
   }
 }
 
@@ -156,10 +136,7 @@ __global__ __launch_bounds__(NTW, 1) void gemm_dw_kernel(DwArgs g) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < NJ; ++j)
-        if constexpr (!(DW_LAB_MODE & 1))
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
-        else
-          acc[i][j][0] += (float)af[i][0] * (float)bf[j][1];
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
   }
 
   // epilogue: acc[i][j][r] = dW[n0 + wn*128 + i*16 + (lane>>4)*4 + r][c0 + wk*64 + j*16 + (lane&15)],
@@ -175,8 +152,7 @@ __global__ __launch_bounds__(NTW, 1) void gemm_dw_kernel(DwArgs g) {
       const int k = c0 + wk * WKC + j * 16 + (lane & 15);
       const int n = n0 + wn * 128 + i * 16 + (lane >> 4) * 4;   // N % 8 == 0: all 4 or none
       const bool ok = n < g.N && k < g.K;
-      if (!(DW_LAB_MODE & 4) || acc[i][j][0] == 1234.5f)
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), cr,
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), cr,
                                                ok ? (k * g.ldc + n) * 4 : OOR, 0, 0);
     }
 }
@@ -188,12 +164,11 @@ bool gemm_dw_supported(int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t B
          Btot * lda * 2 < (int64_t(1) << 31) && Btot * ldb * 2 < (int64_t(1) << 31);
 }
 
-#ifndef DW_WG_TARGET
-#define DW_WG_TARGET 256   // workgroups per launch (lab override)
-#endif
-int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot, int wg_target) {
+// splits: 256 workgroups per launch, one per CU (32 / 40 / 48 splits per
+// 512 x 512 call measured slower, profiles/lab/r03z_dw_splits_ab.txt)
+int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot) {
   const int64_t tiles = cdiv(N, TNW) * cdiv(K, TKW);
-  int64_t s = std::max<int64_t>(8, ((wg_target > 0 ? wg_target : DW_WG_TARGET) / tiles) / 8 * 8);
+  int64_t s = std::max<int64_t>(8, (256 / tiles) / 8 * 8);
   while (s > 8 && cdiv(Btot, s) < 2 * BKW) s -= 8;   // at least two stages per split
   return (int)s;
 }

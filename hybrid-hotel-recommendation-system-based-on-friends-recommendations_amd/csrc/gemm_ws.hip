@@ -31,80 +31,37 @@
 
 #include <type_traits>
 
-#ifndef WS_LAB_MODE
-#define WS_LAB_MODE 0   // tools/ws_lab.hip: 1 no C stores, 2 no X DMAs, 4 no MFMAs, 8 no epilogue,
-                        // 16 no fragment reads in the K loop
-#endif
-#ifndef WS_PREFETCH_PIN
-#define WS_PREFETCH_PIN 1
-#endif
-// lab overrides (tools/ws_lab.sh EXTRA=...): tile rows, ring depth, static
-// priority of waves 4-7
-#ifndef WS_TM_OVR
-#define WS_TM_OVR 0
-#endif
-#ifndef WS_NB_OVR
-#define WS_NB_OVR 0
-#endif
-#ifndef WS_PRIO
-#define WS_PRIO 0
-#endif
-// waves 4-7 run each tile's epilogue after the tile's barrier, at the head
-// of the next tile (MI355X_MICROARCH.md "Two waves per SIMD" item 9): the two
-// waves of a SIMD then alternate MFMA and epilogue phases
-// fragment prefetch distance of the MFMA loop, in K steps
-#ifndef WS_PFD
-#define WS_PFD 1
-#endif
-#ifndef WS_STAGGER
-#define WS_STAGGER 0
-#endif
-// software-pipelined epilogue (epilogues without operand loads): each tile's
-// epilogue runs one row block at a time inside the NEXT tile's K loop, in the
-// MFMA shadow; two accumulator sets, 32-row tiles (the register budget)
-#ifndef WS_PIPE
-#define WS_PIPE 0
-#endif
-#ifndef WS_PIPE_MIX
-#define WS_PIPE_MIX 0   // lab: let the scheduler mix the pending epilogue into the MFMA steps
-#endif
-
 namespace dcnr {
 namespace {
 
 // Per-epilogue tile rows and operand-load placement (measured with
-// tools/ws_lab.hip, M = 131072, K = N = 512): 64-row tiles where registers
-// allow; the epilogues with operands use 32-row tiles and issue every
-// operand load before the MFMAs ("early": RESID 90.5 vs 96.4 us one row block
-// ahead, DROP_BN 104.7 vs 111.9 us at 64 rows); eval BN_RELU at 32 rows
-// (71.5 vs 75.4-77.2 us at 64).
-#ifndef WS_SPLIT
-#define WS_SPLIT 0   // lab: two 4-wave workgroups per CU on 128-column slices
-#endif
-constexpr int WS_WAVES = WS_SPLIT ? 4 : 8, WS_NT = 64 * WS_WAVES, WS_WC = 32, WS_TN = WS_WAVES * WS_WC;
-constexpr int WS_WG_PER_CU = WS_SPLIT ? 2 : 1;
-template <int EPI> constexpr bool ws_pipe() {
-  return WS_PIPE && (EPI == NT_EPI_BIAS || EPI == NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS || EPI == NT_EPI_BN_RELU);
-}
+// tools/ws_lab.hip in rounds 2-3, M = 131072, K = N = 512): 64-row tiles where
+// registers allow; the epilogues with operands use 32-row tiles and issue
+// every operand load before the MFMAs ("early": RESID 90.5 vs 96.4 us one row
+// block ahead, DROP_BN 104.7 vs 111.9 us at 64 rows); eval BN_RELU at 32 rows
+// (71.5 vs 75.4-77.2 us at 64).  Rejected variants (stagger, software-pipelined
+// epilogue, two 4-wave workgroups per CU, static priority, deeper fragment
+// prefetch, in-launch BN reduction) and their numbers: DESIGN.md section 8.
+constexpr int WS_WAVES = 8, WS_NT = 64 * WS_WAVES, WS_WC = 32, WS_TN = WS_WAVES * WS_WC;
+constexpr int WS_PFD = 1;   // fragment prefetch distance of the MFMA loop, in K steps
 template <int KTP, int EPI> constexpr int ws_tm() {
-  return ws_pipe<EPI>() || WS_SPLIT ? 32
-         : WS_TM_OVR && KTP == 16 ? WS_TM_OVR : (EPI <= NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS ? 64 : 32);
+  return EPI <= NT_EPI_F32 || EPI == NT_EPI_BIAS_STATS ? 64 : 32;
 }
 template <int EPI> constexpr bool ws_ops_early() {
   return EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN || EPI == NT_EPI_BN_RESID_RELU ||
          EPI == NT_EPI_BN_RESID_RELU_HEAD;
 }
 // X-tile buffers in the LDS ring: one tile in flight while one is consumed.
-template <int KTP, int EPI> constexpr int ws_nb() { return WS_NB_OVR && KTP == 16 ? WS_NB_OVR : 2; }
+constexpr int WS_NB = 2;
 
-template <int KTP, int TM, int NB = 2> struct WsCfg {
+template <int KTP, int TM, int NB = WS_NB> struct WsCfg {
   static constexpr int P = KTP * 64;                      // LDS bytes per X row
   static constexpr int CPR = KTP * 4;                     // 16-B chunks per row
   static constexpr int TILE = TM * P;                     // bytes per X buffer
   static constexpr int RPD = 1024 / P;                    // rows per DMA wave-instruction
   static constexpr int DPW = TM / RPD / WS_WAVES;         // DMAs per wave per tile
   static constexpr int RB = TM / 16;                      // 16-row blocks per tile
-  static constexpr size_t LDS_BYTES = NB * (size_t)TILE + 4 * WS_TN * 4 + 16;  // + hand-off flag
+  static constexpr size_t LDS_BYTES = NB * (size_t)TILE + 4 * WS_TN * 4;
   static_assert(TM % (RPD * WS_WAVES) == 0 && TM % 16 == 0, "tile rows");
   static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
@@ -150,71 +107,14 @@ __device__ __forceinline__ void issue_tile(u32x4 xr, int64_t ldx, int K, uint32_
     const int r = (wave * C::DPW + d) * C::RPD + lane / C::CPR;
     const int c = (lane % C::CPR) ^ (r & 15);
     const int off = c * 8 < K ? (int)(((int64_t)r * ldx + c * 8) * 2) : OOR;
-    if constexpr (!(WS_LAB_MODE & 2)) dma16(xr, off, dst + (wave * C::DPW + d) * 1024);
+    dma16(xr, off, dst + (wave * C::DPW + d) * 1024);
   }
-}
-
-// In-launch BN reduction (stats epilogues with a.fuse_red): the last
-// workgroup of each column slice to store its partial row sums the slice's
-// partial rows in reduce_small_kernel's fixed order (8 row groups of 32 rows,
-// each summed in fp64 from 0, the groups added in order: the same bits as the
-// separate reduce launch) and hands the column sums to red_finalize -- one
-// launch less per BatchNorm layer.  Thread (c, k): column n0 + c, sum k.
-__device__ __forceinline__ void ws_reduce_tail(const NtArgs& a, int slice, int n0, char* lds) {
-  int* flag = reinterpret_cast<int*>(lds);
-  if (!last_arriver(&a.rf.counter[CNT_WS_BASE + slice], a.groups, flag)) return;
-  const int tid = threadIdx.x, c = tid % WS_TN, k = tid / WS_TN;
-  const int n = n0 + c;
-  const __amdgpu_buffer_rsrc_t pr = buf_rsrc(a.part, (int64_t)a.groups * 2 * a.N * 4);
-  // every row's load in flight at once (one memory round trip: the tail of
-  // the launch), summed in reduce_small's order
-  constexpr int U = 32, NG = 8;
-  double tot = 0.0;
-  if (a.groups <= 4 * U) {
-    float v[4 * U];
-#pragma unroll
-    for (int u = 0; u < 4 * U; ++u) {
-      const bool ok = n < a.N && u < a.groups;
-      v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, ok ? ((u * 2 + k) * a.N + n) * 4 : OOR, 0, 0));
-    }
-#pragma unroll
-    for (int g = 0; g < NG; ++g) {
-      double gs = 0.0;
-      if (g < 4) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) gs += (double)v[g * U + u];
-      }
-      tot += gs;
-    }
-  } else {
-#pragma unroll 1
-    for (int g = 0; g < NG; ++g) {
-      float v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int row = g * U + u;
-        const bool ok = n < a.N && row < a.groups;
-        v[u] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, ok ? ((row * 2 + k) * a.N + n) * 4 : OOR, 0, 0));
-      }
-      double gs = 0.0;
-#pragma unroll
-      for (int u = 0; u < U; ++u) gs += (double)v[u];
-      tot += gs;
-    }
-  }
-  double* red = reinterpret_cast<double*>(lds + 64);
-  red[tid] = tot;
-  __syncthreads();
-  if (k != 0 || n >= a.N) return;
-  const bool has_k = a.rf.shiftf != nullptr;
-  const double K = has_k ? (double)a.rf.shiftf[n] : 0.0;
-  red_finalize(a.rf, n, a.N, a.Nr, tot, red[WS_TN + c], 0.0, has_k, K);
 }
 
 template <int KTP, int EPI>
-__global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs a) {
+__global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   constexpr int WS_TM = ws_tm<KTP, EPI>();
-  constexpr int NB = ws_nb<KTP, EPI>();
+  constexpr int NB = WS_NB;
   using C = WsCfg<KTP, WS_TM, NB>;
   constexpr int WS_RB = C::RB;
   constexpr bool STATS = EPI >= NT_EPI_BIAS_STATS && EPI <= NT_EPI_DROP_BN;
@@ -458,132 +358,22 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
         }
         const u32x4 sv = {o[0][0], o[0][1], o[1][0], o[1][1]};
         const int off = (mok && nst < a.N) ? (int)((m * a.ldc + nst) * 2) : OOR;
-        if constexpr (!(WS_LAB_MODE & 1))
-          __builtin_amdgcn_raw_buffer_store_b128(sv, cr, off, 0, 0);
-        else if (ac[rb][0][0] == 12345.f)
-          __builtin_amdgcn_raw_buffer_store_b128(sv, cr, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(sv, cr, off, 0, 0);
       }
     }
   };
   // ---- epilogue of the whole tile at row m0
   auto epilogue = [&](const int64_t m0, f32x4 (&ac)[WS_RB][2]) {
-    if constexpr (WS_LAB_MODE & 8) {   // lab: no epilogue (keep acc alive)
-      float t = 0.f;
 #pragma unroll
-      for (int rb = 0; rb < WS_RB; ++rb) t += ac[rb][0][0] + ac[rb][1][3];
-      if (t == 12345.f) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(t), cr, 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int rb = 0; rb < WS_RB; ++rb) epi_rb(m0, rb, ac);
-    }
+    for (int rb = 0; rb < WS_RB; ++rb) epi_rb(m0, rb, ac);
   };
 
-  if constexpr (ws_pipe<EPI>()) {
-    static_assert(NB == 2, "pipelined epilogue: two X buffers");
-    f32x4 acc2[WS_RB][2];
-    // the K loop of the tile in X buffer bi into ac; row block rb of the
-    // pending tile (pm0 >= 0, accumulators pa) is finished after K step
-    // ((rb + 1) KTP) / RB - 1, beside this tile's MFMAs
-    auto kloop = [&](auto pend_c, f32x4 (&ac)[WS_RB][2], const int bi, const int64_t pm0,
-                     f32x4 (&pa)[WS_RB][2]) {
-      constexpr bool PEND = decltype(pend_c)::value;   // (compile-time: one basic block per K step)
-      const char* xb = lds + bi * C::TILE + rowoff;
-#pragma unroll
-      for (int rb = 0; rb < WS_RB; ++rb)
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb) ac[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      auto xrd = [&](int kt, int rb) {
-        return *reinterpret_cast<const bf16x8*>(xb + rb * 16 * C::P + (kt >> 2) * 256 + coff[kt & 3]);
-      };
-      constexpr int NXB = WS_PFD + 1;
-      bf16x8 xf[NXB][WS_RB];
-#pragma unroll
-      for (int p = 0; p < WS_PFD; ++p)
-#pragma unroll
-        for (int rb = 0; rb < WS_RB; ++rb) xf[p][rb] = xrd(p, rb);
-#pragma unroll
-      for (int kt = 0; kt < KTP; ++kt) {
-        const int cur = kt % NXB;
-        const bool rd = kt + WS_PFD < KTP;
-        if (rd) {
-#pragma unroll
-          for (int rb = 0; rb < WS_RB; ++rb) xf[(kt + WS_PFD) % NXB][rb] = xrd(kt + WS_PFD, rb);
-        }
-#pragma unroll
-        for (int rb = 0; rb < WS_RB; ++rb)
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb)
-            ac[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][kt], xf[cur][rb], ac[rb][cb], 0, 0, 0);
-        bool piece = false;
-        if constexpr (PEND) {
-#pragma unroll
-          for (int rb = 0; rb < WS_RB; ++rb)
-            if (kt == ((rb + 1) * KTP) / WS_RB - 1) {
-              epi_rb(pm0, rb, pa);
-              piece = true;
-            }
-        }
-#if WS_PREFETCH_PIN
-        if (rd && !(WS_PIPE_MIX && piece)) {
-#pragma unroll
-          for (int rb = 0; rb < WS_RB; ++rb) {
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);   // DS read
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);   // MFMA
-          }
-        }
-        if (!(WS_PIPE_MIX && (piece || (PEND && kt + 1 < KTP && kt % (KTP / WS_RB) != KTP / WS_RB - 1))))
-          __builtin_amdgcn_sched_barrier(0);
-#endif
-      }
-    };
-    constexpr int NSTORE = (EPI == NT_EPI_F32 ? 2 : 1) * WS_RB;
-    // one tile: next tile's DMA, K loop (+ the pending epilogue), then the
-    // tile's X buffer is free and the next one landed: the stores issued
-    // after that DMA are exactly the pending epilogue's
-    auto step = [&](auto pend_c, f32x4 (&ac)[WS_RB][2], f32x4 (&pa)[WS_RB][2], int64_t& mt, int& bi,
-                    int64_t& pm0) {
-      const int64_t mn = mt + groups;
-      if (mn < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + (bi ^ 1) * C::TILE, wave, lane);
-      kloop(pend_c, ac, bi, pm0, pa);
-      const bool stored = decltype(pend_c)::value;
-      pm0 = mt * WS_TM;
-      if (stored && mn < a.mtiles)
-        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NSTORE) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      bi ^= 1;
-      mt = mn;
-    };
-    int64_t mt = group, pm0 = -1;
-    int bi = 0;
-    bool last2 = false;   // the pending tile's accumulators are acc2
-    using Yes = std::integral_constant<bool, true>;
-    using No = std::integral_constant<bool, false>;
-    if (mt < a.mtiles) step(No{}, acc, acc2, mt, bi, pm0);   // the first tile: nothing pending
-    while (mt < a.mtiles) {
-      step(Yes{}, acc2, acc, mt, bi, pm0);
-      last2 = true;
-      if (mt >= a.mtiles) break;
-      step(Yes{}, acc, acc2, mt, bi, pm0);
-      last2 = false;
-    }
-    if (pm0 >= 0) {
-      if (last2) epilogue(pm0, acc2);
-      else epilogue(pm0, acc);
-    }
-  } else {
-  if constexpr (WS_PRIO) {
-    if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-  }
-  const bool late = WS_STAGGER && wave >= 4;   // wave-uniform
-  int64_t pm0 = -1;                            // late waves: the tile whose epilogue is pending
   int buf = 0;
   for (int64_t mt = group; mt < a.mtiles; mt += groups, buf = buf + 1 == NB ? 0 : buf + 1) {
     const int64_t mn = mt + (int64_t)(NB - 1) * groups;
     const int nbuf = buf + NB - 1 >= NB ? buf - 1 : buf + NB - 1;   // (buf + NB - 1) % NB
     if (mn < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + nbuf * C::TILE, wave, lane);
     const int64_t m0 = mt * WS_TM;
-    if (late && pm0 >= 0) epilogue(pm0, acc);   // the previous tile's, beside the partners' MFMAs
     if constexpr (WS_OPS_EARLY) {
 #pragma unroll
       for (int rb = 0; rb < WS_RB; ++rb) load_ops(m0, rb, rb);
@@ -610,7 +400,7 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
 #pragma unroll
     for (int kt = 0; kt < KTP; ++kt) {
       const int cur = kt % NXB;
-      const bool rd = kt + WS_PFD < KTP && !(WS_LAB_MODE & 16);
+      const bool rd = kt + WS_PFD < KTP;
       if (rd) {
 #pragma unroll
         for (int rb = 0; rb < WS_RB; ++rb) xf[(kt + WS_PFD) % NXB][rb] = xrd(kt + WS_PFD, rb);
@@ -619,11 +409,7 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
       for (int rb = 0; rb < WS_RB; ++rb)
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
-          if constexpr (!(WS_LAB_MODE & 4))
-            acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][kt], xf[cur][rb], acc[rb][cb], 0, 0, 0);
-          else
-            acc[rb][cb][0] += (float)xf[cur][rb][cb] + (float)wf[cb][kt][0];
-#if WS_PREFETCH_PIN
+          acc[rb][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[cb][kt], xf[cur][rb], acc[rb][cb], 0, 0, 0);
       // keep step kt+PFD's fragment reads in step kt (PFD full steps of MFMAs
       // between a read and its use), spread between the MFMAs
       if (rd) {
@@ -634,11 +420,9 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
         }
       }
       __builtin_amdgcn_sched_barrier(0);
-#endif
     }
 
-    if (late) pm0 = m0;
-    else epilogue(m0, acc);
+    epilogue(m0, acc);
     // next tile's X landed and every wave is done reading this buffer.  Younger
     // than the next tile's DMAs: the stores of the last NB-1 tiles and the
     // DMAs of the NB-2 tiles after it -- when all of those were issued (near
@@ -649,8 +433,6 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
       asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(NWAIT) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-  }
-  if (late && pm0 >= 0) epilogue(pm0, acc);
   }
   if constexpr (STATS) {
     // 16-lane butterfly: lane (q, m) ends with k = bit2(m), cb = bit3(m),
@@ -669,14 +451,13 @@ __global__ __launch_bounds__(WS_NT, WS_SPLIT ? 2 : 1) void gemm_ws_kernel(NtArgs
     const int k = (lane >> 2) & 1, cb = (lane >> 3) & 1, r = 2 * (lane & 1) + ((lane >> 1) & 1);
     const int n = nw + cb * 16 + q * 4 + r;
     if (n < a.N) a.part[((int64_t)group * 2 + k) * a.N + n] = x[0];
-    if (a.fuse_red) ws_reduce_tail(a, slice, n0, lds);
   }
 }
 
 template <int KTP, int EPI>
 dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   constexpr int WS_TM = ws_tm<KTP, EPI>();
-  using C = WsCfg<KTP, WS_TM, ws_nb<KTP, EPI>()>;
+  using C = WsCfg<KTP, WS_TM>;
   TRY_ST(set_max_dyn_lds((const void*)gemm_ws_kernel<KTP, EPI>, C::LDS_BYTES));
   a.nslices = (int)cdiv(a.N, WS_TN);
   // 32-bit buffer offsets: launch in M-chunks of < 2^29 bytes per operand
@@ -684,7 +465,6 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
                                            a.T ? a.ldt : 0});
   const int64_t mchunk = std::max<int64_t>(WS_TM, ((int64_t(1) << 29) / (maxld * 2)) / WS_TM * WS_TM);
   if (a.M > mchunk) {
-    a.fuse_red = 0;   // partial rows of several launches: reduced by the caller
     int total = 0;
     for (int64_t m0 = 0; m0 < a.M; m0 += mchunk) {
       NtArgs b = a;
@@ -706,14 +486,11 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   }
   a.mtiles = cdiv(a.M, WS_TM);
   const int unit = 8 * a.nslices;
-  int grid = std::max(unit, (256 * WS_WG_PER_CU / unit) * unit);
+  int grid = std::max(unit, (256 / unit) * unit);
   const int64_t need = a.mtiles * a.nslices;
   if (need < grid) grid = (int)(cdiv(need, unit) * unit);
   a.groups = grid / a.nslices;
   if (nparts) *nparts = a.groups;
-  if (a.fuse_red && !(WS_NT == 2 * WS_TN && a.groups <= 256 && a.nslices <= CNT_SLOTS - CNT_WS_BASE))
-    a.fuse_red = 0;
-  if (a.fuse_red && nparts) *nparts = -1;
   hipLaunchKernelGGL((gemm_ws_kernel<KTP, EPI>), dim3(grid), dim3(WS_NT), C::LDS_BYTES, s, a);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;

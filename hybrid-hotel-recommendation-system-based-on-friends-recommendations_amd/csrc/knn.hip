@@ -170,9 +170,7 @@ constexpr int K2_NT = 256, K2_WPB = K2_NT / 64, K2_QT = 32, K2_CAP = 64, K2_KMAX
 // (tools/ab_knn.sh, 1M x 64, k = 11), the VALU scan is faster up to Q = 8
 // (Q=4: 73 vs 104 us, Q=8: 97 vs 116 us), the MFMA scan from Q = 16
 // (138 vs 153 us; Q=32: 189 vs 265 us)
-#ifndef MFMA_MIN_Q
-#define MFMA_MIN_Q 16
-#endif
+constexpr int MFMA_MIN_Q = 16;
 
 __device__ __forceinline__ void wave_sort64(float& d, int& i, int lane) {
 #pragma unroll
@@ -458,10 +456,7 @@ __global__ __launch_bounds__(K2_NT) void scan3_kernel(const float* __restrict__ 
 // distance <= the k-th best of any subset, so rows above the bound are never
 // appended: the wave lists then see a handful of rows instead of refilling
 // and re-sorting while their own thresholds converge.
-#ifndef KNN_TH_S
-#define KNN_TH_S 512
-#endif
-constexpr int TH_S = KNN_TH_S;   // sample rows: the bound sits near quantile k / TH_S
+constexpr int TH_S = 512;   // sample rows: the bound sits near quantile k / TH_S
 constexpr float TH_MARGIN = 1e-5f;
 
 // Block qq: normalises query qq (sklearn normalize(): zero norm -> unchanged;
@@ -565,7 +560,7 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 }
 
 // ---------------------------------------------------------------- scan v4
-// Every table and query count (Q >= V4_MIN_Q; d = 32 or 64): bf16-MFMA coarse scoring of
+// Every table and query count (d = 32 or 64): bf16-MFMA coarse scoring of
 // every (row, query) pair + exact fp32 re-scoring of the rows it admits.
 //
 // The coarse cosine is sum_i bf16(x_i * inv_r) * bf16(q_i / |q|), fp32
@@ -585,38 +580,19 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 // V4_SCAP rows) raises a flag and the exact scan v2 + merge, launched behind
 // it and gated on the flag, recomputes the batch.
 constexpr float V4_EPS = 0.004f;
-#ifndef V4_S_OVR
-#define V4_S_OVR 32768
-#endif
-constexpr int V4_S = V4_S_OVR;   // exact sample rows for the admission bound
-#ifndef V4_TH_S
-#define V4_TH_S 512              // rows of the first bound (kth_bound_kernel) on the v4 path
-#endif
-#ifndef V4_WPS
-#define V4_WPS 3                 // min waves per SIMD of scan4 for NQB > 4
-#endif
-#ifndef V4_SNQ
-#define V4_SNQ 16                // query blocks per launch row of the sample pass (Q=256: 31 vs 43 us at 2)
-#endif
+constexpr int V4_S = 32768;     // exact sample rows for the admission bound (larger first
+                                // bound samples measured slower: DESIGN.md section 4)
+constexpr int V4_WPS = 3;       // min waves per SIMD of scan4 for NQB > 4
+constexpr int V4_SNQ = 16;      // query blocks per launch row of the sample pass (Q=256: 31 vs 43 us at 2)
 constexpr int V4_CAP = 4096;     // admitted rows per query
 constexpr int V4_SCAP = 256;     // rows at or under the selected k-th bin
 constexpr int V4_QC = 256;       // queries per block (LDS: V4_QC x d bf16)
-#ifndef V4_RPB_OVR
-#define V4_RPB_OVR 0
-#endif
 // table rows per block: few query blocks -> long blocks (the per-block
 // prologue and epilogue amortised; measured 69 vs 78 us at Q = 32), many ->
 // short ones (a wave's list fill grows with rows x queries)
-constexpr int v4_rpb(int nqb) { return V4_RPB_OVR ? V4_RPB_OVR : nqb <= 4 ? 2048 : 512; }
-#ifndef V4_MIN_N
-#define V4_MIN_N 0   // lab: the smallest table scan v4 serves
-#endif
-#ifndef V4_Q1_N
-#define V4_Q1_N 800000   // a single query takes scan v2 below this many rows
-#endif
-#ifndef V4_MIN_Q
-#define V4_MIN_Q 1   // from Q = 1: 60-66 us for Q <= 8 against 65-98 on scan v2
-#endif
+constexpr int v4_rpb(int nqb) { return nqb <= 4 ? 2048 : 512; }
+constexpr int64_t V4_Q1_N = 800000;   // a single query takes scan v2 below this many rows
+                                      // (from Q = 2: 60-66 us for Q <= 8 against 65-98 on scan v2)
 
 // k-th smallest of n distances (>= 0) held in LDS, by a 2-pass radix select
 // over their bits (exponent + 7 mantissa bits): returns the upper edge of the
@@ -711,13 +687,7 @@ __device__ __forceinline__ void v4_load_rows(const float* __restrict__ tab, int6
 // (block, query), and scatters.
 constexpr int V4_LIST = 2048;    // admitted (query, row) pairs per block
 constexpr int V4_WL = V4_LIST / 4;   // ... per wave
-#ifndef V4_PF
-#define V4_PF 4                  // packed row tiles in flight per wave
-#endif
-#ifndef V4_LAB                   // lab ablations (tools/knn_lab.sh), 0 in the library:
-#define V4_LAB 0                 // 1 no admission checks, 2 B fragments not re-read
-#endif                           // from LDS, 4 no epilogue distances, 8 only the
-                                 // per-block any-ballot (no per-row checks)
+constexpr int V4_PF = 4;        // packed row tiles in flight per wave
 
 // (NQB > 4: at least 3 waves per SIMD -- left alone the compiler unrolled
 // its way to 284 registers and one wave per SIMD, 1.7x slower)
@@ -771,7 +741,6 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(first + 64 * u, x[u], iv[u]);
   int wc = 0;   // this wave's list fill (wave-uniform)
-  float labsink = 0.f;
   // lane (c = r16, g) of B fragment (b, ks): query 16 b + c's k-chunk
   // [32 ks + 8 g, +8)
   bf16x8 bq[BL ? 1 : NQB][KS];
@@ -846,7 +815,7 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
         bf16x8 cb[KS];
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) cb[ks] = BL ? nb[ks] : bq[BL ? 0 : b][ks];
-        if constexpr (BL && !(V4_LAB & 2)) {
+        if constexpr (BL) {
           if (b + 1 < NQB) {
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) nb[ks] = bqs[((b + 1) * KS + ks) * 64 + lane];
@@ -857,11 +826,6 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
         for (int ks = 0; ks < KS; ++ks)
           acc[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], cb[ks], acc[b], 0, 0, 0);
       }
-      if constexpr ((V4_LAB & 1) != 0) {
-#pragma unroll
-        for (int b = 0; b < NQB; ++b) labsink += acc[b][0] + acc[b][3];
-        continue;
-      }
       const bool full = base + 16 <= r1;   // (wave-uniform) no row of the tile past r1
       const int rb = (int)base + 4 * g;
 #pragma unroll
@@ -869,7 +833,6 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
         // lane (c = r16, g): rows rb + i, query 16 b + c
         const float mx = fmaxf(fmaxf(acc[b][0], acc[b][1]), fmaxf(acc[b][2], acc[b][3]));
         if (!__ballot(mx >= th[b])) continue;
-        if constexpr ((V4_LAB & 8) != 0) { ++wc; continue; }
         // one block adds at most 256 entries: room is checked once here (a
         // full list reads as overflowed, and the batch takes the exact path)
         if (wc > V4_WL - 256) { wc = V4_WL + 1; continue; }
@@ -889,9 +852,6 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
         }
       }
     }
-  }
-  if constexpr ((V4_LAB & 1) != 0) {
-    if (labsink == 12345.f) *flag = 2;
   }
   if (lane == 0) wcnt[w] = wc;
   __syncthreads();
@@ -922,7 +882,7 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
   constexpr int DV = KS * 8;
   const float4* tab4 = reinterpret_cast<const float4*>(tab);
   const float4* qn4 = reinterpret_cast<const float4*>(qn);
-  for (int e = threadIdx.x; e < ((V4_LAB & 4) ? 0 : n); e += 256) {
+  for (int e = threadIdx.x; e < n; e += 256) {
     const int sl = slot(e);
     const int qe = lq[sl], re = lr[sl];
     const float4* rp = tab4 + (int64_t)re * DV;
@@ -1310,7 +1270,7 @@ bool use_v4(int64_t N, int64_t Q, int d, int k) {
   // v2, whose one pass beats v4's fixed chain (29 vs 50 us at 20000 rows, 65
   // vs 61 at 1M); v4's exact distances use v2's arithmetic, so the choice
   // never changes an answer.
-  return use_v2(d, k) && Q >= V4_MIN_Q && d % 32 == 0 && N >= V4_MIN_N && (Q > 1 || N >= V4_Q1_N);
+  return use_v2(d, k) && Q >= 1 && d % 32 == 0 && (Q > 1 || N >= V4_Q1_N);
 }
 
 // v4 scratch after the v2 layout (cands | qn [Q][d] | thr0 [Q]): bf16
@@ -1386,15 +1346,7 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       rows = (int*)x;
       dists = (float*)(rows + Q * V4_CAP);
     }
-    if (v4 && V4_TH_S != TH_S) {   // v4's pass-1 bound from a larger first sample
-      if (d == 32)
-        hipLaunchKernelGGL((kth_bound_kernel<8, V4_TH_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, q, qn,
-                           k, thr0, qb, qcnt, gate);
-      else
-        hipLaunchKernelGGL((kth_bound_kernel<16, V4_TH_S>), dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, q,
-                           qn, k, thr0, qb, qcnt, gate);
-      DCNR_LAUNCH_CHECK();
-    } else {   // (v4: also its bf16 queries, zeroed list counts and gate)
+    {   // (v4: also its bf16 queries, zeroed list counts and gate)
       switch (d / 4) {
 #define CASEK(n)                                                                           \
   case n:                                                                                  \

@@ -31,6 +31,7 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
 # dcnr_grad_ready_fn(ctx, group, stream); groups below
 GRAD_READY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p)
 GRADS_DENSE, GRADS_EMBEDDING = 0, 1
+TOUCHED_MAX_WORLD = 64   # DCNR_TOUCHED_MAX_WORLD: ranks dcnr_emb_touched_rows counts owners for
 
 
 class ModelDesc(ctypes.Structure):

@@ -400,35 +400,44 @@ class DCN_RecSys(nn.Module):
         return (x0, cross) if return_x0 else cross
 
     # ----------------------------------------------------------- flat storage
-    def flatten_(self, pad_to: int = 64):
+    def flatten_(self, pad_to: int = 64, table_align: int = 64):
         """Move every parameter into one contiguous fp32 buffer (views keep the
         state_dict API) and give each a ``.grad`` view into one flat gradient
         buffer: lets the fused optimizer and the DP exchange run as single
         launches.  Two segments, each padded to a multiple of ``pad_to`` (the
         optimizer shards split them evenly): the embedding tables
         [0, flat_emb_end) and the dense parameters after them -- the two
-        gradient groups dcnr_backward completes one after the other.
+        gradient groups dcnr_backward completes one after the other.  Every
+        tensor starts on a 64-element boundary; the user and item tables are
+        padded to a multiple of ``table_align`` (a multiple of 64: the sparse
+        exchange needs their rows on multiples of emb_dim).  Records each
+        tensor's element offset in ``flat_offsets``.
         Returns (flat_params, flat_grads)."""
+        if table_align % 64:
+            raise ValueError("table_align must be a multiple of 64")
         params = self.param_tensors()
         dev = params[0].device
         n_emb = 2 + len(self._dims['cat_dims'])   # the tables lead named_parameters()
-        sizes = [((p.numel() + 63) // 64) * 64 for p in params]
-        rnd = lambda x: ((x + pad_to - 1) // pad_to) * pad_to   # noqa: E731
-        emb_end = rnd(sum(sizes[:n_emb]))   # the dense segment starts on a shard boundary
-        total = emb_end + rnd(sum(sizes[n_emb:]))
+        up = lambda x, u: ((x + u - 1) // u) * u   # noqa: E731
+        sizes = [up(p.numel(), table_align if k < 2 else 64) for k, p in enumerate(params)]
+        emb_end = up(sum(sizes[:n_emb]), pad_to)   # the dense segment starts on a shard boundary
+        total = emb_end + up(sum(sizes[n_emb:]), pad_to)
         flat = torch.zeros(total, dtype=torch.float32, device=dev)
         gflat = torch.zeros(total, dtype=torch.float32, device=dev)
         off = 0
+        offs = []
         for k, (p, sz) in enumerate(zip(params, sizes)):
             if k == n_emb:
                 off = emb_end
             n = p.numel()
+            offs.append(off)
             flat[off:off + n].copy_(p.detach().reshape(-1))
             p.data = flat[off:off + n].view_as(p)
             p.grad = gflat[off:off + n].view_as(p)
             off += sz
         self._flat = (flat, gflat)
         self.flat_emb_end = emb_end
+        self.flat_offsets = offs
         return flat, gflat
 
 

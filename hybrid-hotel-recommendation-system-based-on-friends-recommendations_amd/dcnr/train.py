@@ -33,6 +33,7 @@ reference's dense gradients (every embedding row's moments decay every step).
 from __future__ import annotations
 
 import ctypes
+import math
 from typing import Optional
 
 import torch
@@ -58,22 +59,29 @@ class FusedTrainer:
             raise ValueError("exchange must be 'dense' or 'sparse'")
         self.exchange = exchange
         if exchange == "sparse":
+            if shard_optimizer is False:
+                raise ValueError("exchange='sparse' reduce-scatters into optimizer shards: "
+                                 "it needs shard_optimizer=True (or None)")
+            if self.world > _lib.TOUCHED_MAX_WORLD:
+                raise ValueError(f"exchange='sparse' supports at most {_lib.TOUCHED_MAX_WORLD} "
+                                 f"ranks (world {self.world})")
             shard_optimizer = True
         self.shard = (self.world > 1) if shard_optimizer is None else bool(shard_optimizer)
-        self.flat, self.gflat = model.flatten_(pad_to=64 * self.world)
+        # the sparse exchange's layout: the user and item tables at flat
+        # offsets 0 and nu (rows of emb_dim elements), the categorical tables
+        # after them (dense all-reduce); rows must not straddle a shard, so
+        # both tables and the shards are padded to multiples of lcm(64, emb_dim)
+        d = model._dims['emb_dim']
+        unit = 64 * d // math.gcd(64, d) if exchange == "sparse" else 64
+        self.flat, self.gflat = model.flatten_(pad_to=unit * self.world, table_align=unit)
         self.E = model.flat_emb_end                      # embedding segment [0, E)
         N = self.flat.numel()
         self.Es = self.E // self.world if self.shard else self.E   # this rank's embedding moments
-        # the sparse exchange's layout: the user and item tables at flat
-        # offsets 0 and nu (rows of emb_dim elements), the categorical tables
-        # after them (dense all-reduce); rows must not straddle a shard
-        d = model._dims['emb_dim']
-        pad = lambda x: ((x + 63) // 64) * 64   # noqa: E731 (flatten_'s per-tensor padding)
-        nu = pad(model._dims['n_users'] * d)
-        self._sparse_layout = dict(width=d, tables=(0, 1), elem_off=(0, nu),
-                                   dense_lo=nu + pad(model._dims['n_items'] * d), dense_hi=self.E)
-        self._sparse_ok = self.shard and not (self.Es % d or nu % d)
-        if exchange == "sparse" and not self._sparse_ok:
+        offs = model.flat_offsets
+        self._sparse_layout = dict(width=d, tables=(0, 1), elem_off=(offs[0], offs[1]),
+                                   dense_lo=offs[2], dense_hi=self.E)
+        self._sparse_ok = self.shard and not (self.Es % d or offs[1] % d)
+        if exchange == "sparse" and not self._sparse_ok:   # (cannot happen with the padding above)
             raise ValueError("exchange='sparse' needs table rows aligned to the optimizer "
                              f"shards (emb_dim {d}, shard {self.Es} elements)")
         self._B = 0
@@ -115,8 +123,15 @@ class FusedTrainer:
         try:
             run_backward(model, user, item, cat, num, dz, self._ws, self._grads, seed,
                          accumulate=False, grad_ready=self._grad_ready_cb)
-        except RuntimeError as e:
-            self._dense_work = None
+        except RuntimeError:
+            # the hook may have started the dense all-reduce before the
+            # failure: let it finish before anyone writes gflat again
+            work, self._dense_work = self._dense_work, None
+            if work is not None:
+                try:
+                    work.wait()
+                except Exception:   # noqa: BLE001 -- the original error is what matters
+                    pass
             if self._hook_error is not None:
                 err, self._hook_error = self._hook_error, None
                 raise RuntimeError("gradient exchange hook failed") from err

@@ -221,8 +221,10 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
  * 1 = item, 2.. = categorical) writes the flat element offsets
  * elem_off[i] + row * width of its distinct rows, ascending, to
  * out_offsets[i*B ..] and their number to table_counts[i]; owner_counts[r]
- * (r < world) counts the offsets in [r*shard_elems, (r+1)*shard_elems).
+ * (r < world <= DCNR_TOUCHED_MAX_WORLD) counts the offsets in
+ * [r*shard_elems, (r+1)*shard_elems).
  * Stream-ordered; outputs are device memory. */
+#define DCNR_TOUCHED_MAX_WORLD 64
 dcnr_status dcnr_emb_touched_rows(const dcnr_model_desc* desc, const void* ws, size_t ws_bytes,
                                   int64_t B, int32_t n_tables, const int32_t* tables,
                                   const int64_t* elem_off, int64_t shard_elems, int32_t world,

@@ -39,13 +39,20 @@ CFG = dict(n_users=3000, n_items=700, cat_dims={"a": 50, "b": 1000, "c": 7}, n_n
            params=dict(emb_dim=16, hidden_dim=128, n_cross_layers=2, n_res_blocks=2,
                        dropout=0.0))
 B = 2048
+# BASELINE configs[3] per rank: the bench model (1M x 32 users, 100k x 32
+# items, 12 x 1000 x 32 categorical, 8 dense, 3 cross, 4 x 512 deep) at the
+# bench's 131072 samples per rank -- two ranks on one GPU (3.8 GB of
+# workspace each), so the global batch is 262144
+BENCH = dict(n_users=1_000_000, n_items=100_000, cat_dims={f"c{i}": 1000 for i in range(12)}, n_num=8,
+             params=dict(emb_dim=32, hidden_dim=512, n_cross_layers=3, n_res_blocks=4, dropout=0.0))
+CONFIGS = {"toy": (CFG, B), "bench": (BENCH, 2 * 131072)}
 
 
-def _model(dev, precision="fp32", dropout=0.0):
+def _model(dev, precision="fp32", dropout=0.0, cfg=CFG):
     import dcnr
     torch.manual_seed(5)
-    params = dict(CFG["params"], dropout=dropout)
-    m = dcnr.DCN_RecSys(CFG["n_users"], CFG["n_items"], CFG["cat_dims"], CFG["n_num"],
+    params = dict(cfg["params"], dropout=dropout)
+    m = dcnr.DCN_RecSys(cfg["n_users"], cfg["n_items"], cfg["cat_dims"], cfg["n_num"],
                         params, precision=precision)
     gc.perturb_state(m, 6)
     return m.to(dev)
@@ -58,8 +65,8 @@ def _cos_rel(a, b):
     return cos, rel
 
 
-def _batch(dev):
-    u, i, c, n, y = gc.make_inputs(CFG, B, 123)
+def _batch(dev, cfg=CFG, nb=B, seed=123):
+    u, i, c, n, y = gc.make_inputs(cfg, nb, seed)
     return [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in (u, i, c, n, y)]
 
 
@@ -173,7 +180,7 @@ def test_dp_world2_syncbn_equals_single_process(dev, shard, precision):
         mp.spawn(_worker, args=(2, _free_port(), path, shard, precision), nprocs=2, join=True)
 
 
-def _worker_hook(rank, world, port, shard):
+def _worker_hook(rank, world, port, shard, cfg_name="toy", sync_bn=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -181,13 +188,14 @@ def _worker_hook(rank, world, port, shard):
         import dcnr
         from dcnr.model import dropout_seed, run_backward, run_forward
         from dcnr.ops import bce_with_logits
+        cfg, nb = CONFIGS[cfg_name]
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
-        m = _model(dev, "bf16", dropout=0.6)
-        tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, sync_bn=True,
+        m = _model(dev, "bf16", dropout=0.6, cfg=cfg)
+        tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, sync_bn=sync_bn,
                                shard_optimizer=shard)
-        lo, hi = rank * B // world, (rank + 1) * B // world
-        u, i, c, n, y = [t[lo:hi] for t in _batch(dev)]
+        lo, hi = rank * nb // world, (rank + 1) * nb // world
+        u, i, c, n, y = [t[lo:hi] for t in _batch(dev, cfg, nb)]
         gen = torch.cuda.default_generators[0]
         off0 = gen.get_offset()
         flat0 = tr.flat.clone()
@@ -219,6 +227,8 @@ def _worker_hook(rank, world, port, shard):
         emb_ref = g[rank * Es:(rank + 1) * Es] if shard else g[:E]
         assert torch.equal(emb_hook, emb_ref), "embedding segment differs"
         assert dense_hook.abs().sum().item() > 0
+        if cfg_name == "bench":   # the shard boundary of the 142 MB table segment
+            assert E % (64 * world) == 0 and E >= sum(p.numel() for p in m.param_tensors()[:14])
     finally:
         dist.destroy_process_group()
 
@@ -231,23 +241,34 @@ def test_dp_bf16_hook_ordering(dev, shard):
     mp.spawn(_worker_hook, args=(2, _free_port(), shard), nprocs=2, join=True)
 
 
-def _worker_sparse(rank, world, port):
+@pytest.mark.parametrize("shard", [False, True])
+def test_dp_bf16_hook_ordering_bench_model(dev, shard):
+    """The same pin at BASELINE configs[3]'s per-rank workload: the bench
+    model (1M-row user table, 4 x 512 deep, bf16, dropout 0.6) at 131072
+    samples per rank, local BN as the bench runs it: the 142 MB embedding
+    segment's shards, the side-stream weight-gradient pipe at 4 blocks of
+    512 and the hook firing before the dx0 GEMM (train.py:219-226)."""
+    mp.spawn(_worker_hook, args=(2, _free_port(), shard, "bench", False), nprocs=2, join=True)
+
+
+def _worker_sparse(rank, world, port, cfg_name="toy", sync_bn=True):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import dcnr
+        cfg, nb = CONFIGS[cfg_name]
         dev = torch.device("cuda:0")
         torch.cuda.set_device(dev)
-        lo, hi = rank * B // world, (rank + 1) * B // world
+        lo, hi = rank * nb // world, (rank + 1) * nb // world
         flats = []
         for exchange in ("dense", "sparse"):
-            m = _model(dev, "bf16", dropout=0.6)
-            tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, sync_bn=True, exchange=exchange)
+            m = _model(dev, "bf16", dropout=0.6, cfg=cfg)
+            tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, sync_bn=sync_bn, exchange=exchange)
             gen = torch.cuda.default_generators[0]
             gen.set_offset(0)                      # the same dropout seeds in both runs
             for step in range(2):
-                batch = [t[lo:hi] for t in _batch(dev)]
+                batch = [t[lo:hi] for t in _batch(dev, cfg, nb, 123 + step)]
                 tr.step(*batch)
                 if exchange == "sparse" and step == 0:
                     # the touched rows of this rank's batch, from the backward's sort
@@ -265,6 +286,8 @@ def _worker_sparse(rank, world, port):
             torch.cuda.synchronize()
             flats.append(tr.flat.clone())
             assert tr.exchange != "sparse" or tr.last_exchange["rows_sent"] > 0
+            del tr, m
+            torch.cuda.empty_cache()
         # world 2: the owner's rank-order sum (0 + g_0) + g_1 is the dense
         # reduce-scatter's g_0 + g_1: every parameter bit-identical
         assert torch.equal(flats[0], flats[1])
@@ -278,3 +301,12 @@ def test_dp_sparse_exchange_equals_dense(dev):
     all-reduced) gives exactly the dense reduce-scatter step: bf16, dropout
     0.6, SyncBN, two steps, two ranks on one GPU (train.py:156-158, 225)."""
     mp.spawn(_worker_sparse, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def test_dp_sparse_exchange_equals_dense_bench_model(dev):
+    """The sparse exchange at BASELINE configs[3]'s per-rank workload: the
+    1M-row user and 100k-row item tables' touched rows (~123k + 73k per
+    rank) equal torch.unique of the batch, and two steps give every
+    parameter bit-identical to the dense reduce-scatter's (train.py:156-158,
+    225)."""
+    mp.spawn(_worker_sparse, args=(2, _free_port(), "bench", False), nprocs=2, join=True)

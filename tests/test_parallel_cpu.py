@@ -30,9 +30,9 @@ def _init(rank, world, port):
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
 
-def _run(fn, world=2):
+def _run(fn, world=2, *extra):
     port = _free_port()
-    mp.spawn(fn, args=(world, port), nprocs=world, join=True)
+    mp.spawn(fn, args=(world, port) + tuple(extra), nprocs=world, join=True)
 
 
 def test_shard_range():
@@ -239,7 +239,7 @@ def test_sharded_optimizer_exchange_matches_allreduce_adam(world):
     _run(_exchange_worker, world)
 
 
-def _sparse_worker(rank, world, port):
+def _sparse_worker(rank, world, port, d):
     """Owner-bucketed sparse exchange of the user table (FusedTrainer
     exchange="sparse"): each rank's user-table gradient is nonzero only on
     its batch's ids (what dcnr_backward writes); after the exchange every rank
@@ -248,7 +248,7 @@ def _sparse_worker(rank, world, port):
     _init(rank, world, port)
     try:
         import dcnr
-        n_users, d = 257, 8
+        n_users = 257
         ids = [torch.randint(0, n_users, (40,), generator=torch.Generator().manual_seed(50 + r))
                for r in range(world)]
         ids[world - 1][:5] = n_users - 1          # the last owner's tail row
@@ -315,6 +315,17 @@ def _sparse_worker(rank, world, port):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sparse_user_table_exchange(world):
-    _run(_sparse_worker, world)
+@pytest.mark.parametrize("world,d", [(2, 8), (3, 8), (2, 24), (3, 48)])
+def test_sparse_user_table_exchange(world, d):
+    """emb_dim 24 / 48 (in the reference's Optuna space, train.py:180): the
+    tables and the shards are padded to lcm(64, emb_dim) so rows never
+    straddle a shard."""
+    _run(_sparse_worker, world, d)
+
+
+def test_sparse_exchange_argument_checks():
+    import dcnr
+    m = dcnr.DCN_RecSys(50, 40, {"a": 10}, 3, dict(emb_dim=8, hidden_dim=16, n_cross_layers=1,
+                                                     n_res_blocks=1, dropout=0.0))
+    with pytest.raises(ValueError):
+        dcnr.FusedTrainer(m, exchange="sparse", shard_optimizer=False)
