@@ -297,6 +297,7 @@ struct Layout {
   void* a1s[MAX_RES];       // train: each block's dropout(relu(BN1(t1))), saved for dW2
   float* zc; float* zdeep;
   float* headp;             // eval: [head parts][B] deep-head partial dots (null: row_dot)
+  char* twp;                // eval, fused tower: the packed weight slices (null: layer by layer)
   BnBufs bn[2 * MAX_RES];
   float* part; double* sums; float* coef;
   double* red2; int* red_cnt;   // reduce_fused scratch (counters zeroed by pack_all)
@@ -335,6 +336,13 @@ bool head_rebuild(const Dims& d, bool train) {
 }
 bool eval_fuse_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && gemm_ws_supported(d.Hp, d.Hp); }
 
+// The eval forward's deep tower as one persistent launch (tower.hip): bf16,
+// the shapes it covers (input width <= 512, hidden <= 512), not when the
+// stage tests ask for every intermediate.
+bool tower_ok(const Dims& d, bool train, bool keep) {
+  return !train && !keep && d.prec == DCNR_PREC_BF16 && tower_supported(d.Dp, d.H, d.R);
+}
+
 Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = false) {
   Layout L;
   memset(&L, 0, sizeof(L));
@@ -343,6 +351,13 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
   const size_t es = d.es;
   const size_t act = (size_t)B * d.Hp * es;
   L.err = (int*)b.take(256);
+  if (tower_ok(d, train, keep)) {   // x0, zc, the packed slices: nothing of the tower in HBM
+    L.x0 = b.take((size_t)B * d.Dp * es);
+    L.zc = (float*)b.take(B * 4);
+    L.twp = (char*)b.take((size_t)tower_ws_bytes(d.H, d.R));
+    L.total = b.off + 256;
+    return L;
+  }
   L.W0p = b.take((size_t)d.Hp * d.Dp * es);
   L.W0t = train ? b.take((size_t)d.Dp * d.Hp * es) : nullptr;
   L.b0p = (float*)b.take(d.Hp * 4);
@@ -993,6 +1008,30 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
   // backward's id sort needs the ids alone, so it follows there, under this
   // forward (joined before returning, so the caller's id tensors are free to
   // go once the forward's work is done).
+  if (L.twp) {
+    // eval: gather + cross (x0 bf16, zc) -> the fused deep tower + head
+    TowerPack tp;
+    memset(&tp, 0, sizeof(tp));
+    tp.W0 = P.W0; tp.D = d.D; tp.b0 = P.b0;
+    for (int j = 0; j < d.R; ++j) {
+      const auto& Bk = P.blk[j];
+      tp.w1[j] = Bk.w1; tp.b1[j] = Bk.b1; tp.g1[j] = Bk.g1; tp.be1[j] = Bk.be1; tp.rm1[j] = Bk.rm1; tp.rv1[j] = Bk.rv1;
+      tp.w2[j] = Bk.w2; tp.b2[j] = Bk.b2; tp.g2[j] = Bk.g2; tp.be2[j] = Bk.be2; tp.rm2[j] = Bk.rm2; tp.rv2[j] = Bk.rv2;
+    }
+    tp.wf = P.wf; tp.H = d.H; tp.R = d.R; tp.out = L.twp; tp.err = check ? L.err : nullptr;
+    TRYP(DCNR_K_PACK, tower_pack(tp, s));
+    const GcOut o{nullptr, L.x0, L.zc, 0, d.Dp, nullptr};
+    TRYB(DCNR_K_GATHER_CROSS, (double)B * (gather_row_b(d, desc->n_num) + (double)d.Dp * d.es + 4.0),
+         gather_cross_out(g, cp, user_ids, item_ids, cat_features, num_features, B, o, 1, L.err, check, s));
+    TowerArgs ta;
+    memset(&ta, 0, sizeof(ta));
+    ta.x0 = (const bf16*)L.x0; ta.ldx = d.Dp; ta.M = B; ta.Dp = d.Dp; ta.H = d.H; ta.R = d.R;
+    ta.wp = L.twp; ta.zc = L.zc; ta.bias = P.bf; ta.logits = logits;
+    // algorithmic bytes: the x0 rows + zc in, the logits out (the packed
+    // weights are L2-resident: every CU streams the same 4.7 MB)
+    TRYB(DCNR_K_TOWER, (double)B * (d.Dp * d.es + 8.0), eval_tower(ta, s));
+    return DCNR_OK;
+  }
   SideJoin sj;
   if (train) {
     TRY(sj.fork(s));

@@ -10,11 +10,6 @@
 
 namespace dcnr {
 
-// When set, the next row-pass launch (run_rowcol) records this event as its
-// completion (hipExtLaunchKernel's stop event: no separate marker packet on
-// the stream) and clears it.  The backward's side-stream weight-gradient
-// pipe uses it to depend on the BN apply pass that wrote its dY.
-
 typedef __bf16 bf16;
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
@@ -392,6 +387,34 @@ struct PackDesc {            // W [rows][cols] f32 -> dst T [rows_p][ld] (+ opti
   int rows_p, cols_p;
   int f32;                   // 1: dst is f32 whatever the batch's precision (no transpose)
 };
+// ------------------------------------------------ fused eval deep tower
+// (tower.hip) the eval forward's initial Linear + R ResBlocks + deep head dot
+// in one persistent launch; activations stay in registers.
+constexpr int MAX_RES_TW = 8;
+struct TowerPack {                     // fp32 reference-layout parameters -> packed bf16 slices
+  const float* W0; int D; const float* b0;
+  const float* w1[MAX_RES_TW]; const float* b1[MAX_RES_TW]; const float* g1[MAX_RES_TW];
+  const float* be1[MAX_RES_TW]; const float* rm1[MAX_RES_TW]; const float* rv1[MAX_RES_TW];
+  const float* w2[MAX_RES_TW]; const float* b2[MAX_RES_TW]; const float* g2[MAX_RES_TW];
+  const float* be2[MAX_RES_TW]; const float* rm2[MAX_RES_TW]; const float* rv2[MAX_RES_TW];
+  const float* wf;                     // deep head weights (final_linear.weight[:H])
+  int H, HT, R;                        // HT = H rounded up to 64 (set by tower_pack)
+  char* out;                           // tower_ws_bytes(H, R)
+  int* err;                            // optional: 64 ints zeroed (the gather's error word)
+};
+struct TowerArgs {
+  const bf16* x0; int64_t ldx; int64_t M;   // x0 [M][ldx] bf16, columns >= Dp ignored
+  int Dp, H, R;
+  const char* wp; int64_t wp_bytes;          // tower_pack's output
+  const float* zc; const float* bias;        // cross half of the head [M], final_linear.bias
+  float* logits;
+  int ntiles;                                // (set by eval_tower)
+};
+bool tower_supported(int Dp, int H, int R);
+int64_t tower_ws_bytes(int H, int R);
+dcnr_status tower_pack(const TowerPack& p, hipStream_t s);
+dcnr_status eval_tower(const TowerArgs& a, hipStream_t s);
+
 constexpr int MAX_PACK = 20;
 struct PackBatch { PackDesc d[MAX_PACK]; int n; };
 dcnr_status pack_weights(int precision, const PackBatch& pb, hipStream_t s);

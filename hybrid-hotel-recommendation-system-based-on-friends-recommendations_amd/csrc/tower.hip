@@ -1,0 +1,372 @@
+// Fused eval deep tower (gfx950): the eval forward's whole deep tower --
+// initial Linear, R ResBlocks (Linear -> BN(running stats) -> ReLU ->
+// Linear -> BN -> + residual -> ReLU) and the deep head dot -- in ONE
+// persistent launch whose activations never leave the chip (scoring,
+// main.py:319-322; eval semantics of train.py:102-122, 161-170: dropout is
+// the identity and BatchNorm uses its running statistics, so no batch-global
+// barrier separates the layers).
+//
+//  * one 256-thread workgroup per CU, one wave per SIMD (up to 512 VGPRs);
+//    each wave owns 32 samples (a tile is 128 samples per CU) and keeps their
+//    activations in REGISTERS as MFMA B-operand fragments -- features on k,
+//    samples on the 16 columns: h and a1 of 32 samples x 512 features are
+//    256 VGPRs;
+//  * the weights are the A operand.  They are streamed from L2 (4.7 MB of
+//    bf16 shared by every CU) through a 3-slot LDS ring by LDS-DMA, one slice
+//    per step (32 output features x K, pre-packed in fragment order so each
+//    wave's ds_read_b128 is one contiguous 1 KB), read by all four waves;
+//  * v_mfma_f32_16x16x32_bf16: lane (g = lane/16, c = lane%16) accumulates
+//    features 16b + 4g + r of sample c -- exactly what the next layer's B
+//    fragment needs at elements 4(b&1) + r of k-step b/2, so a layer's output
+//    is its successor's operand with no data movement; tower_pack permutes
+//    the hidden weights' input columns to match (element j of lane group g in
+//    k-step kt is feature 32kt + 16(j>>2) + 4g + (j&3));
+//  * epilogue per slice: BN affine (Linear bias folded into the shift),
+//    ReLU, the residual (read from the output registers themselves: a
+//    ResBlock's second Linear overwrites h in place), bf16 pack;
+//  * head: dot of the bf16 h_R with wf, 4-lane reduce, + zc (the cross half
+//    of the head, written by the gather/cross kernel) + bias.
+//
+// HBM traffic per scored pair: the bf16 x0 row (Dp x 2 B) + zc + the logit;
+// MFMA work 2 x (Dp_pad x HT + 2R x HT^2) FLOP.
+#include "dcnr_internal.h"
+
+namespace dcnr {
+namespace {
+
+constexpr int TW_NT = 256, TW_WAVES = 4, TW_S = 32, TW_TILE = TW_WAVES * TW_S;
+constexpr int TW_KT0 = 16;                    // k-steps of the initial Linear (Dp <= 512, zero padded)
+constexpr int TW_SLOT = 2 * TW_KT0 * 1024 + 256;   // ring slot: 2 output blocks x 16 k-steps + constants
+constexpr int TW_CONST = 2 * TW_KT0 * 1024;   // constants' offset in a slot: sc[32], sh[32]
+constexpr int TW_NSLOT = 3;
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef bf16 bf16x2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f2v{a, b}, bf16x2v));
+}
+__device__ __forceinline__ float lo16(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi16(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+// packed layout: the slices of layer 0 (2R+1 layers, NCH = HT/32 slices
+// each), then the hidden layers', then wf [HT] fp32
+__host__ __device__ inline int64_t tw_slice_bytes(int kt) { return 2048LL * kt + 256; }
+__host__ __device__ inline int64_t tw_slice_off(int l, int ch, int nch, int nkt) {
+  return l == 0 ? ch * tw_slice_bytes(TW_KT0)
+                : nch * tw_slice_bytes(TW_KT0) + ((int64_t)(l - 1) * nch + ch) * tw_slice_bytes(nkt);
+}
+__host__ __device__ inline int64_t tw_packed_bytes(int R, int HT) {
+  const int nch = HT / 32, nkt = HT / 32;
+  return tw_slice_off(2 * R + 1, 0, nch, nkt) + (int64_t)HT * 4;
+}
+
+// --------------------------------------------------------------- pack
+// One thread per 16-B weight group (8 bf16 of one lane's A fragment), then
+// one per (layer, feature) for the constants, then wf.
+__global__ __launch_bounds__(256) void tower_pack_kernel(TowerPack p) {
+  const int HT = p.HT, nch = HT / 32, nkt = HT / 32, H = p.H;
+  const int64_t g0 = (int64_t)nch * 2 * TW_KT0 * 64;   // layer 0 groups
+  const int64_t gl = (int64_t)nch * 2 * nkt * 64;       // per hidden layer
+  const int64_t nw = g0 + 2LL * p.R * gl;
+  const int64_t nc = (int64_t)(2 * p.R + 1) * HT;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0 && p.err) {
+#pragma unroll
+    for (int e = 0; e < 64; ++e) p.err[e] = 0;
+  }
+  if (i < nw) {
+    int l, kt_n;
+    int64_t r;
+    if (i < g0) { l = 0; r = i; kt_n = TW_KT0; }
+    else { l = 1 + (int)((i - g0) / gl); r = (i - g0) % gl; kt_n = nkt; }
+    const int lane = (int)(r % 64);
+    const int kt = (int)((r / 64) % kt_n);
+    const int ob = (int)((r / (64LL * kt_n)) % 2);
+    const int ch = (int)(r / (128LL * kt_n));
+    const int o = 32 * ch + 16 * ob + (lane & 15), g = lane >> 4;
+    const float* W;
+    int K;
+    if (l == 0) { W = p.W0; K = p.D; }
+    else { W = (l & 1) ? p.w1[(l - 1) / 2] : p.w2[(l - 1) / 2]; K = H; }
+    uint32_t w[4];
+#pragma unroll
+    for (int j2 = 0; j2 < 4; ++j2) {
+      float v[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int j = 2 * j2 + e;
+        const int k = l == 0 ? 32 * kt + 8 * g + j : 32 * kt + 16 * (j >> 2) + 4 * g + (j & 3);
+        v[e] = (o < H && k < K) ? W[(int64_t)o * K + k] : 0.f;
+      }
+      w[j2] = pk2(v[0], v[1]);
+    }
+    char* dst = p.out + tw_slice_off(l, ch, nch, nkt) + ((int64_t)ob * kt_n + kt) * 1024 + lane * 16;
+    *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
+    return;
+  }
+  if (i < nw + nc) {
+    const int64_t r = i - nw;
+    const int l = (int)(r / HT), f = (int)(r % HT);
+    float sc = 0.f, sh = 0.f;
+    if (f < H) {
+      if (l == 0) {
+        sc = 1.f;
+        sh = p.b0[f];
+      } else {
+        const int j = (l - 1) / 2;
+        const bool second = (l & 1) == 0;
+        const float* b = second ? p.b2[j] : p.b1[j];
+        const float* gm = second ? p.g2[j] : p.g1[j];
+        const float* be = second ? p.be2[j] : p.be1[j];
+        const float* rm = second ? p.rm2[j] : p.rm1[j];
+        const float* rv = second ? p.rv2[j] : p.rv1[j];
+        // bn_eval_multi_kernel's running-stat affine, the Linear bias folded in
+        const double mean = rm[f], var = rv[f];
+        const float inv = (float)(1.0 / sqrt(var + (double)BN_EPS));
+        sc = gm[f] * inv;
+        sh = fmaf(b[f], sc, be[f] - (float)mean * sc);
+      }
+    }
+    const int kt_n = l == 0 ? TW_KT0 : nkt;
+    float* cst = reinterpret_cast<float*>(p.out + tw_slice_off(l, f / 32, nch, nkt) + 2048LL * kt_n);
+    cst[f % 32] = sc;
+    cst[32 + f % 32] = sh;
+    return;
+  }
+  if (i < nw + nc + HT) {
+    const int f = (int)(i - nw - nc);
+    reinterpret_cast<float*>(p.out + tw_slice_off(2 * p.R + 1, 0, nch, nkt))[f] = f < H ? p.wf[f] : 0.f;
+  }
+}
+
+// ----------------------------------------------------------- one slice
+// MODE 0: initial Linear (acc + b0), 1: BN + ReLU, 2: BN + residual + ReLU
+// (the residual is the output fragment itself).  `sl`: the slice's LDS slot.
+template <int KT, int MODE>
+__device__ __forceinline__ void tw_slice(const char* sl, int g, int lane, const u32x4 (&in)[16][2],
+                                         u32x4& o0, u32x4& o1) {
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) acc[ob][sb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const char* ab = sl + lane * 16;
+  auto rd = [&](int ob, int kt) { return *reinterpret_cast<const bf16x8*>(ab + (ob * KT + kt) * 1024); };
+  bf16x8 af[2][2];
+  af[0][0] = rd(0, 0);
+  af[0][1] = rd(1, 0);
+#pragma unroll
+  for (int kt = 0; kt < KT; ++kt) {
+    if (kt + 1 < KT) {
+      af[(kt + 1) & 1][0] = rd(0, kt + 1);
+      af[(kt + 1) & 1][1] = rd(1, kt + 1);
+    }
+#pragma unroll
+    for (int ob = 0; ob < 2; ++ob)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb)
+        acc[ob][sb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kt & 1][ob], __builtin_bit_cast(bf16x8, in[kt][sb]),
+                                                              acc[ob][sb], 0, 0, 0);
+    if (kt + 1 < KT) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next step's two DS reads
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // this step's MFMAs
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  const float* cst = reinterpret_cast<const float*>(sl + TW_CONST);
+  auto epi = [&](int ob, const f32x4& ac, const float4& sc, const float4& sh, u32x4& w) {
+    float v0 = fmaf(ac[0], sc.x, sh.x);
+    float v1 = fmaf(ac[1], sc.y, sh.y);
+    float v2 = fmaf(ac[2], sc.z, sh.z);
+    float v3 = fmaf(ac[3], sc.w, sh.w);
+    if constexpr (MODE == 2) {
+      const uint32_t r0 = w[2 * ob], r1 = w[2 * ob + 1];
+      v0 += lo16(r0); v1 += hi16(r0); v2 += lo16(r1); v3 += hi16(r1);
+    }
+    if constexpr (MODE >= 1) {
+      v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
+    }
+    w[2 * ob] = pk2(v0, v1);
+    w[2 * ob + 1] = pk2(v2, v3);
+  };
+#pragma unroll
+  for (int ob = 0; ob < 2; ++ob) {
+    const float4 sc = *reinterpret_cast<const float4*>(cst + 16 * ob + 4 * g);
+    const float4 sh = *reinterpret_cast<const float4*>(cst + 32 + 16 * ob + 4 * g);
+    epi(ob, acc[ob][0], sc, sh, o0);
+    epi(ob, acc[ob][1], sc, sh, o1);
+  }
+  // pin the epilogue here: left alone, the compiler sinks it to the next
+  // layer's first use and keeps every slice's accumulators alive till then
+  asm volatile("" : "+v"(o0), "+v"(o1));
+}
+
+template <int NKT>
+__global__ __launch_bounds__(TW_NT, 1) void tower_kernel(TowerArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int NCH = NKT;   // 32-feature slices per layer (HT / 32)
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  float* wf_s = reinterpret_cast<float*>(lds + TW_NSLOT * TW_SLOT);
+  const u32x4 wr = rsrc_words(a.wp, a.wp_bytes);
+  const uint32_t lbase = lds_addr(lds);
+  const int per_tile = NCH * (1 + 2 * a.R);
+  const int my_tiles = a.ntiles > (int)blockIdx.x ? (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  const int total = my_tiles * per_tile;
+  // the slice stream (the same sequence of layers for every tile): step q
+  // consumes slice q in slot q % 3; slice q + 2 is issued at step q
+  auto issue = [&](int q) {
+    if (q >= total) return;
+    const int i = q % per_tile;
+    const int l = i < NCH ? 0 : 1 + (i - NCH) / NCH;
+    const int kt = l == 0 ? TW_KT0 : NKT;
+    const int off = (int)tw_slice_off(l, i < NCH ? i : (i - NCH) % NCH, NCH, NKT);
+    const uint32_t dst = lbase + (q % TW_NSLOT) * TW_SLOT;
+    const int per = kt / 2;   // 1-KB weight pieces per wave
+    for (int d = 0; d < per; ++d) {
+      const int pc = wave * per + d;
+      dma16(wr, off + pc * 1024 + lane * 16, dst + pc * 1024);
+    }
+    if (lane < 4) dma16(wr, off + kt * 2048 + wave * 64 + lane * 16, dst + TW_CONST + wave * 64);
+  };
+  // every wave's DMAs of slice q landed, and every wave is done with slot
+  // (q - 1) % 3, which slice q + 2 then refills (the younger DMAs in flight
+  // at the wait: slice q + 1's, NKT/2 + 1 or more per wave)
+  auto sync = [&](int q) {
+    if (q + 1 < total)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(NKT / 2 + 1) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    issue(q + 2);
+  };
+  for (int f = tid; f < NKT * 32; f += TW_NT)
+    wf_s[f] = reinterpret_cast<const float*>(a.wp + tw_slice_off(2 * a.R + 1, 0, NCH, NKT))[f];
+  issue(0);
+  issue(1);
+
+  const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x0, a.M * a.ldx * 2);
+  u32x4 X[16][2], H[16][2];
+  int q = 0;
+  for (int t = 0; t < my_tiles; ++t) {
+    const int64_t s0 = ((int64_t)blockIdx.x + (int64_t)t * gridDim.x) * TW_TILE + wave * TW_S;
+    // x0 fragments in natural k order: X[kt][sb] = x0[s0 + 16sb + c][32kt + 8g .. +7]
+#pragma unroll
+    for (int kt = 0; kt < TW_KT0; ++kt)
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const int64_t s = s0 + 16 * sb + c;
+        const int k = 32 * kt + 8 * g;
+        X[kt][sb] = __builtin_amdgcn_raw_buffer_load_b128(
+            xr, (s < a.M && k < a.Dp) ? (int)((s * a.ldx + k) * 2) : OOR, 0, 0);
+      }
+    // initial Linear: X -> H
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch, ++q) {
+      sync(q);
+      tw_slice<TW_KT0, 0>(lds + (q % TW_NSLOT) * TW_SLOT, g, lane, X, H[ch][0], H[ch][1]);
+    }
+    for (int j = 0; j < a.R; ++j) {
+      // a1 = relu(BN1(h W1^T + b1)): H -> X
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch, ++q) {
+        sync(q);
+        tw_slice<NKT, 1>(lds + (q % TW_NSLOT) * TW_SLOT, g, lane, H, X[ch][0], X[ch][1]);
+      }
+      // h = relu(BN2(a1 W2^T + b2) + h): X -> H in place
+#pragma unroll
+      for (int ch = 0; ch < NCH; ++ch, ++q) {
+        sync(q);
+        tw_slice<NKT, 2>(lds + (q % TW_NSLOT) * TW_SLOT, g, lane, X, H[ch][0], H[ch][1]);
+      }
+    }
+    // deep head: sum_f bf16(h_R[f]) wf[f], this lane's features, then the
+    // sample's four lanes (g = 0..3): half-wave swap, then row swap
+    float z[2] = {0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < NKT; ++kt) {
+      const float4 wa = *reinterpret_cast<const float4*>(wf_s + 32 * kt + 4 * g);
+      const float4 wb = *reinterpret_cast<const float4*>(wf_s + 32 * kt + 16 + 4 * g);
+#pragma unroll
+      for (int sb = 0; sb < 2; ++sb) {
+        const u32x4 h = H[kt][sb];
+        z[sb] = fmaf(lo16(h[0]), wa.x, z[sb]);
+        z[sb] = fmaf(hi16(h[0]), wa.y, z[sb]);
+        z[sb] = fmaf(lo16(h[1]), wa.z, z[sb]);
+        z[sb] = fmaf(hi16(h[1]), wa.w, z[sb]);
+        z[sb] = fmaf(lo16(h[2]), wb.x, z[sb]);
+        z[sb] = fmaf(hi16(h[2]), wb.y, z[sb]);
+        z[sb] = fmaf(lo16(h[3]), wb.z, z[sb]);
+        z[sb] = fmaf(hi16(h[3]), wb.w, z[sb]);
+      }
+    }
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      const unsigned u = __float_as_uint(z[sb]);
+      auto h2 = __builtin_amdgcn_permlane32_swap(u, u, false, false);
+      const float t2 = __uint_as_float(h2[0]) + __uint_as_float(h2[1]);
+      const unsigned ut = __float_as_uint(t2);
+      auto h4 = __builtin_amdgcn_permlane16_swap(ut, ut, false, false);
+      const float zs = __uint_as_float(h4[0]) + __uint_as_float(h4[1]);
+      const int64_t s = s0 + 16 * sb + c;
+      if (g == 0 && s < a.M) a.logits[s] = zs + a.zc[s] + a.bias[0];
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+}  // namespace
+
+bool tower_supported(int Dp, int H, int R) {
+  return Dp <= 512 && H >= 1 && rup(H, 64) <= 512 && R >= 1 && R <= MAX_RES_TW;
+}
+int64_t tower_ws_bytes(int H, int R) { return tw_packed_bytes(R, (int)rup(H, 64)); }
+
+dcnr_status tower_pack(const TowerPack& p0, hipStream_t s) {
+  TowerPack p = p0;
+  p.HT = (int)rup(p.H, 64);
+  const int nch = p.HT / 32;
+  const int64_t n = (int64_t)nch * 2 * TW_KT0 * 64 + 2LL * p.R * nch * 2 * (p.HT / 32) * 64 +
+                    (int64_t)(2 * p.R + 1) * p.HT + p.HT;
+  hipLaunchKernelGGL(tower_pack_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, p);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status eval_tower(const TowerArgs& a0, hipStream_t s) {
+  TowerArgs a = a0;
+  const int HT = (int)rup(a.H, 64), nkt = HT / 32;
+  if (!tower_supported(a.Dp, a.H, a.R) || a.ldx < a.Dp || a.ldx % 8) {
+    set_error("eval_tower: unsupported Dp=%d H=%d R=%d", a.Dp, a.H, a.R);
+    return DCNR_UNSUPPORTED_SHAPE;
+  }
+  a.wp_bytes = tw_packed_bytes(a.R, HT);
+  const size_t lds = TW_NSLOT * TW_SLOT + (size_t)HT * 4;
+  const void* k = nullptr;
+  switch (nkt) {
+    case 2: k = (const void*)tower_kernel<2>; break;
+    case 4: k = (const void*)tower_kernel<4>; break;
+    case 6: k = (const void*)tower_kernel<6>; break;
+    case 8: k = (const void*)tower_kernel<8>; break;
+    case 10: k = (const void*)tower_kernel<10>; break;
+    case 12: k = (const void*)tower_kernel<12>; break;
+    case 14: k = (const void*)tower_kernel<14>; break;
+    case 16: k = (const void*)tower_kernel<16>; break;
+  }
+  TRY_ST(set_max_dyn_lds(k, lds));
+  // 32-bit buffer offsets into x0: launches of < 2^31 bytes of rows
+  const int64_t chunk = std::max<int64_t>(TW_TILE, ((int64_t(1) << 31) - 1) / (a.ldx * 2) / TW_TILE * TW_TILE);
+  for (int64_t m0 = 0; m0 < a0.M; m0 += chunk) {
+    TowerArgs b = a;
+    b.M = std::min(chunk, a0.M - m0);
+    b.x0 = a.x0 + m0 * a.ldx;
+    b.zc = a.zc + m0;
+    b.logits = a.logits + m0;
+    b.ntiles = (int)cdiv(b.M, TW_TILE);
+    const int grid = (int)std::min<int64_t>(b.ntiles, 256);
+    void* args[] = {&b};
+    DCNR_HIP(hipLaunchKernel(k, dim3(grid), dim3(TW_NT), args, lds, s));
+  }
+  return DCNR_OK;
+}
+
+}  // namespace dcnr

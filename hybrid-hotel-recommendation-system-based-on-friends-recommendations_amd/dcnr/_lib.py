@@ -109,7 +109,8 @@ _SIGS = {
 }
 
 KERNEL_CLASSES = ["gather_cross", "gemm_fwd", "gemm_dx", "gemm_dw", "rowwise", "reduce",
-                  "cross_bwd", "head", "adam", "knn", "pack", "serve", "emb_sort", "emb_sum"]
+                  "cross_bwd", "head", "adam", "knn", "pack", "serve", "emb_sort", "emb_sum",
+                  "tower"]
 
 
 def profile_enable(on):

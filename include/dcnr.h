@@ -370,7 +370,8 @@ typedef enum {
   DCNR_K_SERVE = 11,       /* candidate union, ranking batch, sort, MMR     */
   DCNR_K_EMB_SORT = 12,    /* embedding-backward stable id sort             */
   DCNR_K_EMB_SUM = 13,     /* embedding-backward per-row segmented sums     */
-  DCNR_K_COUNT = 14
+  DCNR_K_TOWER = 14,       /* fused eval deep tower (one persistent launch) */
+  DCNR_K_COUNT = 15
 } dcnr_kernel_class;
 
 /* on = 0: off; 1: every launch timed per class with HIP events on its

@@ -1,0 +1,37 @@
+"""Eval-forward timing probe: the fused tower (default) vs the layer-by-layer
+path (keep_intermediates) on the bench model, several batch sizes."""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests", "golden"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+import golden_common as gc  # noqa: E402
+import dcnr  # noqa: E402
+
+dev = torch.device("cuda:0")
+cfg = dict(n_users=1_000_000, n_items=100_000, cat_dims={f"c{i}": 1000 for i in range(12)}, n_num=8,
+           params=dict(emb_dim=32, hidden_dim=512, n_cross_layers=3, n_res_blocks=4, dropout=0.6))
+torch.manual_seed(42)
+m = dcnr.DCN_RecSys(cfg["n_users"], cfg["n_items"], cfg["cat_dims"], cfg["n_num"], dict(cfg["params"]),
+                    precision="bf16").to(dev).eval()
+for B in [int(x) for x in (sys.argv[1:] or ["200", "4096", "131072"])]:
+    u, i, c, n, _ = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in gc.make_inputs(cfg, B, 1)]
+    for keep in (False, True):
+        m.keep_intermediates = keep
+        with torch.no_grad():
+            for _ in range(5):
+                z = m(u, i, c, n)
+            torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            it = 50
+            a.record()
+            for _ in range(it):
+                z = m(u, i, c, n)
+            b.record()
+            torch.cuda.synchronize()
+        ms = a.elapsed_time(b) / it
+        print(f"B={B} {'layers' if keep else 'tower '} {ms*1e3:8.1f} us/call  {B/ms/1e3:8.2f} M pairs/s", flush=True)
