@@ -53,7 +53,7 @@ def _eval_logits(m, inp, dev, keep):
     with torch.no_grad():
         z = m(t(u), t(i), t(c), t(n))
     torch.cuda.synchronize()
-    return z.double().cpu().numpy()
+    return z.double().cpu().numpy().reshape(-1)
 
 
 def _oracle_check(m, cfg, inp, z, B):

@@ -8,7 +8,8 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tests", "golden"))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..",
+                                "hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd"))
 import golden_common as gc  # noqa: E402
 import dcnr  # noqa: E402
 
