@@ -12,7 +12,7 @@
 //    samples on the 16 columns: h and a1 of 32 samples x 512 features are
 //    256 VGPRs;
 //  * the weights are the A operand.  They are streamed from L2 (4.7 MB of
-//    bf16 shared by every CU) through a 3-slot LDS ring by LDS-DMA, one slice
+//    bf16 shared by every CU) through an LDS ring by LDS-DMA, one slice
 //    per step (32 output features x K, pre-packed in fragment order so each
 //    wave's ds_read_b128 is one contiguous 1 KB), read by all four waves;
 //  * v_mfma_f32_16x16x32_bf16: lane (g = lane/16, c = lane%16) accumulates
@@ -31,6 +31,8 @@
 // MFMA work 2 x (Dp_pad x HT + 2R x HT^2) FLOP.
 #include "dcnr_internal.h"
 
+#include <type_traits>
+
 namespace dcnr {
 namespace {
 
@@ -39,6 +41,23 @@ constexpr int TW_KT0 = 16;                    // k-steps of the initial Linear (
 constexpr int TW_SLOT = 2 * TW_KT0 * 1024 + 256;   // ring slot: 2 output blocks x 16 k-steps + constants
 constexpr int TW_CONST = 2 * TW_KT0 * 1024;   // constants' offset in a slot: sc[32], sh[32]
 constexpr int TW_NSLOT = 3;
+
+// LDS-DMA of 16 B per lane: voff (per lane) + soff (wave-uniform) into
+// lds_dst + 16 * lane.  dma16's form with the uniform part of the offset in
+// an SGPR, so the weight stream costs one VGPR (lane * 16) however many
+// pieces a wave issues.
+__device__ __forceinline__ void dma16s(u32x4 rsrc, int voff, int soff, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds_dst), "s"(soff)
+      : "memory");
+}
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef bf16 bf16x2v __attribute__((ext_vector_type(2)));
@@ -140,16 +159,49 @@ __global__ __launch_bounds__(256) void tower_pack_kernel(TowerPack p) {
 }
 
 // ----------------------------------------------------------- one slice
+// A slice's accumulators and its 32 features' BN constants, kept in
+// registers until its epilogue runs inside the NEXT slice's k-loop (beside
+// that slice's MFMAs: one wave per SIMD has no partner to hide a separate
+// epilogue phase behind).
+struct Pend {
+  f32x4 acc[2][2];   // [output block][sample block]
+  float4 sc[2], sh[2];
+};
+
 // MODE 0: initial Linear (acc + b0), 1: BN + ReLU, 2: BN + residual + ReLU
-// (the residual is the output fragment itself).  `sl`: the slice's LDS slot.
-template <int KT, int MODE>
+// (the residual is the output fragment itself).  Piece p of 8 finishes two
+// features (r = 2(p&1), +1) of output block p>>2 for sample block (p>>1)&1.
+template <int MODE>
+__device__ __forceinline__ void epi_piece(const Pend& pd, int p, u32x4& w0, u32x4& w1) {
+  const int ob = p >> 2, sb = (p >> 1) & 1, hf = p & 1;
+  u32x4& w = sb ? w1 : w0;
+  const f32x4& ac = pd.acc[ob][sb];
+  float v0 = fmaf(ac[2 * hf], hf ? pd.sc[ob].z : pd.sc[ob].x, hf ? pd.sh[ob].z : pd.sh[ob].x);
+  float v1 = fmaf(ac[2 * hf + 1], hf ? pd.sc[ob].w : pd.sc[ob].y, hf ? pd.sh[ob].w : pd.sh[ob].y);
+  if constexpr (MODE == 2) {
+    const uint32_t r = w[2 * ob + hf];
+    v0 += lo16(r);
+    v1 += hi16(r);
+  }
+  if constexpr (MODE >= 1) {
+    v0 = fmaxf(v0, 0.f);
+    v1 = fmaxf(v1, 0.f);
+  }
+  w[2 * ob + hf] = pk2(v0, v1);
+}
+
+// One slice (step): the k-loop of 2 output blocks x 2 sample blocks into
+// `cur`, with the previous slice's epilogue (`pend`, PEND) in its first 8
+// k-steps; then the slice's constants into `cur`.  p0/p1: the previous
+// slice's output fragments.
+template <int KT, int MODE, bool PEND, class Dma>
 __device__ __forceinline__ void tw_slice(const char* sl, int g, int lane, const u32x4 (&in)[16][2],
-                                         u32x4& o0, u32x4& o1) {
-  f32x4 acc[2][2];
+                                         Pend& cur, const Pend& pend, u32x4& p0, u32x4& p1,
+                                         const Dma& dma) {
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
-    for (int sb = 0; sb < 2; ++sb) acc[ob][sb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int sb = 0; sb < 2; ++sb) cur.acc[ob][sb] = f32x4{0.f, 0.f, 0.f, 0.f};
   const char* ab = sl + lane * 16;
   auto rd = [&](int ob, int kt) { return *reinterpret_cast<const bf16x8*>(ab + (ob * KT + kt) * 1024); };
   bf16x8 af[2][2];
@@ -161,44 +213,42 @@ __device__ __forceinline__ void tw_slice(const char* sl, int g, int lane, const 
       af[(kt + 1) & 1][0] = rd(0, kt + 1);
       af[(kt + 1) & 1][1] = rd(1, kt + 1);
     }
+    dma(kt);
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
       for (int sb = 0; sb < 2; ++sb)
-        acc[ob][sb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kt & 1][ob], __builtin_bit_cast(bf16x8, in[kt][sb]),
-                                                              acc[ob][sb], 0, 0, 0);
-    if (kt + 1 < KT) {
-      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next step's two DS reads
-      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);   // this step's MFMAs
+        cur.acc[ob][sb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            af[kt & 1][ob], __builtin_bit_cast(bf16x8, in[kt][sb]), cur.acc[ob][sb], 0, 0, 0);
+    const bool piece = PEND && kt < 8;
+    if (piece) epi_piece<MODE>(pend, kt, p0, p1);
+    if (kt + 1 < KT) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // the next step's DS reads
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);               // an MFMA
+      if (piece) __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);   // ... then epilogue VALU
     }
     __builtin_amdgcn_sched_barrier(0);
   }
+  // (short k-loops: the pieces left over)
+  for (int d = KT; d <= TW_KT0 / 2; ++d) dma(d);
   const float* cst = reinterpret_cast<const float*>(sl + TW_CONST);
-  auto epi = [&](int ob, const f32x4& ac, const float4& sc, const float4& sh, u32x4& w) {
-    float v0 = fmaf(ac[0], sc.x, sh.x);
-    float v1 = fmaf(ac[1], sc.y, sh.y);
-    float v2 = fmaf(ac[2], sc.z, sh.z);
-    float v3 = fmaf(ac[3], sc.w, sh.w);
-    if constexpr (MODE == 2) {
-      const uint32_t r0 = w[2 * ob], r1 = w[2 * ob + 1];
-      v0 += lo16(r0); v1 += hi16(r0); v2 += lo16(r1); v3 += hi16(r1);
-    }
-    if constexpr (MODE >= 1) {
-      v0 = fmaxf(v0, 0.f); v1 = fmaxf(v1, 0.f); v2 = fmaxf(v2, 0.f); v3 = fmaxf(v3, 0.f);
-    }
-    w[2 * ob] = pk2(v0, v1);
-    w[2 * ob + 1] = pk2(v2, v3);
-  };
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {
-    const float4 sc = *reinterpret_cast<const float4*>(cst + 16 * ob + 4 * g);
-    const float4 sh = *reinterpret_cast<const float4*>(cst + 32 + 16 * ob + 4 * g);
-    epi(ob, acc[ob][0], sc, sh, o0);
-    epi(ob, acc[ob][1], sc, sh, o1);
+    cur.sc[ob] = *reinterpret_cast<const float4*>(cst + 16 * ob + 4 * g);
+    cur.sh[ob] = *reinterpret_cast<const float4*>(cst + 32 + 16 * ob + 4 * g);
   }
-  // pin the epilogue here: left alone, the compiler sinks it to the next
-  // layer's first use and keeps every slice's accumulators alive till then
-  asm volatile("" : "+v"(o0), "+v"(o1));
+  // pin the finished epilogue here: left alone, the compiler sinks it to the
+  // next layer's first use and keeps every slice's accumulators alive
+  if constexpr (PEND) asm volatile("" : "+a"(p0), "+a"(p1));
+}
+
+// the whole epilogue of a layer's last slice, right after its k-loop
+template <int MODE>
+__device__ __forceinline__ void tw_finish(const Pend& pd, u32x4& o0, u32x4& o1) {
+#pragma unroll
+  for (int p = 0; p < 8; ++p) epi_piece<MODE>(pd, p, o0, o1);
+  asm volatile("" : "+a"(o0), "+a"(o1));
 }
 
 template <int NKT>
@@ -214,39 +264,67 @@ __global__ __launch_bounds__(TW_NT, 1) void tower_kernel(TowerArgs a) {
   const int my_tiles = a.ntiles > (int)blockIdx.x ? (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
   const int total = my_tiles * per_tile;
   // the slice stream (the same sequence of layers for every tile): step q
-  // consumes slice q in slot q % 3; slice q + 2 is issued at step q
-  auto issue = [&](int q) {
-    if (q >= total) return;
-    const int i = q % per_tile;
-    const int l = i < NCH ? 0 : 1 + (i - NCH) / NCH;
-    const int kt = l == 0 ? TW_KT0 : NKT;
-    const int off = (int)tw_slice_off(l, i < NCH ? i : (i - NCH) % NCH, NCH, NKT);
-    const uint32_t dst = lbase + (q % TW_NSLOT) * TW_SLOT;
-    const int per = kt / 2;   // 1-KB weight pieces per wave
-    for (int d = 0; d < per; ++d) {
-      const int pc = wave * per + d;
-      dma16(wr, off + pc * 1024 + lane * 16, dst + pc * 1024);
+  // consumes slice q in slot q % NSLOT, and issues slice q + NSLOT - 1.  The
+  // issue cursor (layer, slice, byte offset, slot) advances by additions
+  // only: this code is inlined at every step of the unrolled layers.
+  int i_layer = 0, i_ch = 0, i_off = 0, i_slot = 0, i_left = total;
+  // the slice being issued during this step: LDS slot, source offset (an
+  // out-of-range one past the end of the stream: the DMAs then write zeros
+  // into a slot nobody reads again), 1-KB pieces per wave
+  uint32_t i_dst = 0;
+  int i_src = 0, i_pcs = 0;
+  auto issue_begin = [&]() {
+    i_dst = __builtin_amdgcn_readfirstlane(lbase + i_slot * TW_SLOT);
+    i_src = i_left > 0 ? i_off : 0x7f000000;
+    i_pcs = (i_layer == 0 ? TW_KT0 : NKT) / 2;
+    if (i_left > 0) {
+      --i_left;
+      i_off += (i_layer == 0 ? TW_KT0 : NKT) * 2048 + 256;
+      if (++i_ch == NCH) {
+        i_ch = 0;
+        if (++i_layer == 2 * a.R + 1) { i_layer = 0; i_off = 0; }
+      }
     }
-    if (lane < 4) dma16(wr, off + kt * 2048 + wave * 64 + lane * 16, dst + TW_CONST + wave * 64);
+    i_slot = i_slot + 1 == TW_NSLOT ? 0 : i_slot + 1;
+  };
+  // piece d of the slice being issued (d == pieces: its constants), one per
+  // k-step of the consuming slice: each LDS-DMA's issue cost then sits
+  // beside MFMAs instead of in a burst after the barrier
+  auto issue_piece = [&](int d) {
+    const int pcs = NKT == TW_KT0 ? TW_KT0 / 2 : i_pcs;
+    if (d < pcs) {
+      const int pc = wave * pcs + d;
+      dma16s(wr, lane * 16, __builtin_amdgcn_readfirstlane(i_src + pc * 1024), i_dst + pc * 1024);
+    } else if (d == pcs) {
+      if (lane < 4)
+        dma16s(wr, lane * 16, __builtin_amdgcn_readfirstlane(i_src + pcs * 4096 + wave * 64),
+               i_dst + TW_CONST + wave * 64);
+    }
+  };
+  auto issue = [&]() {   // a whole slice at once (the prologue)
+    issue_begin();
+    for (int d = 0; d <= i_pcs; ++d) issue_piece(d);
   };
   // every wave's DMAs of slice q landed, and every wave is done with slot
-  // (q - 1) % 3, which slice q + 2 then refills (the younger DMAs in flight
-  // at the wait: slice q + 1's, NKT/2 + 1 or more per wave)
+  // (q - 1) % NSLOT, which slice q + NSLOT - 1 then refills (the younger
+  // DMAs in flight at the wait: those of the NSLOT - 2 slices after q,
+  // NKT/2 + 1 or more per wave and slice; near the end of the stream fewer)
   auto sync = [&](int q) {
-    if (q + 1 < total)
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(NKT / 2 + 1) : "memory");
+    constexpr int PER = NKT / 2 + 1;
+    if (q + TW_NSLOT - 2 < total)
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"((TW_NSLOT - 2) * PER) : "memory");
     else
       asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    issue(q + 2);
+    issue_begin();
   };
   for (int f = tid; f < NKT * 32; f += TW_NT)
     wf_s[f] = reinterpret_cast<const float*>(a.wp + tw_slice_off(2 * a.R + 1, 0, NCH, NKT))[f];
-  issue(0);
-  issue(1);
+  for (int p = 0; p < TW_NSLOT - 1; ++p) issue();
 
   const __amdgpu_buffer_rsrc_t xr = buf_rsrc(a.x0, a.M * a.ldx * 2);
   u32x4 X[16][2], H[16][2];
-  int q = 0;
+  Pend pa, pb;
+  int q = 0, c_slot = 0;   // step, and the slot it reads
   for (int t = 0; t < my_tiles; ++t) {
     const int64_t s0 = ((int64_t)blockIdx.x + (int64_t)t * gridDim.x) * TW_TILE + wave * TW_S;
     // x0 fragments in natural k order: X[kt][sb] = x0[s0 + 16sb + c][32kt + 8g .. +7]
@@ -259,25 +337,28 @@ __global__ __launch_bounds__(TW_NT, 1) void tower_kernel(TowerArgs a) {
         X[kt][sb] = __builtin_amdgcn_raw_buffer_load_b128(
             xr, (s < a.M && k < a.Dp) ? (int)((s * a.ldx + k) * 2) : OOR, 0, 0);
       }
-    // initial Linear: X -> H
+    // one layer: NCH slices, slice ch's epilogue inside slice ch+1's k-loop,
+    // the last one's right after its own
+    auto layer = [&](auto kt_c, auto mode_c, const u32x4 (&in)[16][2], u32x4 (&out)[16][2]) {
+      constexpr int KT = decltype(kt_c)::value, MODE = decltype(mode_c)::value;
 #pragma unroll
-    for (int ch = 0; ch < NCH; ++ch, ++q) {
-      sync(q);
-      tw_slice<TW_KT0, 0>(lds + (q % TW_NSLOT) * TW_SLOT, g, lane, X, H[ch][0], H[ch][1]);
-    }
+      for (int ch = 0; ch < NCH; ++ch, ++q) {
+        sync(q);
+        const char* sl = lds + c_slot * TW_SLOT;
+        c_slot = c_slot + 1 == TW_NSLOT ? 0 : c_slot + 1;
+        Pend& cur = (ch & 1) ? pb : pa;
+        const Pend& prev = (ch & 1) ? pa : pb;
+        if (ch == 0) tw_slice<KT, MODE, false>(sl, g, lane, in, cur, prev, out[0][0], out[0][1], issue_piece);
+        else tw_slice<KT, MODE, true>(sl, g, lane, in, cur, prev, out[ch - 1][0], out[ch - 1][1], issue_piece);
+      }
+      tw_finish<MODE>((NCH & 1) ? pa : pb, out[NCH - 1][0], out[NCH - 1][1]);
+    };
+    using KT0c = std::integral_constant<int, TW_KT0>;
+    using NKTc = std::integral_constant<int, NKT>;
+    layer(KT0c{}, std::integral_constant<int, 0>{}, X, H);       // initial Linear: X -> H
     for (int j = 0; j < a.R; ++j) {
-      // a1 = relu(BN1(h W1^T + b1)): H -> X
-#pragma unroll
-      for (int ch = 0; ch < NCH; ++ch, ++q) {
-        sync(q);
-        tw_slice<NKT, 1>(lds + (q % TW_NSLOT) * TW_SLOT, g, lane, H, X[ch][0], X[ch][1]);
-      }
-      // h = relu(BN2(a1 W2^T + b2) + h): X -> H in place
-#pragma unroll
-      for (int ch = 0; ch < NCH; ++ch, ++q) {
-        sync(q);
-        tw_slice<NKT, 2>(lds + (q % TW_NSLOT) * TW_SLOT, g, lane, X, H[ch][0], H[ch][1]);
-      }
+      layer(NKTc{}, std::integral_constant<int, 1>{}, H, X);     // a1 = relu(BN1(h W1^T + b1))
+      layer(NKTc{}, std::integral_constant<int, 2>{}, X, H);     // h = relu(BN2(a1 W2^T + b2) + h)
     }
     // deep head: sum_f bf16(h_R[f]) wf[f], this lane's features, then the
     // sample's four lanes (g = 0..3): half-wave swap, then row swap
