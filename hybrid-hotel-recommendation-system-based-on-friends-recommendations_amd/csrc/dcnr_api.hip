@@ -1448,6 +1448,43 @@ dcnr_status dcnr_emb_touched_rows(const dcnr_model_desc* desc, const void* ws, s
                           (hipStream_t)stream);
 }
 
+dcnr_status dcnr_sparse_pack(const float* grad, const int64_t* offsets, int64_t ld,
+                             const int64_t* table_counts, int32_t n_tables, int32_t width,
+                             int64_t* out_offsets, float* out_rows, dcnr_stream_t stream) {
+  if (!grad || !offsets || !table_counts || !out_offsets || !out_rows || ld < 0 || n_tables < 1 ||
+      width < 1) {
+    set_error("dcnr_sparse_pack: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  TRYP(DCNR_K_SERVE, sparse_pack(grad, offsets, ld, table_counts, n_tables, width, out_offsets, out_rows, s));
+  return DCNR_OK;
+}
+
+dcnr_status dcnr_sparse_accumulate(float* shard, int64_t shard_lo, int64_t shard_elems, int32_t width,
+                                   const int64_t* offsets, const float* rows,
+                                   const int64_t* source_counts, int32_t n_sources,
+                                   dcnr_stream_t stream) {
+  if (!shard || shard_lo < 0 || shard_elems < 0 || width < 1 || n_sources < 0 ||
+      (n_sources > 0 && !source_counts)) {
+    set_error("dcnr_sparse_accumulate: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  int64_t n = 0;
+  for (int r = 0; r < n_sources; ++r) {
+    if (source_counts[r] < 0) { set_error("dcnr_sparse_accumulate: negative count"); return DCNR_BAD_ARG; }
+    n += source_counts[r];
+  }
+  if (n > 0 && (!offsets || !rows)) {
+    set_error("dcnr_sparse_accumulate: null rows");
+    return DCNR_BAD_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  TRYP(DCNR_K_SERVE, sparse_accumulate(shard, shard_lo, shard_elems, width, offsets, rows, source_counts,
+                                       n_sources, s));
+  return DCNR_OK;
+}
+
 dcnr_status dcnr_bce_with_logits(const float* logits, const float* labels, int64_t B, float* loss,
                                  float* dlogits, float grad_scale, void* ws, size_t ws_bytes,
                                  dcnr_stream_t stream) {

@@ -501,6 +501,13 @@ struct TouchedArgs {
 };
 dcnr_status emb_touched_rows(const TouchedArgs& a, const EmbSortBufs& sb, int64_t B, int64_t* out,
                              int64_t* table_counts, int64_t* owner_counts, hipStream_t s);
+// the data-parallel sparse exchange's device halves (embed_bwd.hip): pack the
+// touched rows (+ their offsets) into the all_to_all send buffer; add what
+// each source rank sent into the owner's shard, sources in order
+dcnr_status sparse_pack(const float* grad, const int64_t* offs, int64_t ld, const int64_t* tcnt,
+                        int n_tables, int width, int64_t* out_off, float* out_rows, hipStream_t s);
+dcnr_status sparse_accumulate(float* shard, int64_t lo, int64_t elems, int width, const int64_t* offs,
+                              const float* rows, const int64_t* counts, int n_sources, hipStream_t s);
 // grad row r of table t = sum over its samples of dx0_deep[b][off_t:off_t+w_t]
 // + sum_k (sum over its samples of coef[b][k]) V[k][off_t:off_t+w_t]
 dcnr_status emb_segment_sum(const EmbBwdDesc& e, const EmbSortBufs& sb, int64_t B,

@@ -1010,6 +1010,106 @@ dcnr_status emb_touched_rows(const TouchedArgs& a, const EmbSortBufs& sb, int64_
 
 namespace {
 
+// ------------------------------------------------ sparse exchange (DP)
+// Pack: table t's touched rows (offsets offs[t][0 .. tcnt[t]), ascending)
+// go to positions [sum_{u<t} tcnt[u], ...) of the send buffers -- the
+// tables in flat order, so the whole list is ascending and grouped by owner.
+// One thread per 16 B of a row (width % 4 == 0) or per float.
+template <int V>
+__global__ __launch_bounds__(256) void sparse_pack_kernel(const float* __restrict__ grad,
+                                                          const int64_t* __restrict__ offs, int64_t ld,
+                                                          const int64_t* __restrict__ tcnt, int width,
+                                                          int64_t* __restrict__ out_off,
+                                                          float* __restrict__ out_rows) {
+  const int t = blockIdx.y;
+  int64_t base = 0;
+  for (int u = 0; u < t; ++u) base += tcnt[u];
+  const int64_t n = tcnt[t];
+  const int per = width / V;   // threads per row
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * per;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / per;
+    const int c = (int)(e % per) * V;
+    const int64_t o = offs[(int64_t)t * ld + i];
+    if (c == 0) out_off[base + i] = o;
+    if constexpr (V == 4)
+      *reinterpret_cast<float4*>(out_rows + (base + i) * width + c) = *reinterpret_cast<const float4*>(grad + o + c);
+    else
+      out_rows[(base + i) * width + c] = grad[o + c];
+  }
+}
+
+// Accumulate one source's rows (distinct offsets) into the shard [lo, lo +
+// elems): a plain read-add-write, since no two of them share a row; the
+// sources are launched in rank order, so every shard row is summed
+// 0 + g_0 + g_1 + ... whatever the scheduling.  Offsets outside the shard
+// (none, from sparse_pack's owner grouping) are skipped.
+template <int V>
+__global__ __launch_bounds__(256) void sparse_add_kernel(float* __restrict__ shard, int64_t lo, int64_t elems,
+                                                         int width, const int64_t* __restrict__ offs,
+                                                         const float* __restrict__ rows, int64_t n) {
+  const int per = width / V;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n * per;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = e / per;
+    const int c = (int)(e % per) * V;
+    const int64_t r = offs[i] - lo;
+    if (r < 0 || r + width > elems) continue;
+    if constexpr (V == 4) {
+      float4* d = reinterpret_cast<float4*>(shard + r + c);
+      const float4 g = *reinterpret_cast<const float4*>(rows + i * width + c);
+      float4 v = *d;
+      v.x += g.x; v.y += g.y; v.z += g.z; v.w += g.w;
+      *d = v;
+    } else {
+      shard[r + c] += rows[i * width + c];
+    }
+  }
+}
+
+}  // namespace
+
+dcnr_status sparse_pack(const float* grad, const int64_t* offs, int64_t ld, const int64_t* tcnt, int n_tables,
+                        int width, int64_t* out_off, float* out_rows, hipStream_t s) {
+  if (ld <= 0 || n_tables < 1) return DCNR_OK;
+  const bool v4 = width % 4 == 0 && (uintptr_t)grad % 16 == 0 && (uintptr_t)out_rows % 16 == 0;
+  const int per = v4 ? width / 4 : width;
+  const unsigned bx = (unsigned)std::min<int64_t>(cdiv(ld * per, 256), 2048);
+  if (v4)
+    hipLaunchKernelGGL(sparse_pack_kernel<4>, dim3(bx, n_tables), dim3(256), 0, s, grad, offs, ld, tcnt, width,
+                       out_off, out_rows);
+  else
+    hipLaunchKernelGGL(sparse_pack_kernel<1>, dim3(bx, n_tables), dim3(256), 0, s, grad, offs, ld, tcnt, width,
+                       out_off, out_rows);
+  DCNR_LAUNCH_CHECK();
+  return DCNR_OK;
+}
+
+dcnr_status sparse_accumulate(float* shard, int64_t lo, int64_t elems, int width, const int64_t* offs,
+                              const float* rows, const int64_t* counts, int n_sources, hipStream_t s) {
+  DCNR_HIP(hipMemsetAsync(shard, 0, (size_t)elems * 4, s));
+  const bool v4 = width % 4 == 0 && lo % 4 == 0 && (uintptr_t)shard % 16 == 0 && (uintptr_t)rows % 16 == 0;
+  int64_t pos = 0;
+  for (int r = 0; r < n_sources; ++r) {   // rank order: one launch per source
+    const int64_t n = counts[r];
+    if (n > 0) {
+      const int per = v4 ? width / 4 : width;
+      const unsigned bx = (unsigned)std::min<int64_t>(cdiv(n * per, 256), 4096);
+      if (v4)
+        hipLaunchKernelGGL(sparse_add_kernel<4>, dim3(bx), dim3(256), 0, s, shard, lo, elems, width, offs + pos,
+                           rows + pos * width, n);
+      else
+        hipLaunchKernelGGL(sparse_add_kernel<1>, dim3(bx), dim3(256), 0, s, shard, lo, elems, width, offs + pos,
+                           rows + pos * width, n);
+      DCNR_LAUNCH_CHECK();
+    }
+    pos += n;
+  }
+  return DCNR_OK;
+}
+
+namespace {
+
 template <int VEC, int NV>
 void launch_sums(const EmbTabs& et, int nt, int64_t B, const EmbSortBufs& sb, const float* dx0,
                  int ld, const float* coef, int hps, int accumulate, hipStream_t s) {

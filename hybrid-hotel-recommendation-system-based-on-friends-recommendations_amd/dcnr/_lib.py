@@ -75,6 +75,9 @@ _SIGS = {
     "dcnr_emb_touched_rows": (ctypes.c_int, [ctypes.POINTER(ModelDesc), _P, ctypes.c_size_t, _I64,
                                              ctypes.c_int32, _P, _P, _I64, ctypes.c_int32, _P, _P,
                                              _P, _P]),
+    "dcnr_sparse_pack": (ctypes.c_int, [_P, _P, _I64, _P, ctypes.c_int32, ctypes.c_int32, _P, _P, _P]),
+    "dcnr_sparse_accumulate": (ctypes.c_int, [_P, _I64, _I64, ctypes.c_int32, _P, _P, _P,
+                                              ctypes.c_int32, _P]),
     "dcnr_bce_workspace_size": (ctypes.c_size_t, []),
     "dcnr_bce_with_logits": (ctypes.c_int, [_P, _P, _I64, _P, _P, ctypes.c_float, _P,
                                             ctypes.c_size_t, _P]),

@@ -18,15 +18,17 @@ plain data-parallel split of each batch across ranks:
 Default (sync_bn=False) is local BN: every rank normalises with its own
 batch, like torch DDP without SyncBatchNorm.
 
-``sparse_reduce_scatter`` is the owner-bucketed sparse exchange of the big
+``SparseExchange`` is the owner-bucketed sparse exchange of the big
 embedding tables' gradients (SURVEY.md 8e option B), used by
 ``FusedTrainer(exchange="sparse")``: the rows the rank's batch touched
-(``touched_rows``: read from the backward's own stable id sort by
+(``touched_rows``: read from the forward's own stable id sort by
 ``dcnr_emb_touched_rows``, no torch.unique) go to the rank that owns their
 ZeRO-1 shard of the flat parameter buffer (one all_to_all of offsets and
 rows), and each owner sums what it received in source-rank order into its
-gradient shard.  ``sparse_rows_allreduce`` is the earlier host-sized
-variant for one table (kept for the CPU tests of the protocol).
+gradient shard.  Both halves are device kernels (``dcnr_sparse_pack`` /
+``dcnr_sparse_accumulate``); the message sizes are exchanged right after the
+forward and read by the host only after the backward is enqueued, so the
+GPU never waits for the host.
 """
 from __future__ import annotations
 
@@ -98,64 +100,6 @@ def remove_sync_bn(model):
     model._sync_bn_hook = None
 
 
-def sparse_rows_allreduce(grad: torch.Tensor, local_ids: torch.Tensor, group=None) -> dict:
-    """Sum a row-sparse embedding gradient over ranks, in place.
-
-    ``grad`` [n_rows, d] holds this rank's dense gradient, nonzero only in
-    rows listed in ``local_ids`` (the batch's ids for this table).  Rows are
-    owned in contiguous ranges of ceil(n_rows / world).  The exchange:
-      1. every rank sends its touched rows (distinct ids, ascending) to their
-         owners (all_to_all, sizes exchanged first);
-      2. each owner sums what it received in source-rank order (a fixed order:
-         every row is summed 0 + g_0 + g_1 + ..., as a single process would);
-      3. the owners' summed rows are all-gathered (padded to the largest
-         owner list) and written into ``grad``, which is zero elsewhere.
-    Every rank ends with the same ``grad``, bit for bit.  Returns the rows
-    sent / received counts for reporting."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    n, d = grad.shape
-    dev = grad.device
-    per = (n + world - 1) // world
-    uniq = torch.unique(local_ids.reshape(-1))
-    rows = grad.index_select(0, uniq)
-    send = torch.bincount(torch.div(uniq, per, rounding_mode='floor'), minlength=world)
-    recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send, group=group)
-    sc, rc = send.tolist(), recv.tolist()
-    rids = torch.empty(sum(rc), dtype=torch.int64, device=dev)
-    dist.all_to_all_single(rids, uniq, rc, sc, group=group)
-    rrows = torch.empty((sum(rc), d), dtype=grad.dtype, device=dev)
-    dist.all_to_all_single(rrows, rows, rc, sc, group=group)
-    lo = rank * per
-    span = max(0, min(per, n - lo))
-    acc = torch.zeros((span, d), dtype=grad.dtype, device=dev)
-    off = 0
-    for r in range(world):            # fixed source order; ids distinct per source
-        if rc[r]:
-            acc.index_add_(0, rids[off:off + rc[r]] - lo, rrows[off:off + rc[r]])
-        off += rc[r]
-    mine = torch.unique(rids)
-    vals = acc.index_select(0, mine - lo)
-    cnt = torch.tensor([mine.numel()], dtype=torch.int64, device=dev)
-    cnts = [torch.empty_like(cnt) for _ in range(world)]
-    dist.all_gather(cnts, cnt, group=group)
-    cnts = [int(c.item()) for c in cnts]
-    cap = max(max(cnts), 1)
-    pid = torch.full((cap,), -1, dtype=torch.int64, device=dev)
-    pval = torch.zeros((cap, d), dtype=grad.dtype, device=dev)
-    pid[:mine.numel()] = mine
-    pval[:mine.numel()] = vals
-    aid = torch.empty((world * cap,), dtype=torch.int64, device=dev)
-    aval = torch.empty((world * cap, d), dtype=grad.dtype, device=dev)
-    dist.all_gather_into_tensor(aid, pid, group=group)
-    dist.all_gather_into_tensor(aval, pval, group=group)
-    keep = aid >= 0
-    grad.zero_()
-    grad.index_copy_(0, aid[keep], aval[keep])
-    return {"rows_sent": int(uniq.numel()), "rows_owned": int(mine.numel()), "rows_total": sum(cnts)}
-
-
 def touched_rows(model, ws: torch.Tensor, B: int, tables, elem_off, shard_elems: int, world: int):
     """Distinct rows of ``tables`` the batch of the last train-mode forward on
     ``ws`` touched, as flat-buffer element offsets (dcnr_emb_touched_rows):
@@ -180,60 +124,113 @@ def touched_rows(model, ws: torch.Tensor, B: int, tables, elem_off, shard_elems:
     return offs, tcnt, ocnt
 
 
-def sparse_reduce_scatter(gflat: torch.Tensor, gshard: torch.Tensor, width: int,
-                          offsets: torch.Tensor, table_counts: torch.Tensor,
-                          owner_counts: torch.Tensor, dense_lo: int, dense_hi: int,
-                          group=None) -> dict:
-    """The reduce-scatter of the embedding segment of ``gflat`` into this
-    rank's shard ``gshard`` (ZeRO-1: rank r owns elements [r*Es, (r+1)*Es)),
-    moving only touched rows:
+class DeviceSparseOps:
+    """The device halves of the sparse exchange (libdcnr).  The CPU tests hand
+    SparseExchange a host restatement with the same two methods."""
 
-      * ``offsets`` [n_tables, B]: per sparse table, this rank's touched rows
-        as ascending flat element offsets (row i of table t at
-        offsets[t, i] for i < table_counts[t]; each row ``width`` elements,
-        never straddling a shard; the tables in flat order);
-        ``owner_counts`` [world] how many go to each rank (device tensors,
-        as ``touched_rows`` returns them);
-      * one all_to_all of the counts, ONE host read of the send / receive /
-        table counts, one all_to_all of the offsets and of the rows;
-      * the owner zeroes its shard and adds what it received in source-rank
-        order (rows distinct per source: the sum is 0 + g_0 + g_1 + ..., the
-        same bits for every run);
-      * elements [dense_lo, dense_hi) (the small categorical tables) go
-        through an all-reduce and their part of the shard is copied in.
+    def pack(self, grad, offsets, table_counts, width, n_rows):
+        """Touched rows (offsets [n_tables, ld], table_counts on the device)
+        -> (send offsets [n_rows] int64, send rows [n_rows, width])."""
+        lib = _lib.load()
+        dev = grad.device
+        off = torch.empty(max(n_rows, 1), dtype=torch.int64, device=dev)
+        rows = torch.empty((max(n_rows, 1), width), dtype=grad.dtype, device=dev)
+        _lib.check(lib.dcnr_sparse_pack(grad.data_ptr(), offsets.data_ptr(), offsets.shape[1],
+                                        table_counts.data_ptr(), offsets.shape[0], width,
+                                        off.data_ptr(), rows.data_ptr(), _lib.stream_ptr(dev)),
+                   "dcnr_sparse_pack")
+        return off[:n_rows], rows[:n_rows]
+
+    def accumulate(self, shard, lo, width, offsets, rows, counts):
+        """shard = 0 + rows of source 0 + rows of source 1 + ... (counts: host
+        list, sources back to back)."""
+        lib = _lib.load()
+        c = (ctypes.c_int64 * len(counts))(*[int(x) for x in counts])
+        _lib.check(lib.dcnr_sparse_accumulate(shard.data_ptr(), int(lo), shard.numel(), width,
+                                              offsets.data_ptr() if offsets.numel() else None,
+                                              rows.data_ptr() if rows.numel() else None,
+                                              ctypes.cast(c, ctypes.c_void_p), len(counts),
+                                              _lib.stream_ptr(shard.device)),
+                   "dcnr_sparse_accumulate")
+
+
+_count_streams = {}
+
+
+class SparseExchange:
+    """The reduce-scatter of the embedding segment of the flat gradient into
+    this rank's ZeRO-1 shard (rank r owns elements [r*Es, (r+1)*Es)), moving
+    only touched rows, in two halves around the backward:
+
+      * ``begin(touched)`` right after the forward: ``touched`` = (offsets
+        [n_tables, B], table_counts, owner_counts) as ``touched_rows``
+        returns them (the sort that yields them runs under the forward).
+        One all_to_all of the owner counts; the send / receive / table
+        counts are copied to pinned host memory on a side stream that waits
+        for that exchange alone -- not for the backward.
+      * ``finish(gflat, gshard)`` after the backward is enqueued: the host
+        reads the counts (long since copied), then, stream-ordered after the
+        backward: the device pack of the touched rows, the all_to_all of
+        offsets and rows, the owner's fixed-order device accumulate (rows
+        distinct per source: 0 + g_0 + g_1 + ..., the same bits every run),
+        and the all-reduce of elements [dense_lo, dense_hi) (the small
+        categorical tables) copied into the shard.
 
     Rows no rank touched have an exactly-zero gradient (the backward
     zero-fills them), so the shard equals the dense reduce-scatter's sum."""
-    world = dist.get_world_size(group)
-    rank = dist.get_rank(group)
-    Es = gshard.numel()
-    dev = gflat.device
-    recv_counts = torch.empty_like(owner_counts)
-    dist.all_to_all_single(recv_counts, owner_counts, group=group)
-    counts = torch.cat([owner_counts, recv_counts, table_counts]).cpu().tolist()   # one host sync
-    sc, rc, tc = counts[:world], counts[world:2 * world], counts[2 * world:]
-    send_off = torch.cat([offsets[t, :tc[t]] for t in range(len(tc))])
-    col = torch.arange(width, device=dev, dtype=torch.int64)
-    rows = gflat[send_off[:, None] + col[None, :]] if send_off.numel() else \
-        torch.empty((0, width), dtype=gflat.dtype, device=dev)
-    r_off = torch.empty(sum(rc), dtype=torch.int64, device=dev)
-    r_rows = torch.empty((sum(rc), width), dtype=gflat.dtype, device=dev)
-    dist.all_to_all_single(r_off, send_off, rc, sc, group=group)
-    dist.all_to_all_single(r_rows, rows, rc, sc, group=group)
-    gshard.zero_()
-    gv = gshard.view(-1, width)
-    lo = rank * Es
-    pos = 0
-    for r in range(world):                    # fixed source order
-        if rc[r]:
-            gv.index_add_(0, torch.div(r_off[pos:pos + rc[r]] - lo, width, rounding_mode="floor"),
-                          r_rows[pos:pos + rc[r]])
-        pos += rc[r]
-    if dense_hi > dense_lo:                   # the small tables: dense all-reduce
-        dense = gflat[dense_lo:dense_hi].clone()
-        dist.all_reduce(dense, op=dist.ReduceOp.SUM, group=group)
-        a, b = max(dense_lo, lo), min(dense_hi, lo + Es)
-        if b > a:
-            gshard[a - lo:b - lo].copy_(dense[a - dense_lo:b - dense_lo])
-    return {"rows_sent": sum(sc), "rows_received": sum(rc),
-            "bytes_sent": sum(sc) * (8 + 4 * width) + 4 * max(0, dense_hi - dense_lo)}
+
+    def __init__(self, width: int, dense_lo: int, dense_hi: int, group=None, ops=None):
+        self.width, self.dense_lo, self.dense_hi, self.group = width, dense_lo, dense_hi, group
+        self.ops = ops or DeviceSparseOps()
+        self._pending = None
+
+    def begin(self, touched):
+        offsets, tcnt, ocnt = touched
+        world = dist.get_world_size(self.group)
+        dev = ocnt.device
+        recv = torch.empty_like(ocnt)
+        work = dist.all_to_all_single(recv, ocnt, group=self.group, async_op=True)
+        n = 2 * world + tcnt.numel()
+        if dev.type == "cuda":
+            host = torch.empty(n, dtype=torch.int64, pin_memory=True)
+            side = _count_streams.get(dev)
+            if side is None:
+                side = _count_streams[dev] = torch.cuda.Stream(device=dev)
+            side.wait_stream(torch.cuda.current_stream(dev))   # the counts' producers
+            with torch.cuda.stream(side):
+                work.wait()                                     # ... and the exchange, nothing later
+                host.copy_(torch.cat([ocnt, recv, tcnt]), non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(side)
+        else:
+            work.wait()
+            host, ev = torch.cat([ocnt, recv, tcnt]), None
+        self._pending = (offsets, tcnt, ocnt, recv, host, ev)
+
+    def finish(self, gflat: torch.Tensor, gshard: torch.Tensor) -> dict:
+        offsets, tcnt, ocnt, recv, host, ev = self._pending
+        self._pending = None
+        world = dist.get_world_size(self.group)
+        rank = dist.get_rank(self.group)
+        if ev is not None:
+            ev.synchronize()
+        counts = host.tolist()
+        sc, rc = counts[:world], counts[world:2 * world]
+        width, Es = self.width, gshard.numel()
+        dev = gflat.device
+        send_off, rows = self.ops.pack(gflat, offsets, tcnt, width, sum(sc))
+        r_off = torch.empty(sum(rc), dtype=torch.int64, device=dev)
+        r_rows = torch.empty((sum(rc), width), dtype=gflat.dtype, device=dev)
+        dist.all_to_all_single(r_off, send_off, rc, sc, group=self.group)
+        dist.all_to_all_single(r_rows, rows, rc, sc, group=self.group)
+        lo = rank * Es
+        self.ops.accumulate(gshard, lo, width, r_off, r_rows, rc)
+        dense_lo, dense_hi = self.dense_lo, self.dense_hi
+        if dense_hi > dense_lo:                   # the small tables: dense all-reduce
+            dense = gflat[dense_lo:dense_hi].clone()
+            dist.all_reduce(dense, op=dist.ReduceOp.SUM, group=self.group)
+            a, b = max(dense_lo, lo), min(dense_hi, lo + Es)
+            if b > a:
+                gshard[a - lo:b - lo].copy_(dense[a - dense_lo:b - dense_lo])
+        return {"rows_sent": sum(sc), "rows_received": sum(rc),
+                "bytes_sent": sum(sc) * (8 + 4 * width) + 4 * max(0, dense_hi - dense_lo)}

@@ -20,12 +20,14 @@ optimizer.step) as native calls over flat parameter/gradient/moment buffers:
            shard_optimizer=False: all-reduce, every rank updates everything
            exchange="sparse" (ZeRO-1 like the default): the user and item
              tables' gradient rows the rank's batch touched -- read from the
-             backward's own id sort (dcnr_emb_touched_rows) -- go to the
+             forward's own id sort (dcnr_emb_touched_rows) -- go to the
              owners of their parameter shard (all_to_all), each owner sums
-             them in rank order into its shard (dcnr.parallel.
-             sparse_reduce_scatter; one host read of the message sizes), the
-             small categorical tables go through an all-reduce; then AdamW
-             on the shard and the all-gather of the parameters, as above
+             them in rank order into its shard (dcnr.parallel.SparseExchange:
+             device pack and accumulate; the message sizes are exchanged
+             after the forward and read once the backward is enqueued, so the
+             GPU never idles for the host), the small categorical tables go
+             through an all-reduce; then AdamW on the shard and the
+             all-gather of the parameters, as above
 
 Numerically the same update as ``torch.optim.AdamW``/``Adam`` on the
 reference's dense gradients (every embedding row's moments decay every step).
@@ -47,7 +49,7 @@ from .ops import bce_with_logits
 class FusedTrainer:
     def __init__(self, model: DCN_RecSys, lr=1e-3, weight_decay=1e-2, optimizer_name='AdamW',
                  betas=(0.9, 0.999), eps=1e-8, process_group=None, sync_bn=False,
-                 shard_optimizer=None, exchange="dense"):
+                 shard_optimizer=None, exchange="dense", sparse_ops=None):
         if optimizer_name not in ('AdamW', 'Adam'):
             raise ValueError("optimizer_name must be 'AdamW' or 'Adam' (train.py:201-204)")
         self.model = model
@@ -86,6 +88,12 @@ class FusedTrainer:
                              f"shards (emb_dim {d}, shard {self.Es} elements)")
         self._B = 0
         self.last_exchange = None
+        self._sparse = None
+        if self._sparse_ok and self.world > 1:
+            from .parallel import SparseExchange
+            lay = self._sparse_layout
+            self._sparse = SparseExchange(d, lay["dense_lo"], lay["dense_hi"], process_group,
+                                          ops=sparse_ops)
         self.m = torch.zeros(self.Es + N - self.E, dtype=torch.float32, device=self.flat.device)
         self.v = torch.zeros_like(self.m)
         self.gshard = torch.empty(self.Es, dtype=torch.float32,
@@ -117,6 +125,10 @@ class FusedTrainer:
         model._index_watch.poll()
         logits, self._ws = run_forward(model, True, seed, user, item, cat, num, self._ws)
         self._B = user.shape[0]
+        if self.exchange == "sparse" and self._sparse is not None:
+            # the touched rows come from the forward's id sort: their counts
+            # are exchanged now, under the backward
+            self._sparse.begin(self.touched_rows())
         # grad_scale 1/world: the SUM all-reduce then yields the global mean gradient
         loss, dz = bce_with_logits(logits, y, True, 1.0 / self.world)
         self._dense_work = None
@@ -187,14 +199,11 @@ class FusedTrainer:
                                     async_op=True)
         if self.shard:
             if self.exchange == "sparse":
-                if not self._sparse_ok:
+                if self._sparse is None:
                     raise ValueError("exchange='sparse': table rows not aligned to the shards")
-                from .parallel import sparse_reduce_scatter
-                lay = self._sparse_layout
-                offs, tcnt, ocnt = touched if touched is not None else self.touched_rows()
-                self.last_exchange = sparse_reduce_scatter(
-                    self.gflat, self.gshard, lay["width"], offs, tcnt, ocnt, lay["dense_lo"],
-                    lay["dense_hi"], self.pg)
+                if touched is not None or self._sparse._pending is None:
+                    self._sparse.begin(touched if touched is not None else self.touched_rows())
+                self.last_exchange = self._sparse.finish(self.gflat, self.gshard)
             else:
                 dist.reduce_scatter_tensor(self.gshard, self.gflat[:E], op=dist.ReduceOp.SUM,
                                            group=self.pg)

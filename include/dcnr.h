@@ -225,6 +225,30 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
  * [r*shard_elems, (r+1)*shard_elems).
  * Stream-ordered; outputs are device memory. */
 #define DCNR_TOUCHED_MAX_WORLD 64
+
+/* The sparse exchange's send buffers, built on the device from
+ * dcnr_emb_touched_rows' output (SURVEY.md 8(e) option B; the rows of the
+ * dense gradient of train.py:156-158 under train.py:225): for each of
+ * n_tables tables, the table_counts[t] (device) offsets offsets[t*ld ..] and
+ * the `width`-float gradient rows of `grad` they address are appended, tables
+ * in order, to out_offsets / out_rows [sum(table_counts)][width].  Offsets
+ * ascend within a table and the tables are in flat order, so the list is
+ * grouped by shard owner.  Stream-ordered; no host synchronisation. */
+dcnr_status dcnr_sparse_pack(const float* grad, const int64_t* offsets, int64_t ld,
+                             const int64_t* table_counts, int32_t n_tables, int32_t width,
+                             int64_t* out_offsets, float* out_rows, dcnr_stream_t stream);
+
+/* The owner's half of the sparse exchange: zeroes shard [shard_elems] (flat
+ * elements [shard_lo, shard_lo + shard_elems) of the gradient) and adds the
+ * rows the n_sources ranks sent, back to back in `offsets` / `rows`
+ * (source_counts[r] rows from rank r: a HOST array), sources in rank order --
+ * every shard row is summed 0 + g_0 + g_1 + ..., the same bits run to run.
+ * Within one source the offsets are distinct.  Offsets outside the shard are
+ * skipped. */
+dcnr_status dcnr_sparse_accumulate(float* shard, int64_t shard_lo, int64_t shard_elems, int32_t width,
+                                   const int64_t* offsets, const float* rows,
+                                   const int64_t* source_counts, int32_t n_sources,
+                                   dcnr_stream_t stream);
 dcnr_status dcnr_emb_touched_rows(const dcnr_model_desc* desc, const void* ws, size_t ws_bytes,
                                   int64_t B, int32_t n_tables, const int32_t* tables,
                                   const int64_t* elem_off, int64_t shard_elems, int32_t world,

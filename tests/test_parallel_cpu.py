@@ -239,12 +239,37 @@ def test_sharded_optimizer_exchange_matches_allreduce_adam(world):
     _run(_exchange_worker, world)
 
 
+class HostSparseOps:
+    """Host restatement of libdcnr's sparse-exchange kernels (dcnr_sparse_pack:
+    the tables' touched rows in flat order; dcnr_sparse_accumulate: zero,
+    then every source's rows added in rank order) -- the CPU side of the
+    protocol test; the GPU tests run the kernels."""
+
+    def pack(self, grad, offsets, table_counts, width, n_rows):
+        tc = table_counts.tolist()
+        off = torch.cat([offsets[t, :tc[t]] for t in range(len(tc))])
+        assert off.numel() == n_rows
+        col = torch.arange(width, dtype=torch.int64)
+        rows = grad[off[:, None] + col[None, :]] if n_rows else torch.empty((0, width))
+        return off, rows
+
+    def accumulate(self, shard, lo, width, offsets, rows, counts):
+        shard.zero_()
+        sv = shard.view(-1, width)
+        pos = 0
+        for c in counts:
+            if c:
+                sv.index_add_(0, torch.div(offsets[pos:pos + c] - lo, width, rounding_mode="floor"),
+                              rows[pos:pos + c])
+            pos += c
+
+
 def _sparse_worker(rank, world, port, d):
-    """Owner-bucketed sparse exchange of the user table (FusedTrainer
-    exchange="sparse"): each rank's user-table gradient is nonzero only on
-    its batch's ids (what dcnr_backward writes); after the exchange every rank
-    holds the dense SUM, bit for bit (summed in rank order), and the AdamW
-    step matches the single-process update."""
+    """Owner-bucketed sparse exchange of the user and item tables
+    (FusedTrainer exchange="sparse"): each rank's table gradients are nonzero
+    only on its batch's ids (what dcnr_backward writes); after the exchange
+    the owner's shard holds the dense SUM, bit for bit (summed in rank
+    order), and the AdamW step matches the single-process update."""
     _init(rank, world, port)
     try:
         import dcnr
@@ -252,18 +277,6 @@ def _sparse_worker(rank, world, port, d):
         ids = [torch.randint(0, n_users, (40,), generator=torch.Generator().manual_seed(50 + r))
                for r in range(world)]
         ids[world - 1][:5] = n_users - 1          # the last owner's tail row
-        grads = []
-        for r in range(world):
-            gr = torch.zeros(n_users, d)
-            u = torch.unique(ids[r])
-            gr[u] = torch.randn(u.numel(), d, generator=torch.Generator().manual_seed(7 + r))
-            grads.append(gr)
-        mine = grads[rank].clone()
-        info = parallel.sparse_rows_allreduce(mine, ids[rank])
-        want = sum(grads)
-        assert torch.equal(mine, want)
-        assert info["rows_sent"] == torch.unique(ids[rank]).numel()
-        assert info["rows_total"] == torch.unique(torch.cat(ids)).numel()
         # through FusedTrainer(exchange="sparse"): the user and item tables'
         # touched rows go to the owners of their ZeRO-1 shard
         # (sparse_reduce_scatter), the categorical tables through an
@@ -273,7 +286,8 @@ def _sparse_worker(rank, world, port, d):
         m = dcnr.DCN_RecSys(n_users, n_items, {"a": 10, "b": 3}, 3,
                             dict(emb_dim=d, hidden_dim=16, n_cross_layers=1, n_res_blocks=1,
                                  dropout=0.0))
-        tr = dcnr.FusedTrainer(m, lr=1e-2, weight_decay=1e-2, exchange="sparse")
+        tr = dcnr.FusedTrainer(m, lr=1e-2, weight_decay=1e-2, exchange="sparse",
+                               sparse_ops=HostSparseOps())
         assert tr.shard and tr.m.numel() == tr.E // world + tr.flat.numel() - tr.E
         lay = tr._sparse_layout
         nu = lay["elem_off"][1]
