@@ -70,6 +70,7 @@ CLASS_KERNELS = {
     "head": "row_dot / head_parts / logits / bce kernels",
     "adam": "adam_kernel (fused AdamW)",
     "pack": "pack / zero-fill kernels",
+    "tower": "tower_kernel (fused eval deep tower: 9 Linear + BN + ReLU + residual + head, one launch)",
 }
 
 
@@ -609,13 +610,27 @@ def main():
     eval_bytes_pair = sum(v[2] for v in eprof.values() if v[1]) / n_pairs
     eval_gbs = eval_bytes_pair * pairs_per_s / world / 1e9   # per GPU
     eval_tf = EVAL_FLOP_PER_PAIR * pairs_per_s / world / 1e12
+    # the fused tower keeps the activations on chip: the eval forward is then
+    # MFMA-bound (its bytes per pair are the x0 row, zc and the logit), so the
+    # MFMA view is the roofline and the HBM view is reported beside it
+    tower = "tower" in eprof and eprof["tower"][1] > 0
+    tower_ms = eprof["tower"][0] / args.eval_steps if tower else None
     eval_roof = {
-        "bound": "hbm", "unit": "GB/s", "scope": "whole eval forward (every launch), per GPU",
-        "bytes_per_pair": eval_bytes_pair, "achieved": eval_gbs, "peak": PEAK_HBM / 1e9,
-        "frac": eval_gbs * 1e9 / PEAK_HBM,
+        "bound": "mfma" if tower else "hbm",
+        "unit": "TFLOP/s" if tower else "GB/s", "scope": "whole eval forward (every launch), per GPU",
+        "achieved": eval_tf if tower else eval_gbs,
+        "peak": PEAK_BF16 / 1e12 if tower else PEAK_HBM / 1e9,
+        "frac": eval_tf * 1e12 / PEAK_BF16 if tower else eval_gbs * 1e9 / PEAK_HBM,
+        "bytes_per_pair": eval_bytes_pair,
+        "hbm_view": {"achieved_gbs": eval_gbs, "peak_gbs": PEAK_HBM / 1e9,
+                     "frac": eval_gbs * 1e9 / PEAK_HBM},
         "flop_per_pair": EVAL_FLOP_PER_PAIR,
         "mfma_view": {"achieved_tflops": eval_tf, "peak_tflops": PEAK_BF16 / 1e12,
                       "frac": eval_tf * 1e12 / PEAK_BF16},
+        "tower_kernel": None if not tower else {
+            "us_per_call": tower_ms * 1e3, "samples_per_call": B,
+            "achieved_tflops": EVAL_FLOP_PER_PAIR * B / (tower_ms * 1e-3) / 1e12,
+            "frac_of_bf16_peak": EVAL_FLOP_PER_PAIR * B / (tower_ms * 1e-3) / PEAK_BF16},
         "by_class": {k: {"ms_per_call": v[0] / args.eval_steps, "launches_per_call":
                          v[1] / args.eval_steps, "bytes_per_pair": v[2] / n_pairs}
                      for k, v in eprof.items() if v[1]},

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Tower lab variants + fold probe + GPU tests + bench in one box visit.
+#   bash tools/r04_lab.sh <tag> "<variants>"
+set -o pipefail
+R=gpurun_out/$1
+mkdir -p $R
+for v in $2; do
+  DCNR_LIB=$PWD/tools/lab_bin/libdcnr_tw_$v.so timeout -k 10 120 python -u tools/tower_probe.py 200 131072 > $R/probe_$v.log 2>&1 || exit 1
+done
+timeout -k 10 120 python -u tools/fold_probe.py > $R/fold.log 2>&1 || exit 1
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread > $R/gpu_tests.log 2>&1 || exit 1
+timeout -k 10 400 python3 -u bench.py > $R/bench.log 2>&1 || exit 1
