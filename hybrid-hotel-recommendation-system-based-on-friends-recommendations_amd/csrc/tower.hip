@@ -40,7 +40,7 @@ constexpr int TW_NT = 256, TW_WAVES = 4, TW_S = 32, TW_TILE = TW_WAVES * TW_S;
 constexpr int TW_KT0 = 16;                    // k-steps of the initial Linear (Dp <= 512, zero padded)
 constexpr int TW_SLOT = 2 * TW_KT0 * 1024 + 256;   // ring slot: 2 output blocks x 16 k-steps + constants
 constexpr int TW_CONST = 2 * TW_KT0 * 1024;   // constants' offset in a slot: sc[32], sh[32]
-constexpr int TW_NSLOT = 3;
+constexpr int TW_NSLOT = 4;   // (3 slots: 636 vs 622 us per bench-size call, tools/tower_lab.sh)
 
 // LDS-DMA of 16 B per lane: voff (per lane) + soff (wave-uniform) into
 // lds_dst + 16 * lane.  dma16's form with the uniform part of the offset in
@@ -230,8 +230,12 @@ __device__ __forceinline__ void tw_slice(const char* sl, int g, int lane, const 
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  // (short k-loops: the pieces left over)
+  // (short k-loops, KT < 9: the DMA and epilogue pieces left over)
   for (int d = KT; d <= TW_KT0 / 2; ++d) dma(d);
+  if constexpr (PEND) {
+#pragma unroll
+    for (int p = KT; p < 8; ++p) epi_piece<MODE>(pend, p, p0, p1);
+  }
   const float* cst = reinterpret_cast<const float*>(sl + TW_CONST);
 #pragma unroll
   for (int ob = 0; ob < 2; ++ob) {

@@ -15,7 +15,8 @@ import dcnr  # noqa: E402
 
 dev = torch.device("cuda:0")
 cfg = dict(n_users=1_000_000, n_items=100_000, cat_dims={f"c{i}": 1000 for i in range(12)}, n_num=8,
-           params=dict(emb_dim=32, hidden_dim=512, n_cross_layers=3, n_res_blocks=4, dropout=0.6))
+           params=dict(emb_dim=32, hidden_dim=int(os.environ.get("TOWER_H", "512")), n_cross_layers=3,
+                       n_res_blocks=4, dropout=0.6))
 torch.manual_seed(42)
 m = dcnr.DCN_RecSys(cfg["n_users"], cfg["n_items"], cfg["cat_dims"], cfg["n_num"], dict(cfg["params"]),
                     precision="bf16").to(dev).eval()
@@ -35,4 +36,7 @@ for B in [int(x) for x in (sys.argv[1:] or ["200", "4096", "131072"])]:
             b.record()
             torch.cuda.synchronize()
         ms = a.elapsed_time(b) / it
-        print(f"B={B} {'layers' if keep else 'tower '} {ms*1e3:8.1f} us/call  {B/ms/1e3:8.2f} M pairs/s", flush=True)
+        H = cfg["params"]["hidden_dim"]
+        tf = 2 * (456 * H + 8 * H * H) * B / (ms * 1e-3) / 1e12
+        print(f"H={H} B={B} {'layers' if keep else 'tower '} {ms*1e3:8.1f} us/call  {B/ms/1e3:8.2f} M pairs/s"
+              f"  {tf:6.0f} TF/s", flush=True)
