@@ -38,6 +38,8 @@ GROUPS = [
     ("knn scan4<2,2> (<= 32 queries)", r"scan4_kernel<2, 2,"),
     ("knn rescore", r"rescore_kernel"),
     ("knn scan3", r"scan3_kernel"),
+    ("tower_kernel (fused eval tower)", r"tower_kernel"),
+    ("tower_pack", r"tower_pack"),
 ]
 
 
