@@ -338,12 +338,20 @@ bool eval_fuse_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && gemm_ws_su
 
 // The eval forward's deep tower as one persistent launch (tower.hip): bf16,
 // the shapes it covers (input width <= 512, hidden <= 512), not when the
-// stage tests ask for every intermediate.
-bool tower_ok(const Dims& d, bool train, bool keep) {
-  return !train && !keep && d.prec == DCNR_PREC_BF16 && tower_supported(d.Dp, d.H, d.R);
+// stage tests ask for every intermediate, and from TOWER_MIN_B samples (or
+// with DCNR_FLAG_FUSED_TOWER): one 128-sample tile per CU walks all 2R+1
+// layers in sequence, ~150 us however few tiles there are, while the
+// layer-by-layer path spreads each layer over the chip (bench model: 179 vs
+// 139 us at 4096 samples, 622 vs 806 us at 131072).
+constexpr int64_t TOWER_MIN_B = 16384;
+bool tower_ok(const Dims& d, bool train, uint32_t flags, int64_t B) {
+  const bool size_ok = B >= TOWER_MIN_B || (flags & DCNR_FLAG_FUSED_TOWER);
+  return !train && !(flags & DCNR_FLAG_KEEP_INTERMEDIATES) && size_ok && d.prec == DCNR_PREC_BF16 &&
+         tower_supported(d.Dp, d.H, d.R);
 }
 
-Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = false) {
+Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, uint32_t flags = 0) {
+  const bool keep = (flags & DCNR_FLAG_KEEP_INTERMEDIATES) != 0;
   Layout L;
   memset(&L, 0, sizeof(L));
   Bump b(ws);
@@ -351,7 +359,7 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, bool keep = fal
   const size_t es = d.es;
   const size_t act = (size_t)B * d.Hp * es;
   L.err = (int*)b.take(256);
-  if (tower_ok(d, train, keep)) {   // x0, zc, the packed slices: nothing of the tower in HBM
+  if (tower_ok(d, train, flags, B)) {   // x0, zc, the packed slices: nothing of the tower in HBM
     L.x0 = b.take((size_t)B * d.Dp * es);
     L.zc = (float*)b.take(B * 4);
     L.twp = (char*)b.take((size_t)tower_ws_bytes(d.H, d.R));
@@ -900,7 +908,7 @@ dcnr_status dcnr_workspace_size(const dcnr_model_desc* desc, int64_t B, int mode
   Dims d;
   TRY(make_dims(desc, &d));
   if (!bytes || B < 0) { set_error("bad args"); return DCNR_BAD_ARG; }
-  *bytes = make_layout(d, B, mode, nullptr, keep_of(desc)).total;
+  *bytes = make_layout(d, B, mode, nullptr, desc->flags).total;
   return DCNR_OK;
 }
 
@@ -912,7 +920,7 @@ dcnr_status dcnr_workspace_offset(const dcnr_model_desc* desc, int64_t B, int mo
   // a null base yields offsets as pointers from 0 (Bump takes nullptr -> nullptr),
   // so lay out against a fake non-null base
   char* base = (char*)(uintptr_t)4096;
-  Layout L = make_layout(d, B, mode, base, keep_of(desc));
+  Layout L = make_layout(d, B, mode, base, desc->flags);
   const bool train = mode == DCNR_TRAIN;
   const int R = d.R;
   auto blk = [&](int n) { return index >= 0 && index < n; };
@@ -990,7 +998,7 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     set_error("Expected more than 1 value per channel when training");
     return DCNR_BAD_ARG;
   }
-  Layout L = make_layout(d, B, mode, ws, keep_of(desc));
+  Layout L = make_layout(d, B, mode, ws, desc->flags);
   if (ws_bytes < L.total) {
     set_error("workspace too small: %zu < %zu", ws_bytes, L.total);
     return DCNR_WORKSPACE_TOO_SMALL;
@@ -1160,7 +1168,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     set_error("dcnr_backward: bad argument");
     return DCNR_BAD_ARG;
   }
-  Layout L = make_layout(d, B, DCNR_TRAIN, ws, keep_of(desc));
+  Layout L = make_layout(d, B, DCNR_TRAIN, ws, desc->flags);
   if (ws_bytes < L.total) {
     set_error("workspace too small: %zu < %zu", ws_bytes, L.total);
     return DCNR_WORKSPACE_TOO_SMALL;
@@ -1421,7 +1429,7 @@ dcnr_status dcnr_emb_touched_rows(const dcnr_model_desc* desc, const void* ws, s
     set_error("dcnr_emb_touched_rows: bad argument");
     return DCNR_BAD_ARG;
   }
-  Layout L = make_layout(d, B, DCNR_TRAIN, (void*)ws, keep_of(desc));
+  Layout L = make_layout(d, B, DCNR_TRAIN, (void*)ws, desc->flags);
   if (ws_bytes < L.total) {
     set_error("workspace too small: %zu < %zu", ws_bytes, L.total);
     return DCNR_WORKSPACE_TOO_SMALL;

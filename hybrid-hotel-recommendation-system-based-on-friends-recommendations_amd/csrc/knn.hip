@@ -15,7 +15,8 @@
 //  * scan v3 (Q >= 16, d % 16 == 0, d not 32 / 64): exact fp32-MFMA scan
 //    into per-slice k-lists;
 //  * scan v2 (d <= 64, k <= 32): exact VALU scan with wave-register lists --
-//    small Q, and v4's gated fallback (the same distance arithmetic);
+//    small Q (v4's per-query exact fallback is the same scan inside one
+//    block, the same distance arithmetic);
 //  * scan v1 (the rest, k <= 64): the original streaming scan below --
 //    each workgroup scans one contiguous row slice; every thread owns one
 //    row per step (16-B loads), computes QT dots against the LDS-resident
@@ -210,12 +211,10 @@ __global__ __launch_bounds__(K2_NT) void scan2_kernel(const float* __restrict__ 
                                                       const float* __restrict__ qn, int64_t Q,
                                                       int k, int64_t rows_per_block, int nslices,
                                                       int qtiles, Cand* out,
-                                                      const float* __restrict__ thr0,
-                                                      const int* gate = nullptr) {
+                                                      const float* __restrict__ thr0) {
   __shared__ float cd[K2_WPB][K2_QT][K2_CAP];
   __shared__ int ci[K2_WPB][K2_QT][K2_CAP];
   __shared__ int cntl[K2_WPB][K2_QT];
-  if (gate && *gate == 0) return;   // scan v4 fallback: only when v4 overflowed
   const int bid = blockIdx.x;
   const int tile = (bid / 8) % qtiles;
   const int slice = (bid % 8) + 8 * (bid / (8 * qtiles));
@@ -326,10 +325,8 @@ __global__ __launch_bounds__(K2_NT) void scan3_kernel(const float* __restrict__ 
                                                       const float* __restrict__ qn, int64_t Q,
                                                       int k, int64_t rows_per_block, int nslices,
                                                       int qtiles, Cand* out,
-                                                      const float* __restrict__ thr0,
-                                                      const int* gate = nullptr) {
+                                                      const float* __restrict__ thr0) {
   constexpr int S4 = DV / 4;
-  if (gate && *gate == 0) return;   // scan v4 fallback: only when v4 overflowed
   __shared__ float cd[K2_WPB][K3_QT][K2_CAP];
   __shared__ int ci[K2_WPB][K3_QT][K2_CAP];
   __shared__ int cntl[K2_WPB][K3_QT];
@@ -469,7 +466,7 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
                                                         const float* __restrict__ inv, int64_t N,
                                                         const float* __restrict__ q, float* qn,
                                                         int k, float* thr0, bf16* qb = nullptr,
-                                                        int* qcnt = nullptr, int* gate = nullptr) {
+                                                        int* qcnt = nullptr) {
   constexpr int PT = SAMPLE / NTB;
   constexpr int d = DV * 4;   // <= 64: one element per lane
   __shared__ unsigned hist[256];
@@ -488,7 +485,6 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
       if (qb) qb[qq * d + lane] = (bf16)(v * in);
     }
     if (qcnt && lane == 0) qcnt[qq] = 0;
-    if (gate && qq == 0 && lane == 0) *gate = 0;
   }
   __syncthreads();
   const float4* qv = reinterpret_cast<const float4*>(qs);
@@ -575,10 +571,12 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 // kth_bound_kernel (pass 1).  The admitted rows (~N k / V4_S per query) are
 // appended to a per-query list with their exact fp32 distances (scan v2's
 // arithmetic, computed in scan4's epilogue); rescore_kernel selects the k
-// best by (distance, row).  A query whose
-// list overflows V4_CAP (or whose k-th distance is shared by more than
-// V4_SCAP rows) raises a flag and the exact scan v2 + merge, launched behind
-// it and gated on the flag, recomputes the batch.
+// best by (distance, row).  A query whose list overflows V4_CAP (the count
+// word carries V4_OVF when a block's wave list ran out of room), or whose
+// k-th distance is shared by more than V4_SCAP rows, is answered by an exact
+// scan of the whole table inside its own rescore block (scan v2's per-wave
+// lists and arithmetic): no batch-wide flag, no gated launches behind the
+// chain.  In pass 1 the same conditions just keep the 512-row bound.
 constexpr float V4_EPS = 0.004f;
 constexpr int V4_S = 32768;     // exact sample rows for the admission bound (larger first
                                 // bound samples measured slower: DESIGN.md section 4)
@@ -586,6 +584,7 @@ constexpr int V4_WPS = 3;       // min waves per SIMD of scan4 for NQB > 4
 constexpr int V4_SNQ = 16;      // query blocks per launch row of the sample pass (Q=256: 31 vs 43 us at 2)
 constexpr int V4_CAP = 4096;     // admitted rows per query
 constexpr int V4_SCAP = 256;     // rows at or under the selected k-th bin
+constexpr int V4_OVF = 1 << 30;  // count-word mark: a block dropped some of this query's rows
 constexpr int V4_QC = 256;       // queries per block (LDS: V4_QC x d bf16)
 // table rows per block: few query blocks -> long blocks (the per-block
 // prologue and epilogue amortised; measured 69 vs 78 us at Q = 32), many ->
@@ -698,7 +697,7 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
                                                     const bf16* __restrict__ qb,
                                                     const float* __restrict__ thr0,
                                                     const float* __restrict__ qn, int64_t Q, int* qcnt,
-                                                    int* rows, float* dists, int* flag) {
+                                                    int* rows, float* dists) {
   constexpr int D = KS * 32;
   // up to 4 query blocks the B fragments live in registers; beyond that
   // (64+ KS x 4 VGPRs) in LDS, stored in fragment order -- entry (b, ks,
@@ -856,8 +855,9 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
   if (lane == 0) wcnt[w] = wc;
   __syncthreads();
   const int c0 = wcnt[0], c1 = wcnt[1], c2 = wcnt[2], c3 = wcnt[3];
-  if (max(max(c0, c1), max(c2, c3)) > V4_WL) {   // a wave's list overflowed: exact fallback
-    if (threadIdx.x == 0) *flag = 1;
+  if (max(max(c0, c1), max(c2, c3)) > V4_WL) {   // a wave's list overflowed: every query
+    for (int q = threadIdx.x; q < nq; q += 256)     // of the block takes the exact path
+      atomicOr(&qcnt[qc0 + q], V4_OVF);
     return;
   }
   // entry j of the block (waves' lists back to back) -> its LDS slot
@@ -899,35 +899,126 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
     }
     const float dist = fminf(fmaxf(1.f - s * ir, 0.f), 2.f);
     const int pos = atomicAdd(&qn_[qe], 1);
-    if (pos < V4_CAP) {
+    if (pos < V4_CAP) {   // (past it the query's count exceeds V4_CAP: exact path)
       const int64_t o = (qc0 + qe) * V4_CAP + pos;
       rows[o] = re;
       dists[o] = dist;
-    } else {
-      *flag = 1;
     }
   }
 }
 
 
+// Exact top-k of one query over the whole table inside one B4_T-thread block:
+// scan v2's per-wave lists (rows in increasing order per wave, admitted while
+// strictly under the wave's k-th best, compacted by a register bitonic sort)
+// and its distance arithmetic expression for expression, then wave 0 merges
+// the waves' sorted k-lists.  The same (distance, row) order as every other
+// scan, so a query that lands here returns what scan v2 returns.  Needs
+// k <= 32 (two k-lists per 64-lane merge step) and 16 * 64 * 8 B of LDS.
+template <int DV>
+__device__ void exact_query_topk(const float* __restrict__ tab, const float* __restrict__ inv, int64_t N,
+                                 const float* __restrict__ qrow, int k, float* lds, int64_t* idx,
+                                 float* dist) {
+  constexpr int NW = B4_T / 64;
+  __shared__ int cntl[NW];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* lcd = lds + w * 64;
+  int* lci = reinterpret_cast<int*>(lds + NW * 64) + w * 64;
+  // wave-uniform addresses: the query comes in through scalar loads
+  const float4* qv = reinterpret_cast<const float4*>(qrow);
+  int c = 0;
+  float th = FLT_MAX;
+  for (int64_t base = 64 * w; base < N; base += 64 * NW) {
+    const int64_t r = base + lane;
+    const bool ok = r < N;
+    const int64_t rc = ok ? r : 0;
+    float4 x[DV];
+    const float4* rp = reinterpret_cast<const float4*>(tab + rc * DV * 4);
+#pragma unroll
+    for (int v = 0; v < DV; ++v) x[v] = rp[v];
+    const float ir = inv[rc];
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < DV; ++v) {
+      const float4 q = qv[v];
+      s += x[v].x * q.x + x[v].y * q.y + x[v].z * q.z + x[v].w * q.w;
+    }
+    const float dd = fminf(fmaxf(1.f - s * ir, 0.f), 2.f);
+    bool pass = ok && dd < th;
+    uint64_t m = __ballot(pass);
+    while (m) {
+      const int room = 64 - c;
+      if (room == 0) {
+        c = wave_compact(lcd, lci, c, k, lane, &th);
+        pass = pass && dd < th;
+        m = __ballot(pass);
+        continue;
+      }
+      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+      if (pass && rank < room) {
+        lcd[c + rank] = dd;
+        lci[c + rank] = (int)r;
+      }
+      const int n = __popcll(m);
+      c += n < room ? n : room;
+      pass = pass && rank >= room;
+      m = __ballot(pass);
+    }
+  }
+  c = wave_compact(lcd, lci, c, k, lane, &th);
+  if (lane == 0) cntl[w] = c;
+  __syncthreads();
+  if (w == 0) {
+    float d = FLT_MAX;
+    int i = INT_MAX;
+    for (int ww = 0; ww < NW; ++ww) {
+      const int cw = cntl[ww];
+      const int sl = ww == 0 ? lane : lane - k;
+      if (ww == 0 || lane >= k) {
+        const bool has = sl >= 0 && sl < k && sl < cw;
+        d = has ? lds[ww * 64 + sl] : FLT_MAX;
+        i = has ? reinterpret_cast<const int*>(lds + NW * 64)[ww * 64 + sl] : INT_MAX;
+      }
+      if (ww > 0) wave_sort64(d, i, lane);
+    }
+    if (lane < k) {
+      idx[lane] = (int64_t)i;
+      dist[lane] = d;
+    }
+  }
+}
+
 // One block per query: the exact distances of its admitted rows (computed
 // by scan4's epilogue), the k-th smallest by block_select_kth, then a bitonic
 // sort of the rows at or under the selected bin by (distance, row).  SMP: the
 // pass over the V4_S-row sample -- its exact k-th distance becomes the
-// query's admission bound thr0 for the table scan, and the list count is
-// reset for it.
-template <bool SMP>
+// query's admission bound thr0 for the table scan (left at the 512-row bound
+// when the sample list overflowed), and the list count is reset for it.
+// Otherwise a query whose list overflowed takes exact_query_topk (DV = d / 4).
+template <bool SMP, int DV>
 __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__ dists, int* qcnt,
                                                        const int* rows, int k, int64_t* idx,
-                                                       float* dist, int* flag, float* thr0) {
+                                                       float* dist, float* thr0,
+                                                       const float* __restrict__ tab,
+                                                       const float* __restrict__ inv, int64_t N,
+                                                       const float* __restrict__ qn) {
   __shared__ float dl[V4_CAP];
   __shared__ float cd[V4_SCAP];
   __shared__ int ci[V4_SCAP];
   __shared__ int cnt;
+  static_assert(V4_CAP >= 2 * B4_T, "exact fallback lists live in dl");
   const int64_t qq = blockIdx.x;
+  auto fail = [&]() {
+    if constexpr (SMP) {
+      if (threadIdx.x == 0) qcnt[qq] = 0;   // pass 2 runs under the 512-row bound
+    } else {
+      __syncthreads();   // (dl is reused)
+      exact_query_topk<DV>(tab, inv, N, qn + qq * DV * 4, k, dl, idx + qq * k, dist + qq * k);
+    }
+  };
   const int n = qcnt[qq];
-  if (n > V4_CAP || n < k) {   // overflow (fewer than k admitted rows cannot happen
-    if (threadIdx.x == 0) *flag = 1;   // when N >= k; kept as a guard)
+  if (n > V4_CAP || n < k) {   // overflow (fewer than k admitted rows only when N < k)
+    fail();
     return;
   }
   if (threadIdx.x == 0) cnt = 0;
@@ -943,8 +1034,8 @@ __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__
     }
   __syncthreads();
   const int nv = cnt;
-  if (nv > V4_SCAP) {   // too many rows share the k-th bin: exact fallback
-    if (threadIdx.x == 0) *flag = 1;
+  if (nv > V4_SCAP) {   // too many rows share the k-th bin
+    fail();
     return;
   }
   int n2 = 2;
@@ -976,8 +1067,7 @@ constexpr int FT = 24;   // fast path: candidates loaded per thread per round
 // stage writes idx / dist.
 __global__ __launch_bounds__(NT) void merge_kernel(const Cand* in, int nslices, int k,
                                                    int64_t* idx, float* dist, int groups,
-                                                   Cand* gout, const int* gate = nullptr) {
-  if (gate && *gate == 0) return;
+                                                   Cand* gout) {
   __shared__ float cd[CAP];
   __shared__ int ci[CAP];
   __shared__ int cnt;
@@ -1274,7 +1364,7 @@ bool use_v4(int64_t N, int64_t Q, int d, int k) {
 }
 
 // v4 scratch after the v2 layout (cands | qn [Q][d] | thr0 [Q]): bf16
-// queries [Q][d] | per-query counts [Q] | flag | admitted rows [Q][V4_CAP]
+// queries [Q][d] | per-query counts [Q] | admitted rows [Q][V4_CAP]
 // | their exact distances [Q][V4_CAP]
 size_t v4_extra(int64_t Q, int d) {
   return rup((size_t)Q * d * 2, 256) + rup((size_t)Q * 4 + 4, 256) + 2 * (size_t)Q * V4_CAP * 4 + 256;
@@ -1297,9 +1387,9 @@ size_t topk_ws_d(int64_t N, int64_t Q, int k, int d) {
 // one-shot 8192-entry bitonic sort by 1024 threads 107 us; a per-wave register
 // merge 50 us -- the block barriers of a one-block kernel dominate all of them.
 dcnr_status merge_lists(const Cand* cands, int64_t Q, int ns, int k, int64_t* idx, float* dist,
-                        hipStream_t s, const int* gate = nullptr) {
+                        hipStream_t s) {
   hipLaunchKernelGGL(merge_kernel, dim3((unsigned)Q), dim3(NT), 0, s, cands, ns, k, idx, dist, 1,
-                     nullptr, gate);
+                     nullptr);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
@@ -1334,24 +1424,23 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
     float* thr0 = qn + Q * d;
     const bool v4 = use_v4(N, Q, d, k);
     bf16* qb = nullptr;
-    int *qcnt = nullptr, *gate = nullptr, *rows = nullptr;   // v4 scratch
+    int *qcnt = nullptr, *rows = nullptr;   // v4 scratch
     float* dists = nullptr;
     if (v4) {
       char* x = (char*)ws + rup(rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4, 256);
       qb = (bf16*)x;
       x += rup((size_t)Q * d * 2, 256);
       qcnt = (int*)x;
-      gate = qcnt + Q;   // v4: the exact scan v3 below runs only if v4 overflowed
       x += rup((size_t)Q * 4 + 4, 256);
       rows = (int*)x;
       dists = (float*)(rows + Q * V4_CAP);
     }
-    {   // (v4: also its bf16 queries, zeroed list counts and gate)
+    {   // (v4: also its bf16 queries and zeroed list counts)
       switch (d / 4) {
 #define CASEK(n)                                                                           \
   case n:                                                                                  \
     hipLaunchKernelGGL(kth_bound_kernel<n>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, \
-                       q, qn, k, thr0, qb, qcnt, gate);                                    \
+                       q, qn, k, thr0, qb, qcnt);                                          \
     break;
         CASEK(1) CASEK(2) CASEK(3) CASEK(4) CASEK(5) CASEK(6) CASEK(7) CASEK(8)
         CASEK(9) CASEK(10) CASEK(11) CASEK(12) CASEK(13) CASEK(14) CASEK(15) CASEK(16)
@@ -1372,7 +1461,7 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       const dim3 g4((unsigned)cdiv(N, rpb), (unsigned)cdiv(Q, NQ * 16));
 #define SCAN4(ks, nq, pk, g, n, rp)                                                                    \
   hipLaunchKernelGGL((scan4_kernel<ks, nq, pk>), g, dim3(256), 0, s, t, inv, tb, n, rp, qb, thr0, qn, \
-                     Q, qcnt, rows, dists, gate)
+                     Q, qcnt, rows, dists)
 #define CASE4(ks, nq, sel, g, n, rp)                                  \
   if (d == 32 * ks && sel == nq) {                                    \
     if (tb) SCAN4(ks, nq, true, g, n, rp);                            \
@@ -1388,23 +1477,26 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       CASES4(NQS, gs, NS, RPB_S)
       DCNR_LAUNCH_CHECK();
       if (NS < N) {
-        hipLaunchKernelGGL((rescore_kernel<true>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k,
-                           nullptr, nullptr, gate, thr0);
+        hipLaunchKernelGGL((rescore_kernel<true, 0>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows,
+                           k, nullptr, nullptr, thr0, t, inv, N, qn);
         DCNR_LAUNCH_CHECK();
         CASES4(NQ, g4, N, rpb)
         DCNR_LAUNCH_CHECK();
       }
       // (a table of at most V4_S rows: pass 1 covered every row under a valid
       // bound, so its lists already hold the answer)
-      hipLaunchKernelGGL((rescore_kernel<false>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k,
-                         idx, dist, gate, nullptr);
+      // (a query whose list overflowed scans the table exactly in its block)
+      if (d == 32)
+        hipLaunchKernelGGL((rescore_kernel<false, 8>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows,
+                           k, idx, dist, nullptr, t, inv, N, qn);
+      else
+        hipLaunchKernelGGL((rescore_kernel<false, 16>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows,
+                           k, idx, dist, nullptr, t, inv, N, qn);
       DCNR_LAUNCH_CHECK();
 #undef CASES4
 #undef CASE4
 #undef SCAN4
-      // (the exact fallback below admits rows under the same thr0: an upper
-      // bound on every query's k-th best -- the sample's, or the 512-row one
-      // if pass 1 overflowed)
+      return DCNR_OK;
     }
     if (!v4 && Q >= MFMA_MIN_Q && d % 16 == 0) {
       const int qtiles = (int)cdiv(Q, K3_QT);
@@ -1413,31 +1505,30 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
 #define CASE3(n)                                                                                   \
   case n:                                                                                          \
     hipLaunchKernelGGL(scan3_kernel<4 * n>, dim3((unsigned)blocks), dim3(K2_NT), 0, s, t, inv, N,  \
-                       qn, Q, k, rps, ns, qtiles, cands, thr0, gate);                              \
+                       qn, Q, k, rps, ns, qtiles, cands, thr0);                              \
     break;
         CASE3(1) CASE3(2) CASE3(3) CASE3(4)
 #undef CASE3
       }
       DCNR_LAUNCH_CHECK();
-      return merge_lists(cands, Q, ns, k, idx, dist, s, gate);
+      return merge_lists(cands, Q, ns, k, idx, dist, s);
     }
-    // scan v2: the exact VALU scan -- and, gated, v4's fallback when a list
-    // overflowed (the same distance arithmetic as v4's rescoring, so a batch
-    // that falls back still returns what v4 or v2 alone would)
+    // scan v2: the exact VALU scan (the same distance arithmetic as v4's
+    // rescoring and its per-query fallback)
     const int qtiles = (int)cdiv(Q, K2_QT);
     const int64_t blocks = rup(ns, 8) * qtiles;
     switch (d / 4) {
 #define CASE(n)                                                                                  \
   case n:                                                                                        \
     hipLaunchKernelGGL(scan2_kernel<n>, dim3((unsigned)blocks), dim3(K2_NT), 0, s, t, inv, N, qn, \
-                       Q, k, rps, ns, qtiles, cands, thr0, gate);                                \
+                       Q, k, rps, ns, qtiles, cands, thr0);                                \
     break;
       CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8)
       CASE(9) CASE(10) CASE(11) CASE(12) CASE(13) CASE(14) CASE(15) CASE(16)
 #undef CASE
     }
     DCNR_LAUNCH_CHECK();
-    return merge_lists(cands, Q, ns, k, idx, dist, s, gate);
+    return merge_lists(cands, Q, ns, k, idx, dist, s);
   }
   plan(N, Q, k, &ns, &rps);
   dim3 grid(ns, (unsigned)cdiv(Q, QT));

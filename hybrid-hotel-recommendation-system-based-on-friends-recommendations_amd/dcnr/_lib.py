@@ -22,6 +22,7 @@ PREC_FP32, PREC_BF16 = 0, 1
 EVAL, TRAIN = 0, 1
 FLAG_CHECK_INDICES = 1
 FLAG_KEEP_INTERMEDIATES = 2
+FLAG_FUSED_TOWER = 4
 # dcnr_ws_tensor (include/dcnr.h)
 WS_KINDS = ["x0", "h", "t1", "t2", "a1", "mask_a1", "mask_h", "bn_mean", "bn_invstd", "bn_scale",
             "bn_shift", "du", "dt2", "da", "dt1", "G", "dx0", "zc", "xcoef", "sc"]

@@ -186,6 +186,7 @@ class DCN_RecSys(nn.Module):
                           n_cross=n_cross_layers, n_res=n_res_blocks, dropout=float(dropout),
                           input_dim=input_dim)
         self.keep_intermediates = False   # tests: per-block backward buffers (stage checks)
+        self.fused_tower = False   # bf16 eval: fused tower at every batch size (default: B >= 16384)
         self.bn_allreduce = None   # set by dcnr.parallel for SyncBN
         self._sync_bn_hook = None
         self._active_ws = None
@@ -209,7 +210,8 @@ class DCN_RecSys(nn.Module):
         desc.dropout = d['dropout']
         desc.precision = _PRECISIONS[self.precision]
         desc.flags = (_lib.FLAG_CHECK_INDICES if self.check_indices else 0) | \
-            (_lib.FLAG_KEEP_INTERMEDIATES if getattr(self, 'keep_intermediates', False) else 0)
+            (_lib.FLAG_KEEP_INTERMEDIATES if getattr(self, 'keep_intermediates', False) else 0) | \
+            (_lib.FLAG_FUSED_TOWER if getattr(self, 'fused_tower', False) else 0)
         if self.bn_allreduce is not None:
             desc.bn_allreduce = self.bn_allreduce
         if grad_ready is not None:

@@ -100,6 +100,12 @@ typedef enum { DCNR_EVAL = 0, DCNR_TRAIN = 1 } dcnr_mode;
  * train forward does not store h_R (the backward rebuilds it from t2 and
  * h_{R-1}), so DCNR_WS_H at index R is only meaningful with this flag. */
 #define DCNR_FLAG_KEEP_INTERMEDIATES 2u
+/* bf16 eval forward: take the fused deep tower (one persistent launch, the
+ * activations on chip) at any batch size it supports.  Without the flag it
+ * is taken from 16384 samples on, where it overtakes the layer-by-layer path;
+ * below that the layer path is faster (the tower walks a tile's layers in
+ * sequence on one CU).  Same results either way up to bf16 rounding order. */
+#define DCNR_FLAG_FUSED_TOWER 4u
 
 /* Optional collective hook for SyncBN across data-parallel ranks: called
  * (stream-ordered, from the calling thread) with a device buffer of `count`

@@ -46,10 +46,11 @@ def _model(cfg, dev):
     return m.to(dev).eval()
 
 
-def _eval_logits(m, inp, dev, keep):
+def _eval_logits(m, inp, dev, keep, tower=None):
     u, i, c, n, _ = inp
     t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
     m.keep_intermediates = keep
+    m.fused_tower = (not keep) if tower is None else tower   # the tower at every batch size
     with torch.no_grad():
         z = m(t(u), t(i), t(c), t(n))
     torch.cuda.synchronize()
@@ -94,3 +95,26 @@ def test_eval_tower_chunked_launch(dev):
         part = tuple(a[lo:lo + 5000] for a in inp)
         assert np.array_equal(_eval_logits(m, part, dev, keep=False), z[lo:lo + 5000])
     assert np.isfinite(z).all()
+
+
+def test_eval_tower_batch_threshold(dev):
+    """Without DCNR_FLAG_FUSED_TOWER the bf16 eval forward launches the fused
+    tower from 16384 samples on (dcnr_api.hip TOWER_MIN_B: below it the
+    layer-by-layer path is faster) -- counted by the library's per-class
+    launch profiler -- and its logits there equal the forced tower's bit
+    for bit."""
+    from dcnr import _lib
+    cfg = gc.CFG3R
+    m = _model(cfg, dev)
+    for B, want in ((16383, 0), (16384, 1)):
+        inp = gc.make_inputs(cfg, B, 13)
+        _lib.profile_enable(True)
+        _lib.profile_collect()
+        try:
+            z_default = _eval_logits(m, inp, dev, keep=False, tower=False)
+            launches = _lib.profile_collect()["tower"][1]
+        finally:
+            _lib.profile_enable(False)
+        assert launches == want, (B, launches)
+        if want:
+            assert np.array_equal(z_default, _eval_logits(m, inp, dev, keep=False, tower=True))

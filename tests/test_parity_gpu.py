@@ -563,15 +563,18 @@ def test_cosine_knn_v2_v4_same_answer(dev, N, d):
         assert torch.equal(i1[0], i40[r]) and torch.equal(d1[0], d40[r]), r
 
 
-def test_cosine_knn_v4_overflow_falls_back_exact(dev):
+@pytest.mark.parametrize("Q,dim", [(32, 64), (256, 64), (40, 32)])
+def test_cosine_knn_v4_overflow_falls_back_exact(dev, Q, dim):
     """More than V4_CAP rows inside one query's admission bound (12000 rows
     on the query's own direction, every one at distance 0): scan v4's list
-    overflows, its flag gates the exact scan v3 + merge, and the result is
-    the exact top-k, ties by row index (the duplicates' lowest rows)."""
+    overflows and that query is answered by the exact per-query scan inside
+    its rescore block (knn.hip exact_query_topk): the exact top-k, ties by
+    row index (the duplicates' lowest rows); every other query of the batch
+    keeps the v4 answer, checked against torch fp32."""
     import dcnr
-    g = torch.Generator(device=dev).manual_seed(5)
-    table = torch.randn(200_000, 64, device=dev, generator=g)
-    q = torch.randn(32, 64, device=dev, generator=g)
+    g = torch.Generator(device=dev).manual_seed(5 + Q + dim)
+    table = torch.randn(200_000, dim, device=dev, generator=g)
+    q = torch.randn(Q, dim, device=dev, generator=g)
     dup = torch.randperm(200_000, device=dev, generator=g)[:12000]
     table[dup] = q[0] * 2.0
     nn_ = dcnr.NearestNeighbors(metric="cosine", algorithm="brute").fit(table)
@@ -583,7 +586,7 @@ def test_cosine_knn_v4_overflow_falls_back_exact(dev):
     ref_d, ref_i = torch.topk(1.0 - qn @ tn.T, 11, dim=1, largest=False)
     ref_d, ref_i = ref_d.cpu().numpy(), ref_i.cpu().numpy()
     np.testing.assert_allclose(d[1:], ref_d[1:], rtol=0, atol=2e-6)
-    for r in range(1, 32):
+    for r in range(1, Q):
         near = np.diff(ref_d[r]) <= 2e-6
         isolated = np.ones(11, bool)
         isolated[1:] &= ~near

@@ -24,6 +24,7 @@ for B in [int(x) for x in (sys.argv[1:] or ["200", "4096", "131072"])]:
     u, i, c, n, _ = [torch.from_numpy(np.ascontiguousarray(a)).to(dev) for a in gc.make_inputs(cfg, B, 1)]
     for keep in (False, True):
         m.keep_intermediates = keep
+        m.fused_tower = not keep
         with torch.no_grad():
             for _ in range(5):
                 z = m(u, i, c, n)
