@@ -980,11 +980,34 @@ dcnr_status dcnr_gather_cross(const dcnr_model_desc* desc, void* const* params,
   return DCNR_OK;
 }
 
+static dcnr_status forward_body(const dcnr_model_desc* desc, void* const* params,
+                                const int64_t* user_ids, const int64_t* item_ids,
+                                const int64_t* cat_features, const float* num_features, int64_t B,
+                                int mode, uint64_t dropout_seed, float* logits, void* ws,
+                                size_t ws_bytes, dcnr_stream_t stream, bool* mirrored);
+
 dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
                          const int64_t* user_ids, const int64_t* item_ids,
                          const int64_t* cat_features, const float* num_features, int64_t B,
                          int mode, uint64_t dropout_seed, float* logits, void* ws,
                          size_t ws_bytes, dcnr_stream_t stream) {
+  bool mirrored = false;
+  TRY(forward_body(desc, params, user_ids, item_ids, cat_features, num_features, B, mode, dropout_seed,
+                   logits, ws, ws_bytes, stream, &mirrored));
+  // the id-check word to the caller's mirror (the fused eval tower stores it
+  // itself); after the forward's last kernel on the stream
+  if (B > 0 && !mirrored && desc->error_mirror && (desc->flags & DCNR_FLAG_CHECK_INDICES)) {
+    hipStream_t s = (hipStream_t)stream;
+    TRYP(DCNR_K_PACK, mirror_word((const int*)ws, desc->error_mirror, s));
+  }
+  return DCNR_OK;
+}
+
+static dcnr_status forward_body(const dcnr_model_desc* desc, void* const* params,
+                                const int64_t* user_ids, const int64_t* item_ids,
+                                const int64_t* cat_features, const float* num_features, int64_t B,
+                                int mode, uint64_t dropout_seed, float* logits, void* ws,
+                                size_t ws_bytes, dcnr_stream_t stream, bool* mirrored) {
   Dims d;
   TRY(make_dims(desc, &d));
   hipStream_t s = (hipStream_t)stream;
@@ -1035,6 +1058,9 @@ dcnr_status dcnr_forward(const dcnr_model_desc* desc, void* const* params,
     memset(&ta, 0, sizeof(ta));
     ta.x0 = (const bf16*)L.x0; ta.ldx = d.Dp; ta.M = B; ta.Dp = d.Dp; ta.H = d.H; ta.R = d.R;
     ta.wp = L.twp; ta.zc = L.zc; ta.bias = P.bf; ta.logits = logits;
+    ta.err = L.err;
+    ta.err_mirror = check ? desc->error_mirror : nullptr;
+    *mirrored = true;
     // algorithmic bytes: the x0 rows + zc in, the logits out (the packed
     // weights are L2-resident: every CU streams the same 4.7 MB)
     TRYB(DCNR_K_TOWER, (double)B * (d.Dp * d.es + 8.0), eval_tower(ta, s));

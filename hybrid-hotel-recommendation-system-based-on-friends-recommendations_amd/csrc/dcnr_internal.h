@@ -408,6 +408,7 @@ struct TowerArgs {
   const char* wp; int64_t wp_bytes;          // tower_pack's output
   const float* zc; const float* bias;        // cross half of the head [M], final_linear.bias
   float* logits;
+  const int* err; int* err_mirror;           // the call's error word -> its mirror (may be null)
   int ntiles;                                // (set by eval_tower)
 };
 bool tower_supported(int Dp, int H, int R);
@@ -630,6 +631,8 @@ dcnr_status mmr_rerank(const float* table, const float* inv, int d, const int64_
                        int32_t* out_count, hipStream_t s);
 
 dcnr_status fill_zero(void* p, size_t bytes, hipStream_t s);
+// *dst = *src with a system-scope store (dst may be pinned host memory)
+dcnr_status mirror_word(const int* src, int* dst, hipStream_t s);
 dcnr_status fill_zero_multi(int n, void* const* ptrs, const int64_t* bytes, hipStream_t s);
 
 }  // namespace dcnr

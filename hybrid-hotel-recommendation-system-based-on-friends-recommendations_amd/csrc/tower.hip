@@ -107,18 +107,24 @@ __global__ __launch_bounds__(256) void tower_pack_kernel(TowerPack p) {
     int K;
     if (l == 0) { W = p.W0; K = p.D; }
     else { W = (l & 1) ? p.w1[(l - 1) / 2] : p.w2[(l - 1) / 2]; K = H; }
+    // elements j = 0..3 and 4..7 are two runs of 4 consecutive k: two 16-B
+    // loads where the row allows (K % 4 == 0, whole run inside the row)
+    float v[8];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int kh = l == 0 ? 32 * kt + 8 * g + 4 * h : 32 * kt + 16 * h + 4 * g;
+      const float* src = W + (int64_t)o * K + kh;
+      if (o < H && kh + 4 <= K && (K & 3) == 0) {
+        const float4 f = *reinterpret_cast<const float4*>(src);
+        v[4 * h] = f.x; v[4 * h + 1] = f.y; v[4 * h + 2] = f.z; v[4 * h + 3] = f.w;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[4 * h + e] = (o < H && kh + e < K) ? src[e] : 0.f;
+      }
+    }
     uint32_t w[4];
 #pragma unroll
-    for (int j2 = 0; j2 < 4; ++j2) {
-      float v[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int j = 2 * j2 + e;
-        const int k = l == 0 ? 32 * kt + 8 * g + j : 32 * kt + 16 * (j >> 2) + 4 * g + (j & 3);
-        v[e] = (o < H && k < K) ? W[(int64_t)o * K + k] : 0.f;
-      }
-      w[j2] = pk2(v[0], v[1]);
-    }
+    for (int j2 = 0; j2 < 4; ++j2) w[j2] = pk2(v[2 * j2], v[2 * j2 + 1]);
     char* dst = p.out + tw_slice_off(l, ch, nch, nkt) + ((int64_t)ob * kt_n + kt) * 1024 + lane * 16;
     *reinterpret_cast<u32x4*>(dst) = u32x4{w[0], w[1], w[2], w[3]};
     return;
@@ -322,6 +328,10 @@ __global__ __launch_bounds__(TW_NT, 1) void tower_kernel(TowerArgs a) {
       asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     issue_begin();
   };
+  // the call's id-check word (the gather before this launch set it) to its
+  // mirror, e.g. pinned host memory: no copy of its own on the stream
+  if (a.err_mirror && blockIdx.x == 0 && tid == 0)
+    __hip_atomic_store(a.err_mirror, *a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   for (int f = tid; f < NKT * 32; f += TW_NT)
     wf_s[f] = reinterpret_cast<const float*>(a.wp + tw_slice_off(2 * a.R + 1, 0, NCH, NKT))[f];
   for (int p = 0; p < TW_NSLOT - 1; ++p) issue();

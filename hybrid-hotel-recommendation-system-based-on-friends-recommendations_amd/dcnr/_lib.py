@@ -53,6 +53,7 @@ class ModelDesc(ctypes.Structure):
         ("bn_allreduce_ctx", ctypes.c_void_p),
         ("grad_ready", GRAD_READY_FN),
         ("grad_ready_ctx", ctypes.c_void_p),
+        ("error_mirror", ctypes.c_void_p),
     ]
 
 
@@ -161,7 +162,7 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.dcnr_abi_version() != 2:
+        if lib.dcnr_abi_version() != 3:
             raise LibraryMissing("libdcnr ABI version mismatch")
         if path is None:
             _lib = lib

@@ -24,6 +24,7 @@ from __future__ import annotations
 
 import ctypes
 import threading
+import time
 from typing import Any, Dict, List, Optional
 
 import numpy as np
@@ -98,18 +99,54 @@ def dropout_seed(dev: torch.device, advance: bool = True) -> int:
 
 
 class IndexErrorWatch:
-    """Deferred id checks: the device error word of each call is copied into
-    a pinned ring slot after the call (stream-ordered, no host wait) and
-    polled without blocking; a set word raises IndexError.  Thread-safe:
-    the serving path scores from Starlette's threadpool (main.py:306-307 is
-    a sync ``def``), so slot assignment and polling hold a lock."""
-    RING = 8
+    """Deferred id checks: the error word of each call lands in a slot of a
+    pinned host ring -- stored there by the forward's last kernel
+    (``reserve`` / ``commit``: the slot is the call's ``error_mirror``), or
+    copied after the call (``push``) -- stream-ordered, with no event and no
+    host wait.  A slot holds PENDING (-1, set by the host before the call)
+    until the device's word arrives: 0 = every id in range, else the next
+    poll raises IndexError.  Thread-safe: the serving path scores from
+    Starlette's threadpool (main.py:306-307 is a sync ``def``), so slot
+    assignment and polling hold a lock."""
+    RING = 64
+    DEPTH = 8      # calls in flight before the oldest is waited for
+    PENDING = -1
 
     def __init__(self):
         self.ring = None
         self.pending = []
-        self.next = 0
+        self.free = list(range(self.RING))
         self.lock = threading.Lock()
+
+    def _slot(self):
+        if self.ring is None:
+            self.ring = torch.zeros(self.RING, dtype=torch.int32, pin_memory=True)
+            self.view = self.ring.numpy()   # host view of the pinned words
+        if len(self.pending) >= self.DEPTH:
+            self._poll(oldest=True)
+        if not self.free:
+            return None
+        slot = self.free.pop(0)
+        self.view[slot] = self.PENDING
+        return slot
+
+    def reserve(self):
+        """A free ring slot and its address (for dcnr_model_desc.error_mirror),
+        or (None, None) when every slot is taken."""
+        with self.lock:
+            slot = self._slot()
+        if slot is None:
+            return None, None
+        return slot, self.ring.data_ptr() + 4 * slot
+
+    def commit(self, slot):
+        """The call that got ``slot`` is enqueued: watch its word."""
+        with self.lock:
+            self.pending.append(slot)
+
+    def cancel(self, slot):
+        with self.lock:
+            self.free.append(slot)
 
     # copies (deepcopy / pickle of the model) start with an empty watch
     def __getstate__(self):
@@ -119,31 +156,41 @@ class IndexErrorWatch:
         self.__init__()
 
     def push(self, word: torch.Tensor):
+        """Copy a device error word into a ring slot (stream-ordered)."""
         with self.lock:
-            if self.ring is None:
-                self.ring = torch.zeros(self.RING, dtype=torch.int32, pin_memory=True)
-            if len(self.pending) == self.RING:
-                self._poll(oldest=True)
-            slot = self.next
-            self.next = (slot + 1) % self.RING
-            self.ring[slot:slot + 1].copy_(word.view(torch.int32)[:1], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            self.pending.append((ev, slot))
+            slot = self._slot()
+            if slot is not None:
+                self.ring[slot:slot + 1].copy_(word.view(torch.int32)[:1], non_blocking=True)
+                self.pending.append(slot)
+                return
+        # every slot held by calls still being enqueued: check this one now
+        if int(word.view(torch.int32)[0]) != 0:
+            raise IndexError("index out of range in self")
 
     def poll(self, oldest=False, all_=False):
         with self.lock:
             self._poll(oldest, all_)
 
+    def _wait(self, slot):
+        while int(self.view[slot]) == self.PENDING:
+            time.sleep(20e-6)
+
     def _poll(self, oldest=False, all_=False):
         keep = []
-        for n, (ev, slot) in enumerate(self.pending):
+        for n, slot in enumerate(self.pending):
             if all_ or (oldest and n == 0):
-                ev.synchronize()
-            elif not ev.query():
-                keep.append((ev, slot))
+                self._wait(slot)
+            elif int(self.view[slot]) == self.PENDING:
+                keep.append(slot)
                 continue
-            if int(self.ring[slot]) != 0:
+            bad = int(self.view[slot]) != 0
+            self.free.append(slot)
+            if bad:
+                # the other words are dropped; their slots return to the ring
+                # once nothing can still write them
+                for sl in keep + self.pending[n + 1:]:
+                    if int(self.view[sl]) != self.PENDING:
+                        self.free.append(sl)
                 self.pending = []
                 raise IndexError("index out of range in self (ids passed to an earlier call)")
         self.pending = keep
@@ -465,18 +512,30 @@ def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
     logits = torch.empty(B, dtype=torch.float32, device=dev)
     state = model.state_ptr_array()
     desc = model.desc()
+    # deferred id check: the forward's last kernel stores the error word in a
+    # pinned ring slot (no copy on the stream)
+    slot = None
+    if model.check_indices and model.check_indices != "sync" and B > 0:
+        slot, mirror = model._index_watch.reserve()
+        if slot is not None:
+            desc.error_mirror = mirror
     model._active_ws = ws          # the SyncBN hook (dcnr.parallel) maps pointers into it
     st = lib.dcnr_forward(ctypes.byref(desc), state, user.data_ptr(), item.data_ptr(),
                           cat.data_ptr() if cat.numel() else None,
                           num.data_ptr() if num.numel() else None, B, mode, seed,
                           logits.data_ptr(), ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev))
     model._active_ws = None
+    if slot is not None:
+        if st == 0:
+            model._index_watch.commit(slot)
+        else:
+            model._index_watch.cancel(slot)
     _hook_error(model)
     _lib.check(st, "dcnr_forward")
     if model.check_indices == "sync":
         _lib.check(lib.dcnr_check_errors(ws.data_ptr(), ws.numel(), _lib.stream_ptr(dev)),
                    "embedding")
-    elif model.check_indices:
+    elif model.check_indices and slot is None and B > 0:
         model._index_watch.push(ws[:4])
     return logits, ws
 

@@ -73,7 +73,7 @@
 extern "C" {
 #endif
 
-#define DCNR_ABI_VERSION 2
+#define DCNR_ABI_VERSION 3
 
 typedef void* dcnr_stream_t; /* hipStream_t */
 
@@ -144,6 +144,12 @@ typedef struct {
   void* bn_allreduce_ctx;
   dcnr_grad_ready_fn grad_ready;  /* gradient-group hook or NULL (ABI 2) */
   void* grad_ready_ctx;
+  /* ABI 3.  With DCNR_FLAG_CHECK_INDICES: where dcnr_forward's last kernel
+   * stores the call's index-error word (0 = every id in range), e.g. a slot
+   * of pinned host memory the caller polls once an event recorded after the
+   * call has completed -- no copy of its own on the stream.  NULL: the word
+   * stays in the workspace (dcnr_check_errors / a caller's copy). */
+  int32_t* error_mirror;
 } dcnr_model_desc;
 
 int dcnr_abi_version(void);

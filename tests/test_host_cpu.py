@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(lib, s), f"libdcnr.so does not export {s}"
     assert sorted(_lib.exported_symbols()) == syms
-    assert lib.dcnr_abi_version() == 2
+    assert lib.dcnr_abi_version() == 3
 
 
 def test_input_dim_and_workspace_queries():
