@@ -118,3 +118,56 @@ def test_eval_tower_batch_threshold(dev):
         assert launches == want, (B, launches)
         if want:
             assert np.array_equal(z_default, _eval_logits(m, inp, dev, keep=False, tower=True))
+
+
+@pytest.mark.parametrize("col", ["user", "item", "cat", "neg"])
+def test_eval_tower_index_check(dev, col):
+    """An out-of-range id in a fused-tower eval call raises IndexError --
+    deferred (the tower launch stores the call's error word into the pinned
+    ring slot the call reserved: no copy, no event) and with
+    check_indices="sync" -- and a clean call afterwards raises nothing."""
+    cfg = gc.CFG3R
+    m = _model(cfg, dev)
+    m.fused_tower = True
+    u, i, c, n, _ = gc.make_inputs(cfg, 300, 21)
+    u, i, c = u.copy(), i.copy(), c.copy()
+    if col == "user":
+        u[7] = cfg["n_users"]
+    elif col == "item":
+        i[290] = cfg["n_items"] + 5
+    elif col == "cat":
+        c[100, 11] = 1000
+    else:
+        u[0] = -1
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)   # noqa: E731
+    with torch.no_grad(), pytest.raises(IndexError):
+        m(t(u), t(i), t(c), t(n))
+        m.check_index_errors()
+    m.check_indices = "sync"
+    with torch.no_grad(), pytest.raises(IndexError):
+        m(t(u), t(i), t(c), t(n))
+    m.check_indices = True
+    with torch.no_grad():
+        for _ in range(20):   # past the ring's in-flight depth: slots recycle
+            m(t(u * 0), t(i * 0), t(c * 0), t(n))
+        m.check_index_errors()
+
+
+def test_eval_tower_other_widths(dev):
+    """CFG3R with one categorical table widened to 40 / 35 columns (x0 groups
+    no longer at multiples of 32): the tower against the layer-by-layer path,
+    run to run, and against the fp64 oracle."""
+    for card in (1599, 1224):   # int(sqrt(n)) + 1 = 40 / 35
+        cfg = dict(gc.CFG3R)
+        cats = dict(cfg["cat_dims"])
+        cats["c0"] = card
+        cfg["cat_dims"] = cats
+        m = _model(cfg, dev)
+        B = 20000
+        inp = gc.make_inputs(cfg, B, 31)
+        zf = _eval_logits(m, inp, dev, keep=False)
+        zk = _eval_logits(m, inp, dev, keep=True)
+        scale = max(1.0, float(np.abs(zk).max()))
+        assert np.abs(zf - zk).max() / scale < 2e-3, card
+        assert np.array_equal(_eval_logits(m, inp, dev, keep=False), zf)
+        _oracle_check(m, cfg, inp, zf, B)
