@@ -20,4 +20,5 @@ python3 tools/stats_summary.py $OUT/trace/run_kernel_stats.csv \
 python3 tools/pmc_traffic.py $OUT/fetch/run_counter_collection.csv $OUT/write/run_counter_collection.csv \
     --json $OUT/pmc_traffic.json > $OUT/pmc_traffic.txt &&
 python3 tools/trace_passes.py $OUT/trace/run_kernel_trace.csv gemm_dw_kernel --per-step 9 \
-    --warmup 5 --steps 20 > $OUT/gemm_dw_passes.txt
+    --warmup 5 --steps 20 > $OUT/gemm_dw_passes.txt &&
+python3 tools/step_timeline.py $OUT/trace/run_kernel_trace.csv --step 12 --all > $OUT/step_timeline.txt
