@@ -283,6 +283,29 @@ def test_index_out_of_range_raises(dev):
         m(*to_dev(dev, u, i, c, n))
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_index_out_of_range_raises_train(dev, precision):
+    """Train mode: FusedTrainer's step with an out-of-range id raises
+    IndexError through the deferred check (the forward's error word stored
+    into the pinned ring slot by the one-wave mirror kernel after its last
+    launch); steps with valid ids afterwards (past the ring's in-flight
+    depth, so slots recycle) raise nothing."""
+    import dcnr
+    cfg = gc.CFG3R
+    m = our_model(cfg, precision).to(dev)
+    t = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, optimizer_name="AdamW")
+    u, i, c, n, y = gc.make_inputs(cfg, 512, 77)
+    c = c.copy()
+    c[5, 3] = 1000   # one past the end of a 1000-row categorical table
+    with pytest.raises(IndexError):
+        t.step(*to_dev(dev, u, i, c, n, y))
+        t.check_indices()
+    c[5, 3] = 0
+    for _ in range(12):
+        t.step(*to_dev(dev, u, i, c, n, y))
+    t.check_indices()
+
+
 def test_backward_deterministic(dev):
     """Two backward passes on the same state and batch are bit-identical for
     EVERY gradient, the embedding tables included (csrc/embed_bwd.hip)."""
