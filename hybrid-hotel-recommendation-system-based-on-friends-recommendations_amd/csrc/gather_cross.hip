@@ -524,9 +524,12 @@ dcnr_status launch_fwd(const GatherDesc& g, const CrossParams& cp, const int64_t
 
 constexpr int GC_V4_SPW = 4;   // samples per wave-tile
 // waves per launch (measured, same box, tools/ab_variants.sh): writing x0
-// (train / eval forward) 3072 (2048: +20 %, 6144: +12 % kernel time); the
-// gather + cross front alone (configs[1]) 2048 (+6 % pairs/s over 3072)
-constexpr int GC_V4_WAVES = 3072, GC_V4_WAVES_NOX0 = 2048;
+// (train / eval forward) 4096 -- every wave resident at 4 per SIMD (104
+// VGPRs) -- (round 4, tools/gather_probe.py, profiles/lab/r04q_gather_waves_ab.txt:
+// train 84.0 vs 88.7 us, eval 61.8 vs 63.4 at 3072; 2560: 103.6 / 69.1;
+// earlier: 2048 +20 %, 6144 +12 % kernel time); the gather + cross front
+// alone (configs[1]) 2048 (+6 % pairs/s over 3072)
+constexpr int GC_V4_WAVES = 4096, GC_V4_WAVES_NOX0 = 2048;
 
 template <int R4, int X0BF16>
 dcnr_status launch_v4(const GatherDesc& g, const CrossParams& cp, const int64_t* user,
