@@ -328,6 +328,7 @@ bool masks_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && d.Hp % 32 == 0
 int dq_of(const Dims& d) { return (int)rup(d.Dp, 32); }
 bool keep_of(const dcnr_model_desc* desc) { return (desc->flags & DCNR_FLAG_KEEP_INTERMEDIATES) != 0; }
 
+
 // bf16 train: the last block's head pass does not store h_R; the backward's
 // BN2 statistics pass rebuilds it from t2, h_{R-1} and the BN2 affine
 // (KEEP_INTERMEDIATES still stores it for the stage tests)
@@ -443,19 +444,24 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, uint32_t flags 
       L.emb.tmp_bytes = emb_sort_tmp_bytes(d.rows, d.widths, 2 + d.K, B);
       L.emb.tmp = b.take(L.emb.tmp_bytes);
     }
-    // the backward's dt2 / dt1 buffers alternate between two sets by block
-    // parity, so a main-stream writer of one never waits for the side
-    // stream's weight-gradient GEMM of the block just before
-    if (!keep && d.prec == DCNR_PREC_BF16 && d.R > 1) {
+    // bf16: every residual block has its own dt2 / dt1 buffers (blocks 0
+    // and 1 take the shared set and dt2b / dt1b): the side stream's
+    // weight-gradient GEMMs read them while the main stream goes on, and the
+    // main stream never waits for the side stream inside the backward
+    // (4.029-4.044 vs 4.068-4.075 ms per step with two sets alternating by
+    // block parity and a wait for call n-3, same box, profiles/lab/r04s_dt_per_block_ab.txt;
+    // +0.54 GB of workspace at the bench shape)
+    const bool own_dt = !keep && d.prec == DCNR_PREC_BF16 && d.R > 1;
+    if (own_dt) {
       L.dt2b = b.take(act);
       L.dt1b = b.take(act);
     }
     for (int j = 0; j < d.R; ++j) {
-      const bool odd = (j & 1) && L.dt2b;
+      const bool fresh = own_dt && j > 1;
       L.duk[j] = keep ? b.take(act) : L.du;
-      L.dt2k[j] = keep ? b.take(act) : odd ? L.dt2b : L.dt2;
+      L.dt2k[j] = keep || fresh ? b.take(act) : own_dt && j == 1 ? L.dt2b : L.dt2;
       L.dak[j] = keep ? b.take(act) : L.da;
-      L.dt1k[j] = keep ? b.take(act) : odd ? L.dt1b : L.a1;
+      L.dt1k[j] = keep || fresh ? b.take(act) : own_dt && j == 1 ? L.dt1b : L.a1;
     }
 
   }
@@ -693,11 +699,9 @@ dcnr_status wgrad_bf16(const void* dY, int64_t ldy, int N, const void* X, int64_
 // The backward's bf16 weight gradients run on the side stream: each call's
 // gemm_dw + split-K reduce are ordered after the main stream's work so far
 // (its dY is complete) and overlap the main stream's next dX GEMM and BN
-// passes. The operands stay alive because call n's enter() orders the main
-// stream after call n-lag's GEMM: with one shared dt2 / dt1 set (lag 1) the
-// next writer of a call's dY comes after the next call; with the two
-// alternating sets (lag 3) it comes after call n+3 (the writer of call n's dt2
-// is block j-2's BN2 apply, which follows block j-1's dW1 call). The reduces
+// passes. The operands stay alive: with a dt2 / dt1 set per block nothing
+// writes a call's dY again before the join (lag: never); with one shared set
+// (a single residual block) call n's enter() orders the main stream after call n-1's GEMM. The reduces
 // share one slab because they are serialised on the side stream. join()
 // orders the main stream after all of it. Same kernels, same order per
 // output: the gradients are unchanged.
@@ -1252,8 +1256,9 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   // alone, on the main stream, as before the overlap -- except in profile
   // mode 2, which times the side stream's gemm_dw launches in place)
   if (d.prec == DCNR_PREC_BF16 && (!g_prof || g_prof_mode == 2)) {
-    // lag 3 needs the alternating dt2 / dt1 sets (or one set per block)
-    TRY(dwp.init(sj.side, L.dt2b || keep_of(desc) ? 3 : 1));
+    // with a dt2 / dt1 set per block the main stream never waits for the
+    // side stream before the join (one shared set: after the previous call)
+    TRY(dwp.init(sj.side, keep_of(desc) || L.dt2b ? 1 << 30 : 1));
     pipe = &dwp;
   }
 
