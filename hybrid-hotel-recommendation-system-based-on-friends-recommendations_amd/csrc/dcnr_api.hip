@@ -328,7 +328,6 @@ bool masks_ok(const Dims& d) { return d.prec == DCNR_PREC_BF16 && d.Hp % 32 == 0
 int dq_of(const Dims& d) { return (int)rup(d.Dp, 32); }
 bool keep_of(const dcnr_model_desc* desc) { return (desc->flags & DCNR_FLAG_KEEP_INTERMEDIATES) != 0; }
 
-
 // bf16 train: the last block's head pass does not store h_R; the backward's
 // BN2 statistics pass rebuilds it from t2, h_{R-1} and the BN2 affine
 // (KEEP_INTERMEDIATES still stores it for the stage tests)
@@ -701,9 +700,9 @@ dcnr_status wgrad_bf16(const void* dY, int64_t ldy, int N, const void* X, int64_
 // (its dY is complete) and overlap the main stream's next dX GEMM and BN
 // passes. The operands stay alive: with a dt2 / dt1 set per block nothing
 // writes a call's dY again before the join (lag: never); with one shared set
-// (a single residual block) call n's enter() orders the main stream after call n-1's GEMM. The reduces
-// share one slab because they are serialised on the side stream. join()
-// orders the main stream after all of it. Same kernels, same order per
+// (a single residual block) call n's enter() orders the main stream after
+// call n-1's GEMM. The reduces share one slab because they are serialised
+// on the side stream. join() orders the main stream after all of it. Same kernels, same order per
 // output: the gradients are unchanged.
 struct DwPipe {
   static constexpr int RING = 4;
