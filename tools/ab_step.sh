@@ -11,5 +11,5 @@ for i in $(seq $N); do
   DCNR_LIB=$PWD/tools/lab_bin/libdcnr_$V.so timeout -k 10 300 python3 -u bench.py $A > $R/${V}_$i.log 2>&1 || exit 1
 done
 for f in $R/*_[0-9].log; do
-  echo "$(basename $f .log) $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],4), round(d["value"]/1e6,2), round(d["scored_pairs_per_sec"]/1e6,1))')"
+  echo "$(basename $f .log) $(tail -1 $f | python3 -c 'import json,sys; d=json.loads(sys.stdin.read()); print(round(d["ms_per_step"],4), round(d["value"]/1e6,2), round(d["scored_pairs_per_sec"]/1e6,1), round(d.get("configs1",{}).get("kernel_pairs_per_sec",0)/1e6,1))')"
 done > $R/summary.txt
