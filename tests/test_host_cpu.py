@@ -173,3 +173,46 @@ def test_workspace_query_huge_table():
     cfg = dict(gc.CFG1, n_users=(1 << 24) + 3)
     m = our_model(cfg, precision="bf16")
     assert m.workspace_bytes(4096, 1) > m.workspace_bytes(4096, 0) > 0
+
+
+def test_index_error_watch_ring():
+    """The deferred id-check ring (dcnr.model.IndexErrorWatch): a reserved
+    slot reads PENDING (-1) until the device stores the call's word; a
+    completed 0 frees the slot, a nonzero word raises IndexError on the next
+    poll, and at DEPTH calls in flight the oldest is waited for.  (The ring
+    is pinned host memory on a GPU box; a plain host tensor here, written by
+    the test where the forward's last kernel would.)"""
+    from dcnr.model import IndexErrorWatch
+    w = IndexErrorWatch()
+    w.ring = torch.zeros(IndexErrorWatch.RING, dtype=torch.int32)
+    w.view = w.ring.numpy()
+    slots = []
+    for _ in range(3):
+        s, ptr = w.reserve()
+        assert w.view[s] == IndexErrorWatch.PENDING and ptr == w.ring.data_ptr() + 4 * s
+        w.commit(s)
+        slots.append(s)
+    assert len(set(slots)) == 3
+    w.poll()                                   # nothing finished: all kept
+    assert w.pending == slots
+    w.view[slots[0]] = 0
+    w.view[slots[1]] = 0
+    w.poll()
+    assert w.pending == [slots[2]] and slots[0] in w.free
+    w.view[slots[2]] = 1                       # an out-of-range id in that call
+    with pytest.raises(IndexError):
+        w.poll()
+    assert w.pending == []
+    # a failed call gives its slot back
+    s, _ = w.reserve()
+    w.cancel(s)
+    assert s in w.free
+    # DEPTH calls in flight: the next reserve waits for the oldest
+    held = []
+    for _ in range(IndexErrorWatch.DEPTH):
+        s, _ = w.reserve()
+        w.view[s] = 0                          # (already finished)
+        w.commit(s)
+        held.append(s)
+    s, _ = w.reserve()
+    assert held[0] not in w.pending and s is not None
