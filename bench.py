@@ -156,8 +156,14 @@ def cpu_baseline(B_cpu=32768, steps=3):
     batches = [tc.make_cpu_batch(CFG["n_users"], CFG["n_items"], cat, CFG["n_num"], B_cpu, k)
                for k in range(steps + 1)]
     t = tc.time_steps(step.step, batches, warmup=1)
+    # scored pairs/s: the eval-mode forward (main.py:319-322) of the same model
+    ts = tc.time_steps(lambda u, i, c, n, y: step.score(u, i, c, n), batches, warmup=1)
     del step, batches
     return {"value": B_cpu / t, "unit": "samples/s", "cores": th, "kind": "port",
+            "scored_pairs": {"value": B_cpu / ts, "unit": "pairs/s", "cores": th, "kind": "port",
+                             "sample": f"{steps} eval-mode forwards (running-stat BN, no dropout, "
+                                       f"no_grad) at batch {B_cpu}, torch-CPU ops of "
+                                       f"oracle/torch_cpu.py, {steps * ts:.1f} s"},
             "validated": "step time within 10 % of the imported reference train.py step on the "
                          "same host (tools/validate_cpu_baseline.py, profiles/r02_cpu_baseline.txt)",
             "sample": f"{steps} timed train steps (zero_grad, fwd, BCEWithLogits, bwd, AdamW) at "

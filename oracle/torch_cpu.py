@@ -74,7 +74,9 @@ class TorchCPUStep:
         self.p = p
         self.opt = torch.optim.AdamW(list(p.values()), lr=lr, weight_decay=weight_decay)
 
-    def forward(self, user, item, cat, num):
+    def forward(self, user, item, cat, num, train=True):
+        """train.py:155-170; train=False: eval semantics (running-stat BN,
+        no dropout), the scoring call of main.py:319-322."""
         p = self.p
         embs = [F.embedding(user, p["user"]), F.embedding(item, p["item"])]
         embs += [F.embedding(cat[:, k], p[name]) for k, name in enumerate(self.cats)]
@@ -84,11 +86,11 @@ class TorchCPUStep:
             rm1, rv1 = self.bn[2 * j]
             rm2, rv2 = self.bn[2 * j + 1]
             out = F.linear(h, p[f"W{j}_1"], p[f"b{j}_1"])
-            out = F.batch_norm(out, rm1, rv1, p[f"g{j}_1"], p[f"be{j}_1"], True, 0.1, 1e-5)
+            out = F.batch_norm(out, rm1, rv1, p[f"g{j}_1"], p[f"be{j}_1"], train, 0.1, 1e-5)
             out = F.relu(out)
-            out = F.dropout(out, self.dropout, True)
+            out = F.dropout(out, self.dropout, train)
             out = F.linear(out, p[f"W{j}_2"], p[f"b{j}_2"])
-            out = F.batch_norm(out, rm2, rv2, p[f"g{j}_2"], p[f"be{j}_2"], True, 0.1, 1e-5)
+            out = F.batch_norm(out, rm2, rv2, p[f"g{j}_2"], p[f"be{j}_2"], train, 0.1, 1e-5)
             out = out + h
             h = F.relu(out)
         x = x0
@@ -96,6 +98,11 @@ class TorchCPUStep:
             xa, xt = x.unsqueeze(2), x.unsqueeze(1)
             x = xa.squeeze(2) + torch.matmul(xa, F.linear(xt, p[f"cw{l}"])).squeeze(2) + p[f"cb{l}"]
         return F.linear(torch.cat([h, x], dim=1), p["Wf"], p["bf"]).squeeze()
+
+    def score(self, user, item, cat, num):
+        """Eval-mode logits under no_grad (main.py:319-322)."""
+        with torch.no_grad():
+            return self.forward(user, item, cat, num, train=False)
 
     def step(self, user, item, cat, num, y):
         self.opt.zero_grad()
