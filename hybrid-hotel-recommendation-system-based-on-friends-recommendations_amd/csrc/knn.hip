@@ -587,9 +587,15 @@ constexpr int V4_SCAP = 256;     // rows at or under the selected k-th bin
 constexpr int V4_OVF = 1 << 30;  // count-word mark: a block dropped some of this query's rows
 constexpr int V4_QC = 256;       // queries per block (LDS: V4_QC x d bf16)
 // table rows per block: few query blocks -> long blocks (the per-block
-// prologue and epilogue amortised; measured 69 vs 78 us at Q = 32), many ->
-// short ones (a wave's list fill grows with rows x queries)
-constexpr int v4_rpb(int nqb) { return nqb <= 4 ? 2048 : 512; }
+// prologue and epilogue amortised; measured 69 vs 78 us at Q = 32).  Many
+// (NQB > 4: 16-32 KB of query fragments staged per block) -> about two blocks
+// per CU, 512-2048 rows: Q = 256 over 1M rows 134 us against 146 at a fixed
+// 512 (1954 blocks), 145 at 1024, 180 at 4096 (245 blocks, CUs left idle);
+// profiles/lab/r04zz_knn_rpb_ab.txt.  A wave's list fill (rows x queries x
+// admission rate, ~50 of 512 at 2048 rows) stays well inside V4_WL.
+inline int v4_rpb(int nqb, int64_t N) {
+  return nqb <= 4 ? 2048 : (int)std::min<int64_t>(2048, std::max<int64_t>(512, rup(cdiv(N, 512), 64)));
+}
 constexpr int64_t V4_Q1_N = 800000;   // a single query takes scan v2 below this many rows
                                       // (from Q = 2: 60-66 us for Q <= 8 against 65-98 on scan v2)
 
@@ -1454,10 +1460,13 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       const int nqb = (int)std::min<int64_t>(cdiv(Q, 16), V4_QC / 16);
       const int NQ = nqb <= 2 ? 2 : nqb <= 4 ? 4 : nqb <= 8 ? 8 : 16;
       const int NQS = std::min(NQ, V4_SNQ);
-      constexpr int RPB_S = 64;   // one row tile per wave: the sample pass is latency-bound
+      // one or two row tiles per wave: the sample pass is latency-bound (two
+      // when the block stages at most 4 query blocks: Q = 1 55.5 vs 57.3 us,
+      // Q = 32 64.1 vs 65.0; at 16 query blocks one tile, 149 vs 146 us at two)
+      const int RPB_S = NQS <= 4 ? 128 : 64;
       const int64_t NS = std::min<int64_t>(N, V4_S);   // sample rows
       const dim3 gs((unsigned)cdiv(NS, RPB_S), (unsigned)cdiv(Q, NQS * 16));
-      const int rpb = v4_rpb(NQ);
+      const int rpb = v4_rpb(NQ, N);
       const dim3 g4((unsigned)cdiv(N, rpb), (unsigned)cdiv(Q, NQ * 16));
 #define SCAN4(ks, nq, pk, g, n, rp)                                                                    \
   hipLaunchKernelGGL((scan4_kernel<ks, nq, pk>), g, dim3(256), 0, s, t, inv, tb, n, rp, qb, thr0, qn, \
