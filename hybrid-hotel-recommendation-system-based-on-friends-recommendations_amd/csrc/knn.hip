@@ -567,8 +567,8 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 // <= T0 (the k-th best of a V4_S-row exact sample: any subset's k-th best
 // bounds the table's), hence coarse distance <= T0 + V4_EPS: admitting the
 // rows under that bound keeps every true neighbour, ties included.  T0 comes
-// from the same machinery run on the sample under the 512-row bound of
-// kth_bound_kernel (pass 1).  The admitted rows (~N k / V4_S per query) are
+// from the same machinery run on the sample under kth_bound_kernel's 512-row
+// (Q >= 128: 1024-row) bound (pass 1).  The admitted rows (~N k / V4_S per query) are
 // appended to a per-query list with their exact fp32 distances (scan v2's
 // arithmetic, computed in scan4's epilogue); rescore_kernel selects the k
 // best by (distance, row).  A query whose list overflows V4_CAP (the count
@@ -1443,10 +1443,17 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
     }
     {   // (v4: also its bf16 queries and zeroed list counts)
       switch (d / 4) {
-#define CASEK(n)                                                                           \
-  case n:                                                                                  \
-    hipLaunchKernelGGL(kth_bound_kernel<n>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, \
-                       q, qn, k, thr0, qb, qcnt);                                          \
+// (v4 at Q >= 128: a 1024-row first bound halves pass 1's admissions -- Q =
+// 256 131 vs 134 us; below, the longer kth_bound block costs more than it
+// saves, +3 us at Q <= 32: profiles/lab/r04zz_knn_rpb_ab.txt)
+#define CASEK(n)                                                                             \
+  case n:                                                                                    \
+    if (v4 && Q >= 128)                                                                      \
+      hipLaunchKernelGGL((kth_bound_kernel<n, 2 * TH_S>), dim3((unsigned)Q), dim3(256), 0, s, \
+                         t, inv, N, q, qn, k, thr0, qb, qcnt);                               \
+    else                                                                                     \
+      hipLaunchKernelGGL(kth_bound_kernel<n>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, \
+                         q, qn, k, thr0, qb, qcnt);                                          \
     break;
         CASEK(1) CASEK(2) CASEK(3) CASEK(4) CASEK(5) CASEK(6) CASEK(7) CASEK(8)
         CASEK(9) CASEK(10) CASEK(11) CASEK(12) CASEK(13) CASEK(14) CASEK(15) CASEK(16)
