@@ -678,6 +678,8 @@ def main():
                         "lists every class)",
                 "achieved": dt["achieved_gbs"], "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                 "frac": dt["frac"], "traffic": pmc_traffic(dom),
+                "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc passes of the "
+                                  "committed profile set, not measured in this run)",
                 "bytes_per_launch": dt["bytes_per_launch"], "avg_launch_ms": dt["avg_launch_ms"]}
         roof["frac_of_measured_copy"] = dt["achieved_gbs"] / peaks["copy_gbs"]
         if prof_dw and prof_dw.get("gemm_dw", (0, 0, 0))[1] and dom == "gemm_dw":
@@ -751,6 +753,24 @@ def main():
             out["cpu_baseline"] = cpu_baseline()
         if rehearse:
             out["rehearsal"] = "DCNR_BENCH_REHEARSE: all ranks on cuda:0 over gloo (not a scaling number)"
+        # both halves of BASELINE's metric, restated LAST so that a record
+        # keeping only the line's tail still holds them
+        tk = eval_roof["tower_kernel"] or {}
+        out["summary"] = {
+            "train_samples_per_sec": out["value"], "ms_per_step": out["ms_per_step"],
+            "scored_pairs_per_sec": pairs_per_s,
+            "scored_pairs_frac_of_bf16_peak": eval_roof["mfma_view"]["frac"],
+            "tower_kernel_frac_of_bf16_peak": tk.get("frac_of_bf16_peak"),
+            "tower_us_per_131072": tk.get("us_per_call", 0) * 131072 / B if tk else None,
+            "deep_tower_mfma_frac": out["deep_tower_mfma"]["frac_of_bf16_peak"],
+            "gemm_fwd_avg_launch_ms": table.get("gemm_fwd", {}).get("avg_launch_ms"),
+            "roofline_frac": roof["frac"], "roofline_class": dom,
+            "gather_frac": out["roofline_gather"]["frac"],
+            "topk_us": None if cfg5 is None else
+            {f"q{Q}": cfg5.get(f"topk_q{Q}_us") for Q in (1, 32, 256)},
+            "request_ms": None if cfg5 is None else cfg5.get("request_ms"),
+            "cpu_baseline_samples_per_sec": out.get("cpu_baseline", {}).get("value"),
+        }
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -317,6 +317,7 @@ struct Layout {
   uint8_t* mask_a1[MAX_RES]; uint8_t* mask_h[MAX_RES + 1];
   EmbSortBufs emb;                              // deterministic embedding backward
   double* bce_part;
+  uint8_t* rowmap; size_t rowmap_bytes;   // DCNR_FLAG_ROW_MAP: byte per table row (last in ws)
   size_t total;
 };
 
@@ -465,6 +466,12 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, uint32_t flags 
 
   }
   L.bce_part = (double*)b.take(bce_ws_bytes());
+  if (train && (flags & DCNR_FLAG_ROW_MAP)) {   // last: every other offset as without the flag
+    int64_t rows = 0;
+    for (int t = 0; t < 2 + d.K; ++t) rows += d.rows[t];
+    L.rowmap_bytes = (size_t)rup(rows, 256);
+    L.rowmap = (uint8_t*)b.take(L.rowmap_bytes);
+  }
   L.total = b.off + 256;
   return L;
 }
@@ -949,6 +956,7 @@ dcnr_status dcnr_workspace_offset(const dcnr_model_desc* desc, int64_t B, int mo
     case DCNR_WS_ZC: p = L.zc; break;
     case DCNR_WS_XCOEF: if (train) p = L.xcoef; break;
     case DCNR_WS_SC: if (train) p = L.sc; break;
+    case DCNR_WS_ROW_MAP: p = L.rowmap; break;
   }
   *offset = p ? (int64_t)((const char*)p - base) : -1;
   return DCNR_OK;
@@ -1207,10 +1215,19 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   const float* dz = dlogits;
   const int Hp = d.Hp, H = d.H;
   const float p = d.dropout;
+  const bool rowmap = (desc->flags & DCNR_FLAG_ROW_MAP) != 0;
+  if (rowmap && (accumulate || !L.rowmap)) {
+    set_error("dcnr_backward: DCNR_FLAG_ROW_MAP needs accumulate = 0");
+    return DCNR_BAD_ARG;
+  }
   // dense embedding grads: zeroed; the per-row sums (emb_segment_sum) then
   // write every row an id references.  (On the side stream under the deep
   // tower instead: 3.99-4.00 vs 3.98-3.99 ms/step, same box; kept here.)
-  if (!accumulate) {
+  // DCNR_FLAG_ROW_MAP: only the row map is zeroed; the sums mark the rows
+  // they write and the optimizer reads unmarked rows as 0.
+  if (rowmap) {
+    TRYB(DCNR_K_PACK, (double)L.rowmap_bytes, fill_zero(L.rowmap, L.rowmap_bytes, s));
+  } else if (!accumulate) {
     void* zp[2 + MAX_CAT];
     int64_t zn[2 + MAX_CAT];
     for (int t = 0; t < 2 + d.K; ++t) { zp[t] = Gr.tab[t]; zn[t] = d.rows[t] * d.widths[t] * 4; }
@@ -1225,6 +1242,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   EmbBwdDesc eb;
   memset(&eb, 0, sizeof(eb));
   eb.n_tab = g.n_tab;
+  eb.touched = rowmap ? L.rowmap : nullptr;
   for (int t = 0; t < g.n_tab; ++t) {
     eb.grad[t] = Gr.tab[t]; eb.rows[t] = g.rows[t]; eb.width[t] = g.width[t]; eb.off[t] = g.off[t];
   }
@@ -1553,6 +1571,35 @@ dcnr_status dcnr_adam_step(int32_t n_tensors, float* const* params, const float*
   for (int i = 0; i < n_tensors; ++i) nparam += (double)numel[i];
   TRYB(DCNR_K_ADAM, 28.0 * nparam, adam(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, lr, beta1, beta2,
                          eps, weight_decay, step, decoupled, s));
+  return DCNR_OK;
+}
+
+dcnr_status dcnr_adam_step_rows(int32_t n_tensors, float* const* params, const float* const* grads,
+                                float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
+                                const uint8_t* const* row_map, const int32_t* row_width,
+                                float lr, float beta1, float beta2, float eps, float weight_decay,
+                                int64_t step, int decoupled, dcnr_stream_t stream) {
+  if (n_tensors < 0 || (n_tensors > 0 && (!params || !grads || !exp_avg || !exp_avg_sq || !numel ||
+                                          !row_map || !row_width)) || step < 1) {
+    set_error("dcnr_adam_step_rows: bad argument");
+    return DCNR_BAD_ARG;
+  }
+  double nbytes = 0;
+  for (int i = 0; i < n_tensors; ++i) {
+    if (row_map[i] && (row_width[i] < 1 || numel[i] % row_width[i] || numel[i] >= (int64_t(1) << 32))) {
+      set_error("dcnr_adam_step_rows: tensor %d: %lld elements in rows of %d", i, (long long)numel[i],
+                row_width[i]);
+      return DCNR_BAD_ARG;
+    }
+    // p, m, v read and written, the map byte per row; the gradient of a
+    // mapped tensor only where marked (a share the library does not know:
+    // not counted, so the figure is a floor)
+    nbytes += (row_map[i] ? 24.0 : 28.0) * (double)numel[i] +
+              (row_map[i] ? (double)numel[i] / row_width[i] : 0.0);
+  }
+  hipStream_t s = (hipStream_t)stream;
+  TRYB(DCNR_K_ADAM, nbytes, adam(n_tensors, params, grads, exp_avg, exp_avg_sq, numel, lr, beta1, beta2,
+                                 eps, weight_decay, step, decoupled, s, row_map, row_width));
   return DCNR_OK;
 }
 

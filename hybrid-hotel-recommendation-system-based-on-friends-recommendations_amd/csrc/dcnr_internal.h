@@ -480,6 +480,7 @@ struct EmbBwdDesc {
   int n_tab;
   const float* V[8];             // dx0_cross = sum_k coef[b][k] V[k] (w_0..w_{L-1}, w_f[H:])
   int nv;                        // L + 1
+  uint8_t* touched;              // null, or a byte per sort key (row): set to 1 for each row written
 };
 struct EmbSortBufs {
   uint32_t *ids;                 // [n_tab * B] clamped ids, table-major
@@ -601,7 +602,8 @@ dcnr_status bce(const float* z, const float* y, int64_t B, float* loss, float* d
 // optimizer
 dcnr_status adam(int n, float* const* p, const float* const* g, float* const* m, float* const* v,
                  const int64_t* numel, float lr, float b1, float b2, float eps, float wd,
-                 int64_t step, int decoupled, hipStream_t s);
+                 int64_t step, int decoupled, hipStream_t s,
+                 const uint8_t* const* row_map = nullptr, const int32_t* row_width = nullptr);
 
 // knn
 dcnr_status row_inv_norms(const float* t, int64_t N, int d, float* out, hipStream_t s);

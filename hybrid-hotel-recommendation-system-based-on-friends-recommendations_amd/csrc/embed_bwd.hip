@@ -53,6 +53,7 @@ struct EmbTabs {
   int width[MAX_TABLES];
   int off[MAX_TABLES];
   const float* V[8];   // dx0_cross basis (w_0..w_{L-1}, w_f[H:]), indexed by x0 column
+  uint8_t* touched;    // DCNR_FLAG_ROW_MAP: byte per key, 1 for every row written
 };
 
 EmbTabs make_tabs(const EmbBwdDesc& e) {
@@ -68,6 +69,7 @@ EmbTabs make_tabs(const EmbBwdDesc& e) {
     base += (uint32_t)e.rows[i];
   }
   for (int k = 0; k < e.nv && k < 8; ++k) t.V[k] = e.V[k];
+  t.touched = e.touched;
   return t;
 }
 
@@ -508,6 +510,7 @@ __global__ __launch_bounds__(ENT) void emb_runs_short_kernel(EmbTabs et, int nt,
   const int64_t t0 = (int64_t)t * B, t1 = t0 + B;
   const uint32_t k = ks[i];
   if (i > t0 && ks[i - 1] == k) return;   // not the head of its run
+  if (et.touched) et.touched[k] = 1;      // every run (short, long, huge) has its head here
   uint32_t nk[LIM];
 #pragma unroll
   for (int q = 0; q < LIM; ++q) nk[q] = i + 1 + q < t1 ? ks[i + 1 + q] : ~0u;
@@ -1032,10 +1035,17 @@ __global__ __launch_bounds__(256) void sparse_pack_kernel(const float* __restric
     const int c = (int)(e % per) * V;
     const int64_t o = offs[(int64_t)t * ld + i];
     if (c == 0) out_off[base + i] = o;
-    if constexpr (V == 4)
-      *reinterpret_cast<float4*>(out_rows + (base + i) * width + c) = *reinterpret_cast<const float4*>(grad + o + c);
-    else
+    if constexpr (V == 4) {
+      float* d = out_rows + (base + i) * width + c;
+      if ((o & 3) == 0) {
+        *reinterpret_cast<float4*>(d) = *reinterpret_cast<const float4*>(grad + o + c);
+      } else {   // a caller's offset off the 16-B grid (FusedTrainer's never are)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) d[j] = grad[o + c + j];
+      }
+    } else {
       out_rows[(base + i) * width + c] = grad[o + c];
+    }
   }
 }
 
@@ -1056,6 +1066,11 @@ __global__ __launch_bounds__(256) void sparse_add_kernel(float* __restrict__ sha
     const int64_t r = offs[i] - lo;
     if (r < 0 || r + width > elems) continue;
     if constexpr (V == 4) {
+      if (r & 3) {   // a row off the 16-B grid: scalar adds
+#pragma unroll
+        for (int j = 0; j < 4; ++j) shard[r + c + j] += rows[i * width + c + j];
+        continue;
+      }
       float4* d = reinterpret_cast<float4*>(shard + r + c);
       const float4 g = *reinterpret_cast<const float4*>(rows + i * width + c);
       float4 v = *d;

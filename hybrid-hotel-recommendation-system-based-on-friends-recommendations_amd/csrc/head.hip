@@ -119,12 +119,15 @@ __global__ __launch_bounds__(NT) void bce_final_kernel(const double* part, int n
   if (threadIdx.x == 0) loss[0] = (float)(red[0] / (double)B);
 }
 
-constexpr int MAXT = 64;
+constexpr int MAXT = 48;   // (the batch is a kernel argument: <= 4 KB)
 struct AdamBatch {
   float* p[MAXT]; const float* g[MAXT]; float* m[MAXT]; float* v[MAXT];
+  const uint8_t* map[MAXT];   // null, or a byte per row: 0 = gradient row not stored (exactly 0)
   int64_t n[MAXT]; int64_t blk0[MAXT + 1];
+  int rw[MAXT];               // row width (elements) of a mapped tensor
   int nt;
 };
+static_assert(sizeof(AdamBatch) <= 4096, "kernel argument size");
 
 // torch.optim._functional single-tensor Adam/AdamW algorithm, fp32:
 //   AdamW: p *= 1 - lr*wd ; Adam: g += wd*p
@@ -141,11 +144,16 @@ __global__ __launch_bounds__(NT) void adam_kernel(AdamBatch ab, float lr, float 
   float* m = ab.m[t];
   float* v = ab.v[t];
   const int64_t n = ab.n[t];
+  const uint8_t* map = ab.map[t];
+  const uint32_t rw = (uint32_t)ab.rw[t];
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     int64_t i = base + u * NT + threadIdx.x;
     if (i >= n) break;
-    float pp = p[i], gg = g[i], mm = m[i], vv = v[i];
+    // an unmarked row's gradient is exactly 0 and is not read (the same
+    // arithmetic as a stored +0: m, v decay, weight decay, the update)
+    const bool gr = !map || map[(uint32_t)i / rw];
+    float pp = p[i], gg = gr ? g[i] : 0.f, mm = m[i], vv = v[i];
     if (decoupled) pp = pp * (1.f - lr * wd);
     else if (wd != 0.f) gg = gg + wd * pp;
     mm = mm + (1.f - b1) * (gg - mm);
@@ -212,7 +220,8 @@ dcnr_status bce(const float* z, const float* y, int64_t B, float* loss, float* d
 
 dcnr_status adam(int n, float* const* p, const float* const* g, float* const* m, float* const* v,
                  const int64_t* numel, float lr, float b1, float b2, float eps, float wd,
-                 int64_t step, int decoupled, hipStream_t s) {
+                 int64_t step, int decoupled, hipStream_t s, const uint8_t* const* row_map,
+                 const int32_t* row_width) {
   double bc1 = 1.0 - std::pow((double)b1, (double)step);
   double bc2 = 1.0 - std::pow((double)b2, (double)step);
   float step_size = (float)(lr / bc1);
@@ -224,6 +233,8 @@ dcnr_status adam(int n, float* const* p, const float* const* g, float* const* m,
     for (int i = 0; i < ab.nt; ++i) {
       ab.p[i] = p[off + i]; ab.g[i] = g[off + i]; ab.m[i] = m[off + i]; ab.v[i] = v[off + i];
       ab.n[i] = numel[off + i];
+      ab.map[i] = row_map ? row_map[off + i] : nullptr;
+      ab.rw[i] = ab.map[i] ? row_width[off + i] : 1;
       ab.blk0[i + 1] = ab.blk0[i] + cdiv(ab.n[i], NT * 4);
     }
     int64_t blocks = ab.blk0[ab.nt];

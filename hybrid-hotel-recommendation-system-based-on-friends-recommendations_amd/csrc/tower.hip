@@ -458,6 +458,9 @@ dcnr_status eval_tower(const TowerArgs& a0, hipStream_t s) {
     b.zc = a.zc + m0;
     b.logits = a.logits + m0;
     b.ntiles = (int)cdiv(b.M, TW_TILE);
+    // the mirror is stored once, by the last chunk: an earlier chunk's store
+    // would let the host recycle the slot while a later one can still write it
+    b.err_mirror = m0 + b.M >= a0.M ? a.err_mirror : nullptr;
     const int grid = (int)std::min<int64_t>(b.ntiles, 256);
     void* args[] = {&b};
     DCNR_HIP(hipLaunchKernel(k, dim3(grid), dim3(TW_NT), args, lds, s));

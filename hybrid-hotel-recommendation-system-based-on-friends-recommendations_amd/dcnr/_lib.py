@@ -23,9 +23,11 @@ EVAL, TRAIN = 0, 1
 FLAG_CHECK_INDICES = 1
 FLAG_KEEP_INTERMEDIATES = 2
 FLAG_FUSED_TOWER = 4
+FLAG_ROW_MAP = 8
+ABI_VERSION = 4
 # dcnr_ws_tensor (include/dcnr.h)
 WS_KINDS = ["x0", "h", "t1", "t2", "a1", "mask_a1", "mask_h", "bn_mean", "bn_invstd", "bn_scale",
-            "bn_shift", "du", "dt2", "da", "dt1", "G", "dx0", "zc", "xcoef", "sc"]
+            "bn_shift", "du", "dt2", "da", "dt1", "G", "dx0", "zc", "xcoef", "sc", "row_map"]
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.c_void_p)
@@ -86,6 +88,9 @@ _SIGS = {
     "dcnr_adam_step": (ctypes.c_int, [ctypes.c_int32, _P, _P, _P, _P, _P, ctypes.c_float,
                                       ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                       ctypes.c_float, _I64, ctypes.c_int, _P]),
+    "dcnr_adam_step_rows": (ctypes.c_int, [ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P,
+                                           ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                           ctypes.c_float, ctypes.c_float, _I64, ctypes.c_int, _P]),
     "dcnr_row_inv_norms": (ctypes.c_int, [_P, _I64, ctypes.c_int32, _P, _P]),
     "dcnr_cosine_topk_workspace_size": (ctypes.c_size_t, [_I64, _I64, ctypes.c_int32]),
     "dcnr_cosine_topk": (ctypes.c_int, [_P, _P, _I64, ctypes.c_int32, _P, _I64, ctypes.c_int32,
@@ -162,7 +167,7 @@ def load(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
-        if lib.dcnr_abi_version() != 3:
+        if lib.dcnr_abi_version() != ABI_VERSION:
             raise LibraryMissing("libdcnr ABI version mismatch")
         if path is None:
             _lib = lib

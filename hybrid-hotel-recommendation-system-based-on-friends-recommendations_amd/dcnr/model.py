@@ -112,9 +112,13 @@ class IndexErrorWatch:
     DEPTH = 8      # calls in flight before the oldest is waited for
     PENDING = -1
 
+    SPIN_S = 2e-3  # host spin on one word between queries of its stream
+
     def __init__(self):
         self.ring = None
         self.pending = []
+        self.orphans = []   # slots dropped by a raised error, still PENDING
+        self.streams = {}   # slot -> the stream of the call that writes it
         self.free = list(range(self.RING))
         self.lock = threading.Lock()
 
@@ -122,6 +126,7 @@ class IndexErrorWatch:
         if self.ring is None:
             self.ring = torch.zeros(self.RING, dtype=torch.int32, pin_memory=True)
             self.view = self.ring.numpy()   # host view of the pinned words
+        self._reclaim()
         if len(self.pending) >= self.DEPTH:
             self._poll(oldest=True)
         if not self.free:
@@ -139,10 +144,11 @@ class IndexErrorWatch:
             return None, None
         return slot, self.ring.data_ptr() + 4 * slot
 
-    def commit(self, slot):
-        """The call that got ``slot`` is enqueued: watch its word."""
+    def commit(self, slot, stream=None):
+        """The call that got ``slot`` is enqueued (on ``stream``): watch its word."""
         with self.lock:
             self.pending.append(slot)
+            self.streams[slot] = stream
 
     def cancel(self, slot):
         with self.lock:
@@ -162,6 +168,8 @@ class IndexErrorWatch:
             if slot is not None:
                 self.ring[slot:slot + 1].copy_(word.view(torch.int32)[:1], non_blocking=True)
                 self.pending.append(slot)
+                self.streams[slot] = torch.cuda.current_stream(word.device) \
+                    if word.is_cuda else None
                 return
         # every slot held by calls still being enqueued: check this one now
         if int(word.view(torch.int32)[0]) != 0:
@@ -171,26 +179,59 @@ class IndexErrorWatch:
         with self.lock:
             self._poll(oldest, all_)
 
+    def _stream_idle(self, slot):
+        """Whether the stream the slot's call was enqueued on has drained.  A
+        sticky stream error (a faulting kernel, a launch that failed after
+        commit) raises here, as the old per-call event's synchronize did."""
+        st = self.streams.get(slot)
+        if st is None:
+            return False
+        return bool(st.query())
+
     def _wait(self, slot):
+        """True once the slot's word has landed; False if its stream drained
+        without storing it (the writer never ran)."""
+        t0 = time.perf_counter()
         while int(self.view[slot]) == self.PENDING:
+            if time.perf_counter() - t0 > self.SPIN_S:
+                # the word is late: ask the stream (raises its error, if any)
+                if self._stream_idle(slot) and int(self.view[slot]) == self.PENDING:
+                    return False
+                t0 = time.perf_counter()
             time.sleep(20e-6)
+        return True
+
+    def _reclaim(self):
+        """Orphaned slots return to the ring once their word has landed."""
+        if self.orphans:
+            left = [s for s in self.orphans if int(self.view[s]) == self.PENDING]
+            self.free.extend(s for s in self.orphans if s not in left)
+            self.orphans = left
 
     def _poll(self, oldest=False, all_=False):
+        self._reclaim()
         keep = []
         for n, slot in enumerate(self.pending):
             if all_ or (oldest and n == 0):
-                self._wait(slot)
+                if not self._wait(slot):
+                    self.pending = keep + self.pending[n + 1:]
+                    self.free.append(slot)
+                    raise RuntimeError("id-check word never stored: the call that owned ring "
+                                       f"slot {slot} did not run to completion")
             elif int(self.view[slot]) == self.PENDING:
                 keep.append(slot)
                 continue
             bad = int(self.view[slot]) != 0
             self.free.append(slot)
             if bad:
-                # the other words are dropped; their slots return to the ring
-                # once nothing can still write them
+                # the other words are dropped; a slot whose word has not
+                # landed yet is an orphan until it does (_reclaim), so the
+                # ring never loses it and a late store never hits a new call
                 for sl in keep + self.pending[n + 1:]:
                     if int(self.view[sl]) != self.PENDING:
                         self.free.append(sl)
+                    else:
+                        self.orphans.append(sl)
                 self.pending = []
                 raise IndexError("index out of range in self (ids passed to an earlier call)")
         self.pending = keep
@@ -240,9 +281,10 @@ class DCN_RecSys(nn.Module):
         self._flat = None
 
     # ------------------------------------------------------------ native glue
-    def desc(self, grad_ready=None) -> _lib.ModelDesc:
+    def desc(self, grad_ready=None, extra_flags: int = 0) -> _lib.ModelDesc:
         """The native model descriptor.  ``grad_ready``: the backward's
-        gradient-group hook (FusedTrainer passes it per call)."""
+        gradient-group hook (FusedTrainer passes it per call); ``extra_flags``:
+        per-call DCNR_FLAG_* (FusedTrainer's DCNR_FLAG_ROW_MAP)."""
         d = self._dims
         desc = _lib.ModelDesc()
         desc.n_users = d['n_users']
@@ -258,7 +300,7 @@ class DCN_RecSys(nn.Module):
         desc.precision = _PRECISIONS[self.precision]
         desc.flags = (_lib.FLAG_CHECK_INDICES if self.check_indices else 0) | \
             (_lib.FLAG_KEEP_INTERMEDIATES if getattr(self, 'keep_intermediates', False) else 0) | \
-            (_lib.FLAG_FUSED_TOWER if getattr(self, 'fused_tower', False) else 0)
+            (_lib.FLAG_FUSED_TOWER if getattr(self, 'fused_tower', False) else 0) | int(extra_flags)
         if self.bn_allreduce is not None:
             desc.bn_allreduce = self.bn_allreduce
         if grad_ready is not None:
@@ -329,20 +371,21 @@ class DCN_RecSys(nn.Module):
         self.__dict__['_ptr_cache'] = (key, arr)
         return arr
 
-    def workspace_bytes(self, B: int, mode: int) -> int:
+    def workspace_bytes(self, B: int, mode: int, extra_flags: int = 0) -> int:
         lib = _lib.load()
         n = ctypes.c_size_t(0)
-        desc = self.desc()
+        desc = self.desc(extra_flags=extra_flags)
         _lib.check(lib.dcnr_workspace_size(ctypes.byref(desc), int(B), int(mode), ctypes.byref(n)),
                    "dcnr_workspace_size")
         return int(n.value)
 
-    def workspace_offset(self, B: int, mode: int, kind: str, index: int = 0) -> int:
+    def workspace_offset(self, B: int, mode: int, kind: str, index: int = 0,
+                         extra_flags: int = 0) -> int:
         """Byte offset of a stored tensor in the workspace (dcnr_workspace_offset;
         -1 if not materialised)."""
         lib = _lib.load()
         off = ctypes.c_int64(0)
-        desc = self.desc()
+        desc = self.desc(extra_flags=extra_flags)
         _lib.check(lib.dcnr_workspace_offset(ctypes.byref(desc), int(B), int(mode),
                                              _lib.WS_KINDS.index(kind), int(index),
                                              ctypes.byref(off)), "dcnr_workspace_offset")
@@ -498,7 +541,7 @@ def _hook_error(model):
 
 
 def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
-                ws: Optional[torch.Tensor] = None):
+                ws: Optional[torch.Tensor] = None, extra_flags: int = 0):
     """One native forward.  With ``model.check_indices`` the workspace's
     error word (``ws[:4]``) is checked: in this call (``"sync"``) or through
     the model's deferred watch."""
@@ -506,12 +549,12 @@ def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
     B = user.shape[0]
     dev = user.device
     mode = _lib.TRAIN if train else _lib.EVAL
-    nbytes = model.workspace_bytes(B, mode)
+    nbytes = model.workspace_bytes(B, mode, extra_flags)
     if ws is None or ws.numel() < nbytes:
         ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     logits = torch.empty(B, dtype=torch.float32, device=dev)
     state = model.state_ptr_array()
-    desc = model.desc()
+    desc = model.desc(extra_flags=extra_flags)
     # deferred id check: the forward's last kernel stores the error word in a
     # pinned ring slot (no copy on the stream)
     slot = None
@@ -527,7 +570,7 @@ def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
     model._active_ws = None
     if slot is not None:
         if st == 0:
-            model._index_watch.commit(slot)
+            model._index_watch.commit(slot, torch.cuda.current_stream(dev))
         else:
             model._index_watch.cancel(slot)
     _hook_error(model)
@@ -541,12 +584,13 @@ def run_forward(model: DCN_RecSys, train: bool, seed: int, user, item, cat, num,
 
 
 def run_backward(model: DCN_RecSys, user, item, cat, num, dlogits, ws, grads: List[torch.Tensor],
-                 seed: int, accumulate=False, grad_ready=None):
+                 seed: int, accumulate=False, grad_ready=None, extra_flags: int = 0):
     """``seed`` must be the dropout seed of the train-mode forward that filled ws.
-    ``grad_ready``: optional dcnr_grad_ready_fn for this call only."""
+    ``grad_ready``: optional dcnr_grad_ready_fn for this call only;
+    ``extra_flags``: the forward's per-call flags (the same workspace layout)."""
     lib = _lib.load()
     B = user.shape[0]
-    desc = model.desc(grad_ready)
+    desc = model.desc(grad_ready, extra_flags)
     model._active_ws = ws
     st = lib.dcnr_backward(ctypes.byref(desc), model.state_ptr_array(),
                            _lib.ptr_array(grads), user.data_ptr(), item.data_ptr(),

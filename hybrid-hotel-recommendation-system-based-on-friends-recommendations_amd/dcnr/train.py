@@ -31,6 +31,13 @@ optimizer.step) as native calls over flat parameter/gradient/moment buffers:
 
 Numerically the same update as ``torch.optim.AdamW``/``Adam`` on the
 reference's dense gradients (every embedding row's moments decay every step).
+
+world == 1 (unless ``dense_table_grads=True``): the backward does not zero the
+tables' gradients (142 MB at the bench shape) but marks the rows it writes in a
+byte map (DCNR_FLAG_ROW_MAP), and the optimizer launch reads unmarked rows'
+gradients as exactly 0 (dcnr_adam_step_rows): the same parameters bit for bit,
+without the zero fill and without reading the untouched rows' gradients.  The
+tables' ``.grad`` rows a step did not touch then hold stale values.
 """
 from __future__ import annotations
 
@@ -49,7 +56,7 @@ from .ops import bce_with_logits
 class FusedTrainer:
     def __init__(self, model: DCN_RecSys, lr=1e-3, weight_decay=1e-2, optimizer_name='AdamW',
                  betas=(0.9, 0.999), eps=1e-8, process_group=None, sync_bn=False,
-                 shard_optimizer=None, exchange="dense", sparse_ops=None):
+                 shard_optimizer=None, exchange="dense", sparse_ops=None, dense_table_grads=False):
         if optimizer_name not in ('AdamW', 'Adam'):
             raise ValueError("optimizer_name must be 'AdamW' or 'Adam' (train.py:201-204)")
         self.model = model
@@ -110,6 +117,10 @@ class FusedTrainer:
         self.step_count = 0
         self._ws = None
         self._grads = [p.grad for p in model.param_tensors()]   # views into gflat
+        # world 1: the row-map step (module docstring)
+        self.row_map = self.world == 1 and not dense_table_grads
+        self._flags = _lib.FLAG_ROW_MAP if self.row_map else 0
+        self._rows_cache = None
         if sync_bn and self.world > 1:
             from .parallel import install_sync_bn
             install_sync_bn(model, process_group)
@@ -123,7 +134,8 @@ class FusedTrainer:
         y = y.reshape(-1).to(torch.float32).contiguous()
         seed = dropout_seed(user.device)
         model._index_watch.poll()
-        logits, self._ws = run_forward(model, True, seed, user, item, cat, num, self._ws)
+        logits, self._ws = run_forward(model, True, seed, user, item, cat, num, self._ws,
+                                       extra_flags=self._flags)
         self._B = user.shape[0]
         if self.exchange == "sparse" and self._sparse is not None:
             # the touched rows come from the forward's id sort: their counts
@@ -134,7 +146,8 @@ class FusedTrainer:
         self._dense_work = None
         try:
             run_backward(model, user, item, cat, num, dz, self._ws, self._grads, seed,
-                         accumulate=False, grad_ready=self._grad_ready_cb)
+                         accumulate=False, grad_ready=self._grad_ready_cb,
+                         extra_flags=self._flags)
         except RuntimeError:
             # the hook may have started the dense all-reduce before the
             # failure: let it finish before anyone writes gflat again
@@ -150,8 +163,59 @@ class FusedTrainer:
             raise
         # the all-reduce this step's backward started (None: start it now)
         dense, self._dense_work = self._dense_work, None
-        self._exchange_and_update(None, None, dense)
+        if self.row_map:
+            self.step_count += 1
+            self._adam_rows(self.step_count)
+        else:
+            self._exchange_and_update(None, None, dense)
         return (loss, logits) if return_logits else loss
+
+    def _row_segments(self):
+        """dcnr_adam_step_rows' tensor list over the flat buffers: each table
+        with its slice of the workspace's row map, the gaps and the dense
+        segment without (cached per workspace pointer and batch)."""
+        ws, B = self._ws, self._B
+        key = (ws.data_ptr(), B)
+        if self._rows_cache is not None and self._rows_cache[0] == key:
+            return self._rows_cache[1]
+        model = self.model
+        map_off = model.workspace_offset(B, _lib.TRAIN, "row_map", extra_flags=_lib.FLAG_ROW_MAP)
+        if map_off < 0:
+            raise RuntimeError("train workspace has no row map")
+        d = model._dims
+        rows = [d['n_users'], d['n_items']] + list(d['cat_dims'])
+        offs = model.flat_offsets
+        params = model.param_tensors()
+        segs = []   # (lo, numel, map pointer or None, width)
+        pos, kb = 0, 0
+        for t, r in enumerate(rows):
+            if offs[t] > pos:
+                segs.append((pos, offs[t] - pos, None, 1))
+            w = params[t].shape[1]
+            segs.append((offs[t], r * w, ws.data_ptr() + map_off + kb, w))
+            pos, kb = offs[t] + r * w, kb + r
+        N = self.flat.numel()
+        if N > pos:
+            segs.append((pos, N - pos, None, 1))
+        n = len(segs)
+        P = lambda buf: (ctypes.c_void_p * n)(*[buf.data_ptr() + 4 * lo for lo, *_ in segs])  # noqa: E731
+        arrs = (P(self.flat), P(self.gflat), P(self.m), P(self.v),
+                (ctypes.c_int64 * n)(*[c for _, c, _, _ in segs]),
+                (ctypes.c_void_p * n)(*[mp for _, _, mp, _ in segs]),
+                (ctypes.c_int32 * n)(*[w for _, _, _, w in segs]), n)
+        self._rows_cache = (key, arrs)
+        return arrs
+
+    def _adam_rows(self, step):
+        """The world-1 optimizer step of a row-map backward (module docstring)."""
+        p, g, m, v, numel, maps, widths, n = self._row_segments()
+        lib = _lib.load()
+        _lib.check(lib.dcnr_adam_step_rows(n, p, g, m, v, numel, maps, widths,
+                                           float(self.lr), float(self.betas[0]),
+                                           float(self.betas[1]), float(self.eps), float(self.wd),
+                                           int(step), 1 if self.decoupled else 0,
+                                           _lib.stream_ptr(self.flat.device)),
+                   "dcnr_adam_step_rows")
 
     def _on_grads_ready(self, ctx, group, stream):
         """dcnr_grad_ready_fn: the dense gradients are enqueued -> start their

@@ -73,7 +73,7 @@
 extern "C" {
 #endif
 
-#define DCNR_ABI_VERSION 3
+#define DCNR_ABI_VERSION 4
 
 typedef void* dcnr_stream_t; /* hipStream_t */
 
@@ -106,6 +106,15 @@ typedef enum { DCNR_EVAL = 0, DCNR_TRAIN = 1 } dcnr_mode;
  * below that the layer path is faster (the tower walks a tile's layers in
  * sequence on one CU).  Same results either way up to bf16 rounding order. */
 #define DCNR_FLAG_FUSED_TOWER 4u
+/* Train mode (ABI 4): the backward leaves the embedding tables' gradient rows
+ * that the batch did not reference as they were (no 142 MB zero fill at the
+ * bench shape) and instead marks, in a byte map at the end of the workspace
+ * (DCNR_WS_ROW_MAP: one byte per table row, the tables in order, 1 = this
+ * call wrote the row), every row it wrote.  dcnr_adam_step_rows reads the map
+ * and treats unmarked rows' gradients as exactly 0, which is bit-identical to
+ * the dense-gradient step.  Only with accumulate = 0 (the flag and accumulate
+ * together are DCNR_BAD_ARG).  Same workspace offsets for every other tensor. */
+#define DCNR_FLAG_ROW_MAP 8u
 
 /* Optional collective hook for SyncBN across data-parallel ranks: called
  * (stream-ordered, from the calling thread) with a device buffer of `count`
@@ -178,7 +187,7 @@ typedef enum {
   DCNR_WS_MASK_A1 = 5, DCNR_WS_MASK_H = 6, DCNR_WS_BN_MEAN = 7, DCNR_WS_BN_INVSTD = 8,
   DCNR_WS_BN_SCALE = 9, DCNR_WS_BN_SHIFT = 10, DCNR_WS_DU = 11, DCNR_WS_DT2 = 12,
   DCNR_WS_DA = 13, DCNR_WS_DT1 = 14, DCNR_WS_G = 15, DCNR_WS_DX0 = 16, DCNR_WS_ZC = 17,
-  DCNR_WS_XCOEF = 18, DCNR_WS_SC = 19, DCNR_WS_KINDS = 20
+  DCNR_WS_XCOEF = 18, DCNR_WS_SC = 19, DCNR_WS_ROW_MAP = 20, DCNR_WS_KINDS = 21
 } dcnr_ws_tensor;
 dcnr_status dcnr_workspace_offset(const dcnr_model_desc* desc, int64_t B, int mode, int kind,
                                   int index, int64_t* offset);
@@ -283,6 +292,20 @@ dcnr_status dcnr_adam_step(int32_t n_tensors, float* const* params, const float*
                            float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
                            float lr, float beta1, float beta2, float eps, float weight_decay,
                            int64_t step, int decoupled, dcnr_stream_t stream);
+
+/* dcnr_adam_step over gradients some of whose rows are not stored (ABI 4,
+ * the same step, train.py:201-204, 226): tensor i with row_map[i] != NULL is
+ * [numel[i] / row_width[i]][row_width[i]] and element e's gradient is
+ * grads[i][e] where row_map[i][e / row_width[i]] != 0, else exactly 0 (the
+ * row is not read) -- bit-identical to dcnr_adam_step on the dense gradient
+ * with those rows zeroed.  row_map[i] == NULL: dense.  row_map / row_width are
+ * HOST arrays (row_map entries device pointers, e.g. into the DCNR_WS_ROW_MAP
+ * of the train workspace, offset to the table's first row). */
+dcnr_status dcnr_adam_step_rows(int32_t n_tensors, float* const* params, const float* const* grads,
+                                float* const* exp_avg, float* const* exp_avg_sq, const int64_t* numel,
+                                const uint8_t* const* row_map, const int32_t* row_width,
+                                float lr, float beta1, float beta2, float eps, float weight_decay,
+                                int64_t step, int decoupled, dcnr_stream_t stream);
 
 /* 1/||row|| for each row of table [N,d] (0-norm rows -> 1, as sklearn's normalize). */
 dcnr_status dcnr_row_inv_norms(const float* table, int64_t N, int32_t d, float* inv_norms,

@@ -27,7 +27,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(lib, s), f"libdcnr.so does not export {s}"
     assert sorted(_lib.exported_symbols()) == syms
-    assert lib.dcnr_abi_version() == 3
+    assert lib.dcnr_abi_version() == _lib.ABI_VERSION == 4
 
 
 def test_input_dim_and_workspace_queries():
@@ -216,3 +216,86 @@ def test_index_error_watch_ring():
         held.append(s)
     s, _ = w.reserve()
     assert held[0] not in w.pending and s is not None
+
+
+def test_index_error_watch_orphans_and_dead_writer():
+    """(1) a slot whose call drained its stream without storing
+    the word (the writer never ran: a sticky error, a failed launch after
+    commit) raises RuntimeError instead of spinning forever, and the slot
+    returns to the ring; a stream error raised by the query propagates.
+    (2) Slots still PENDING when an IndexError drops the pending list become
+    orphans and return to the ring once their word lands, so repeated bad ids
+    never exhaust the 64-slot ring."""
+    from dcnr.model import IndexErrorWatch
+
+    class FakeStream:
+        def __init__(self, idle=True, err=None):
+            self.idle, self.err = idle, err
+
+        def query(self):
+            if self.err:
+                raise RuntimeError(self.err)
+            return self.idle
+
+    w = IndexErrorWatch()
+    w.SPIN_S = 1e-4
+    w.ring = torch.zeros(IndexErrorWatch.RING, dtype=torch.int32)
+    w.view = w.ring.numpy()
+    n_free = len(w.free)
+    s, _ = w.reserve()
+    w.commit(s, FakeStream(idle=True))         # drained, word never stored
+    with pytest.raises(RuntimeError, match="never stored"):
+        w.poll(all_=True)
+    assert w.pending == [] and s in w.free and len(w.free) == n_free
+    s, _ = w.reserve()
+    w.commit(s, FakeStream(err="hipErrorLaunchFailure"))
+    with pytest.raises(RuntimeError, match="LaunchFailure"):
+        w.poll(all_=True)
+    w.cancel(w.pending.pop())                  # (the caller's cleanup)
+    # orphans: a bad word drops two later calls still in flight
+    a, _ = w.reserve(); w.commit(a, FakeStream(idle=False))
+    b, _ = w.reserve(); w.commit(b, FakeStream(idle=False))
+    c, _ = w.reserve(); w.commit(c, FakeStream(idle=False))
+    w.view[a] = 1
+    with pytest.raises(IndexError):
+        w.poll()
+    assert w.pending == [] and sorted(w.orphans) == sorted([b, c])
+    assert b not in w.free and c not in w.free
+    w.view[b] = 0                              # b's late store lands
+    w.poll()
+    assert b in w.free and w.orphans == [c]
+    w.view[c] = 0
+    w.poll()
+    assert w.orphans == [] and c in w.free
+    # many bad calls never leak slots
+    for _ in range(3 * IndexErrorWatch.RING):
+        x, _ = w.reserve(); w.commit(x, FakeStream(idle=False))
+        y, _ = w.reserve(); w.commit(y, FakeStream(idle=False))
+        w.view[x] = 1
+        with pytest.raises(IndexError):
+            w.poll()
+        w.view[y] = 0
+    w.poll()
+    assert len(w.free) + len(w.orphans) + len(w.pending) == IndexErrorWatch.RING
+    assert w.orphans == []
+
+
+def test_row_map_workspace_is_last():
+    """DCNR_FLAG_ROW_MAP (ABI 4) appends a byte per table row to the train
+    workspace and moves nothing else: every other stored tensor keeps its
+    offset; eval and flag-less train workspaces have no map."""
+    from dcnr import _lib
+    m = our_model(gc.CFG3R, precision="bf16")
+    B = 1024
+    F = _lib.FLAG_ROW_MAP
+    rows = gc.CFG3R["n_users"] + gc.CFG3R["n_items"] + sum(gc.CFG3R["cat_dims"].values())
+    assert m.workspace_offset(B, _lib.TRAIN, "row_map") == -1
+    assert m.workspace_offset(B, _lib.EVAL, "row_map", extra_flags=F) == -1
+    off = m.workspace_offset(B, _lib.TRAIN, "row_map", extra_flags=F)
+    assert off > 0
+    assert m.workspace_bytes(B, _lib.TRAIN, F) >= off + rows
+    assert m.workspace_bytes(B, _lib.TRAIN, F) - m.workspace_bytes(B, _lib.TRAIN) >= rows
+    for kind in _lib.WS_KINDS[:-1]:
+        for idx in (0, 1):
+            assert m.workspace_offset(B, _lib.TRAIN, kind, idx) == \
+                m.workspace_offset(B, _lib.TRAIN, kind, idx, extra_flags=F), kind
