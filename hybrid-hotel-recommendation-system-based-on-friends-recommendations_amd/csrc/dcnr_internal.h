@@ -86,6 +86,22 @@ __device__ __forceinline__ void dma16(u32x4 rsrc, int off, uint32_t lds_dst) {
       : "memory");
 }
 
+// dma16's form with the uniform part of the offset in an SGPR (soff): a
+// stream of pieces then costs one VGPR per lane pattern however many pieces
+// a wave issues.
+__device__ __forceinline__ void dma16s(u32x4 rsrc, int voff, int soff, uint32_t lds_dst) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rsrc), "s"(lds_dst), "s"(soff)
+      : "memory");
+}
+
 __device__ __forceinline__ u32x4 rsrc_words(const void* p, int64_t bytes) {
   const uint64_t a = (uint64_t)p;
   return u32x4{(uint32_t)a, (uint32_t)(a >> 32) & 0xFFFFu, p ? (uint32_t)bytes : 0u, 0x00020000u};
@@ -359,6 +375,10 @@ struct NtArgs {
   int nslices, groups; int64_t mtiles;   // filled by gemm_ws
 };
 bool gemm_ws_supported(int64_t K, int64_t N);
+// the train forward's BIAS / BIAS_STATS epilogues at 256 < K <= 512: the
+// pipelined one-wave-per-SIMD variant (gemm_wsp.hip), taken by gemm_ws
+bool gemm_wsp_supported(int epi, int64_t K, int64_t N);
+dcnr_status gemm_wsp(int epi, const NtArgs& a, hipStream_t s, int* nparts);
 // nparts (stats epilogues): rows of part written (the nchunks of reduce_fused)
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
 // head partials of NT_EPI_BN_RESID_RELU_HEAD: rows of headp written (0: unsupported shape)

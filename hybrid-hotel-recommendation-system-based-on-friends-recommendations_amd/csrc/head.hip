@@ -133,33 +133,66 @@ static_assert(sizeof(AdamBatch) <= 4096, "kernel argument size");
 //   AdamW: p *= 1 - lr*wd ; Adam: g += wd*p
 //   m = lerp(m, g, 1-b1) ; v = b2*v + (1-b2)*g*g
 //   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+__device__ __forceinline__ void adam_elem(float& pp, float gg, float& mm, float& vv, float lr, float b1,
+                                          float b2, float eps, float wd, float step_size,
+                                          float bc2_sqrt, int decoupled) {
+  if (decoupled) pp = pp * (1.f - lr * wd);
+  else if (wd != 0.f) gg = gg + wd * pp;
+  mm = mm + (1.f - b1) * (gg - mm);
+  vv = vv * b2 + (1.f - b2) * gg * gg;
+  float denom = sqrtf(vv) / bc2_sqrt + eps;
+  pp = pp - step_size * (mm / denom);
+}
+
+// One thread per 4 consecutive elements (16-B loads and stores where the
+// tensor's four arrays are 16-B aligned, else element by element).
 __global__ __launch_bounds__(NT) void adam_kernel(AdamBatch ab, float lr, float b1, float b2,
                                                   float eps, float wd, float step_size,
                                                   float bc2_sqrt, int decoupled) {
   int t = 0;
   while (t + 1 < ab.nt && (int64_t)blockIdx.x >= ab.blk0[t + 1]) ++t;
-  const int64_t base = ((int64_t)blockIdx.x - ab.blk0[t]) * (NT * 4);
+  const int64_t i0 = ((int64_t)blockIdx.x - ab.blk0[t]) * (NT * 4) + threadIdx.x * 4;
   float* p = ab.p[t];
   const float* g = ab.g[t];
   float* m = ab.m[t];
   float* v = ab.v[t];
   const int64_t n = ab.n[t];
+  if (i0 >= n) return;
   const uint8_t* map = ab.map[t];
   const uint32_t rw = (uint32_t)ab.rw[t];
+  // an unmarked row's gradient is exactly 0 and is not read (the same
+  // arithmetic as a stored +0: m, v decay, weight decay, the update)
+  bool gr[4];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    int64_t i = base + u * NT + threadIdx.x;
+  for (int e = 0; e < 4; ++e) gr[e] = !map || (i0 + e < n && map[(uint32_t)(i0 + e) / rw]);
+  const bool vec = i0 + 4 <= n && ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0);
+  if (vec) {
+    float4 pp = *reinterpret_cast<const float4*>(p + i0);
+    float4 mm = *reinterpret_cast<const float4*>(m + i0);
+    float4 vv = *reinterpret_cast<const float4*>(v + i0);
+    float4 gg = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (gr[0] || gr[1] || gr[2] || gr[3]) {
+      gg = *reinterpret_cast<const float4*>(g + i0);
+      if (!gr[0]) gg.x = 0.f;
+      if (!gr[1]) gg.y = 0.f;
+      if (!gr[2]) gg.z = 0.f;
+      if (!gr[3]) gg.w = 0.f;
+    }
+    adam_elem(pp.x, gg.x, mm.x, vv.x, lr, b1, b2, eps, wd, step_size, bc2_sqrt, decoupled);
+    adam_elem(pp.y, gg.y, mm.y, vv.y, lr, b1, b2, eps, wd, step_size, bc2_sqrt, decoupled);
+    adam_elem(pp.z, gg.z, mm.z, vv.z, lr, b1, b2, eps, wd, step_size, bc2_sqrt, decoupled);
+    adam_elem(pp.w, gg.w, mm.w, vv.w, lr, b1, b2, eps, wd, step_size, bc2_sqrt, decoupled);
+    *reinterpret_cast<float4*>(p + i0) = pp;
+    *reinterpret_cast<float4*>(m + i0) = mm;
+    *reinterpret_cast<float4*>(v + i0) = vv;
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int64_t i = i0 + e;
     if (i >= n) break;
-    // an unmarked row's gradient is exactly 0 and is not read (the same
-    // arithmetic as a stored +0: m, v decay, weight decay, the update)
-    const bool gr = !map || map[(uint32_t)i / rw];
-    float pp = p[i], gg = gr ? g[i] : 0.f, mm = m[i], vv = v[i];
-    if (decoupled) pp = pp * (1.f - lr * wd);
-    else if (wd != 0.f) gg = gg + wd * pp;
-    mm = mm + (1.f - b1) * (gg - mm);
-    vv = vv * b2 + (1.f - b2) * gg * gg;
-    float denom = sqrtf(vv) / bc2_sqrt + eps;
-    pp = pp - step_size * (mm / denom);
+    float pp = p[i], gg = gr[e] ? g[i] : 0.f, mm = m[i], vv = v[i];
+    adam_elem(pp, gg, mm, vv, lr, b1, b2, eps, wd, step_size, bc2_sqrt, decoupled);
     p[i] = pp; m[i] = mm; v[i] = vv;
   }
 }

@@ -42,23 +42,6 @@ constexpr int TW_SLOT = 2 * TW_KT0 * 1024 + 256;   // ring slot: 2 output blocks
 constexpr int TW_CONST = 2 * TW_KT0 * 1024;   // constants' offset in a slot: sc[32], sh[32]
 constexpr int TW_NSLOT = 4;   // (3 slots: 636 vs 622 us per bench-size call, tools/tower_lab.sh)
 
-// LDS-DMA of 16 B per lane: voff (per lane) + soff (wave-uniform) into
-// lds_dst + 16 * lane.  dma16's form with the uniform part of the offset in
-// an SGPR, so the weight stream costs one VGPR (lane * 16) however many
-// pieces a wave issues.
-__device__ __forceinline__ void dma16s(u32x4 rsrc, int voff, int soff, uint32_t lds_dst) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rsrc), "s"(lds_dst), "s"(soff)
-      : "memory");
-}
-
 typedef float f2v __attribute__((ext_vector_type(2)));
 typedef bf16 bf16x2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk2(float a, float b) {

@@ -15,6 +15,7 @@ for e in "$@"; do sed -i "$e" $src; done
 if cmp -s $C/$f $src; then echo "lab_sed: no edit applied" >&2; exit 1; fi
 extra=""
 [ "$f" = tower.hip ] && extra="-mllvm -amdgpu-mfma-vgpr-form"
+[ "$f" = gemm_wsp.hip ] && extra="-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC $extra -I$C -c $src -o tools/lab_bin/src/${name}.o
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o tools/lab_bin/libdcnr_$name.so \
   $(ls $B/*.o | grep -v "/${f%.hip}.o\$") tools/lab_bin/src/${name}.o

@@ -20,6 +20,8 @@ import re
 import sys
 
 GROUPS = [
+    ("gemm_wsp<0,0> fwd BIAS (pipelined)", r"gemm_wsp_kernel<false, false>"),
+    ("gemm_wsp<1,0> fwd BIAS_STATS (pipelined)", r"gemm_wsp_kernel<true, false>"),
     ("gemm_ws<16,0> fwd BIAS (initial Linear)", r"gemm_ws_kernel<16, 0>"),
     ("gemm_ws<16,3> fwd BIAS_STATS (BN inputs)", r"gemm_ws_kernel<16, 3>"),
     ("gemm_ws<16,4> dX RESID_BN", r"gemm_ws_kernel<16, 4>"),
