@@ -375,10 +375,6 @@ struct NtArgs {
   int nslices, groups; int64_t mtiles;   // filled by gemm_ws
 };
 bool gemm_ws_supported(int64_t K, int64_t N);
-// the train forward's BIAS / BIAS_STATS epilogues at 256 < K <= 512: the
-// pipelined one-wave-per-SIMD variant (gemm_wsp.hip), taken by gemm_ws
-bool gemm_wsp_supported(int epi, int64_t K, int64_t N);
-dcnr_status gemm_wsp(int epi, const NtArgs& a, hipStream_t s, int* nparts);
 // nparts (stats epilogues): rows of part written (the nchunks of reduce_fused)
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
 // head partials of NT_EPI_BN_RESID_RELU_HEAD: rows of headp written (0: unsupported shape)

@@ -524,7 +524,6 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
     set_error("gemm_ws: unsupported K=%d N=%d / missing epilogue operand", a.K, a.N);
     return DCNR_UNSUPPORTED_SHAPE;
   }
-  if (gemm_wsp_supported(epi, a.K, a.N)) return gemm_wsp(epi, a, s, nparts);
   switch (epi) {
     case NT_EPI_BIAS: return dispatch_ws<NT_EPI_BIAS>(a, s, nparts);
     case NT_EPI_F32: return dispatch_ws<NT_EPI_F32>(a, s, nparts);

@@ -136,12 +136,17 @@ static_assert(sizeof(AdamBatch) <= 4096, "kernel argument size");
 __device__ __forceinline__ void adam_elem(float& pp, float gg, float& mm, float& vv, float lr, float b1,
                                           float b2, float eps, float wd, float step_size,
                                           float bc2_sqrt, int decoupled) {
+  // every fused multiply-add spelled out, no other contraction: the 16-B
+  // path and the element path (a tensor's unaligned tail, a mapped table's
+  // last partial group) then round alike -- left to the compiler they
+  // differed by an ulp of v
+#pragma clang fp contract(off)
   if (decoupled) pp = pp * (1.f - lr * wd);
-  else if (wd != 0.f) gg = gg + wd * pp;
-  mm = mm + (1.f - b1) * (gg - mm);
-  vv = vv * b2 + (1.f - b2) * gg * gg;
-  float denom = sqrtf(vv) / bc2_sqrt + eps;
-  pp = pp - step_size * (mm / denom);
+  else if (wd != 0.f) gg = fmaf(wd, pp, gg);
+  mm = fmaf(1.f - b1, gg - mm, mm);
+  vv = fmaf(vv, b2, (1.f - b2) * gg * gg);
+  const float denom = sqrtf(vv) / bc2_sqrt + eps;
+  pp = fmaf(-step_size, mm / denom, pp);
 }
 
 // One thread per 4 consecutive elements (16-B loads and stores where the

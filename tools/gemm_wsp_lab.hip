@@ -1,3 +1,7 @@
+// LAB (not built into libdcnr): the round-5 pipelined forward GEMM, kept for
+// reference -- faster on the BIAS epilogue (67 vs 72 us) but nondeterministic
+// inside the full train step; build it with
+// tools/lab_sed.sh-style one-file lab builds only.
 // Pipelined weight-stationary GEMM for the bf16 deep tower's train forward
 // (gfx950): the initial Linear and both Linears of every ResBlock
 // (train.py:143, 105, 109 under :161-165),
