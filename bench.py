@@ -302,7 +302,7 @@ def bench_cfg5(dev, iters, cpu):
             pass
         out["roofline" if Q == 1 else f"roofline_q{Q}"] = {
             "traffic": knn_pmc.get(f"topk_q{Q}"),   # PMC HBM bytes per call (whole chain)
-            "bound": "hbm", "kernel": "kth_bound + scan4 (bf16 MFMA%s) + rescore (dcnr_cosine_topk, Q=%d)"
+            "bound": "hbm", "kernel": "bound5 (+ merge) + scan4 (bf16 MFMA%s) + rescore (dcnr_cosine_topk, Q=%d)"
             % (" over the fit-time bf16 copy" if packed else "", Q),
             "achieved": nbytes / t / 1e9, "peak": PEAK_HBM / 1e9, "unit": "GB/s",
             "frac": nbytes / t / PEAK_HBM, "bytes_per_call": nbytes,

@@ -461,13 +461,12 @@ constexpr float TH_MARGIN = 1e-5f;
 // a 2-pass radix select over the distances' bits (exponent + 7 mantissa
 // bits): the upper edge of the selected bin, an upper bound within 2^-7
 // relative of the exact k-th value.
-template <int DV, int SAMPLE = TH_S, int NTB = 256>
+template <int DV, int NTB = 256>
 __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict__ tab,
                                                         const float* __restrict__ inv, int64_t N,
                                                         const float* __restrict__ q, float* qn,
-                                                        int k, float* thr0, bf16* qb = nullptr,
-                                                        int* qcnt = nullptr) {
-  constexpr int PT = SAMPLE / NTB;
+                                                        int k, float* thr0) {
+  constexpr int PT = TH_S / NTB;
   constexpr int d = DV * 4;   // <= 64: one element per lane
   __shared__ unsigned hist[256];
   __shared__ unsigned sel_prefix, sel_need;
@@ -482,13 +481,11 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
     if (lane < d) {
       qs[lane] = v * in;
       qn[qq * d + lane] = v * in;
-      if (qb) qb[qq * d + lane] = (bf16)(v * in);
     }
-    if (qcnt && lane == 0) qcnt[qq] = 0;
   }
   __syncthreads();
   const float4* qv = reinterpret_cast<const float4*>(qs);
-  const int S = (int)min<int64_t>(N, SAMPLE);
+  const int S = (int)min<int64_t>(N, TH_S);
   unsigned key[PT];
 #pragma unroll 4
   for (int j = 0; j < PT; ++j) {
@@ -567,21 +564,20 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 // <= T0 (the k-th best of a V4_S-row exact sample: any subset's k-th best
 // bounds the table's), hence coarse distance <= T0 + V4_EPS: admitting the
 // rows under that bound keeps every true neighbour, ties included.  T0 comes
-// from the same machinery run on the sample under kth_bound_kernel's 512-row
-// (Q >= 128: 1024-row) bound (pass 1).  The admitted rows (~N k / V4_S per query) are
-// appended to a per-query list with their exact fp32 distances (scan v2's
-// arithmetic, computed in scan4's epilogue); rescore_kernel selects the k
-// best by (distance, row).  A query whose list overflows V4_CAP (the count
-// word carries V4_OVF when a block's wave list ran out of room), or whose
-// k-th distance is shared by more than V4_SCAP rows, is answered by an exact
-// scan of the whole table inside its own rescore block (scan v2's per-wave
-// lists and arithmetic): no batch-wide flag, no gated launches behind the
-// chain.  In pass 1 the same conditions just keep the 512-row bound.
+// from bound5_kernel (exact distances of the sample rows, per-block k-lists,
+// merged by the last-arriving block).  The admitted rows (~N k / V4_S per
+// query) are appended to a per-query list with their exact fp32 distances
+// (scan v2's arithmetic, computed in scan4's epilogue); rescore_kernel
+// selects the k best by (distance, row).  A query whose list overflows
+// V4_CAP (the count word carries V4_OVF when a block's wave list ran out of
+// room), or whose k-th distance is shared by more than V4_SCAP rows, is
+// answered by an exact scan of the whole table inside its own rescore block
+// (scan v2's per-wave lists and arithmetic): no batch-wide flag, no gated
+// launches behind the chain.  Three launches per call: bound5, scan4,
+// rescore.
 constexpr float V4_EPS = 0.004f;
-constexpr int V4_S = 32768;     // exact sample rows for the admission bound (larger first
-                                // bound samples measured slower: DESIGN.md section 4)
+constexpr int V4_S = 65536;     // sample rows for the admission bound
 constexpr int V4_WPS = 3;       // min waves per SIMD of scan4 for NQB > 4
-constexpr int V4_SNQ = 16;      // query blocks per launch row of the sample pass (Q=256: 31 vs 43 us at 2)
 constexpr int V4_CAP = 4096;     // admitted rows per query
 constexpr int V4_SCAP = 256;     // rows at or under the selected k-th bin
 constexpr int V4_OVF = 1 << 30;  // count-word mark: a block dropped some of this query's rows
@@ -684,6 +680,178 @@ __device__ __forceinline__ void v4_load_rows(const float* __restrict__ tab, int6
   }
 }
 
+// ------------------------------------------------- scan v4 admission bound
+// Replaces the round-4 sample chain (512-row bound -> sample scan -> sample
+// rescore, three launches).  bound5_kernel: B5_G blocks per group of 16
+// queries each score B5_C of the first V4_S table rows with scan4's coarse
+// bf16 MFMA cosine and store each query's smallest coarse distance over them;
+// v4_kth_bound then takes the k-th smallest M of those block minima.  k
+// distinct rows (one per block) have coarse distance <= M, hence exact
+// distance <= M + V4_EPS, so E_k <= T0 = M + V4_EPS: the same kind of bound
+// the exact sample k-th gave (scan4 admits coarse <= T0 + V4_EPS), a rank or
+// two looser when two of the sample's k best share a block.  The minima are
+// merged where they are used -- in scan4's prologue for up to V4_MQ queries,
+// by bound5_merge_kernel above that -- so no block waits on another (a
+// last-arriving-block merge cost a device-scope release per block: 140 us
+// at Q = 256, profiles/lab/r05_knn_bound_lab.txt).  Blocks of column 0 also
+// write the normalised fp32 / bf16 queries (kth_bound_kernel's arithmetic)
+// and zero the list counts for scan4.
+constexpr int B5_C = 512;           // sample rows per block (4 waves x 8 row tiles)
+constexpr int B5_G = V4_S / B5_C;   // blocks per query group (<= 128: two minima per lane)
+constexpr int B5_QG = 4;            // 16-query groups per block past V4_MQ queries (rows loaded once
+                                    // for them; at or under V4_MQ one group per block)
+constexpr int V4_MQ = 32;           // queries up to which scan4 merges the minima itself
+static_assert(B5_G <= 128, "the merge holds two block minima per lane");
+
+// one query's ng block minima as two per lane (block g: lane g % 64, slot g / 64)
+struct Mins2 { unsigned u0, u1; };
+__device__ __forceinline__ Mins2 v4_load_mins(const float* mq, int ng, int lane) {
+  return Mins2{lane < ng ? __float_as_uint(mq[lane]) : 0x7f7fffffu,
+               lane + 64 < ng ? __float_as_uint(mq[lane + 64]) : 0x7f7fffffu};
+}
+// wave-wide: the admission bounds of MQ queries from their block minima:
+// the k-th smallest by a bitwise search over their non-negative float bits,
+// down to 10 mantissa bits, and the upper edge of that bin (>= the k-th,
+// within 2^-10 relative: 5e-4 at the usual bounds against V4_EPS = 0.004).
+// The MQ searches are interleaved (each step's ballot -> count -> select is
+// otherwise one dependent chain).  Every lane returns the bounds.
+constexpr int V4_LOWBIT = 13;
+template <int MQ>
+__device__ __forceinline__ void v4_kth_bounds(const Mins2 (&m)[MQ], int ng, int k, float (&out)[MQ]) {
+  unsigned ans[MQ];
+#pragma unroll
+  for (int j = 0; j < MQ; ++j) ans[j] = 0;
+  for (int b = 30; b >= V4_LOWBIT; --b) {
+#pragma unroll
+    for (int j = 0; j < MQ; ++j) {
+      const unsigned t = ans[j] | (1u << b);
+      if (__popcll(__ballot(m[j].u0 < t)) + __popcll(__ballot(m[j].u1 < t)) < k) ans[j] = t;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < MQ; ++j) {
+    const float M = __uint_as_float(ans[j] | ((1u << V4_LOWBIT) - 1));
+    out[j] = ng >= k && M < 2.5f ? M + V4_EPS + TH_MARGIN : FLT_MAX;
+  }
+}
+
+template <int KS, bool PK, int QG>
+__global__ __launch_bounds__(256) void bound5_kernel(const float* __restrict__ tab, const float* __restrict__ inv,
+                                                     const bf16* __restrict__ tb, int64_t N,
+                                                     const float* __restrict__ q, int64_t Q, float* qn,
+                                                     bf16* qb, int* qcnt, float* mins) {
+  constexpr int D = KS * 32;    // 32 or 64: one query element per lane
+  constexpr int U = B5_C / 64;  // row tiles per wave
+  constexpr int QB = 16 * QG;
+  __shared__ __attribute__((aligned(16))) float qs[QB][D];
+  __shared__ float wbest[4][QB];
+  const int g = blockIdx.x;
+  const int64_t q0 = (int64_t)blockIdx.y * QB;
+  const int nq = (int)min<int64_t>(QB, Q - q0);
+  const int ngr = (nq + 15) / 16;   // 16-query groups present
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int r16 = lane & 15, gl = lane >> 4;
+  const int64_t S = min<int64_t>(N, V4_S);
+  // the block's row tiles first (wave w: rows r0 + 16 u + r16), as scan4 loads them
+  const int64_t r0 = (int64_t)g * B5_C + (B5_C / 4) * w;
+  using Frag = typename std::conditional<PK, bf16x8[KS], float4[KS][2]>::type;
+  Frag x[U];
+  float iv[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t r = min<int64_t>(r0 + 16 * u + r16, S - 1);
+    if constexpr (PK) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) x[u][ks] = *reinterpret_cast<const bf16x8*>(tb + r * D + ks * 32 + 8 * gl);
+    } else {
+      v4_load_rows<KS>(tab, r, x[u], gl);
+      iv[u] = inv[r];
+    }
+  }
+  // kth_bound_kernel's normalisation, the wave's query loads all in flight first
+  float qv[QB / 4];
+#pragma unroll
+  for (int j = 0; j < QB / 4; ++j) {
+    const int qq = w + 4 * j;
+    qv[j] = qq < nq && lane < D ? q[(q0 + qq) * D + lane] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < QB / 4; ++j) {
+    const int qq = w + 4 * j;
+    if (qq >= 16 * ngr) break;
+    const float v = qv[j];
+    const float ss = wave_sum(v * v);
+    const float in = ss > 0.f ? 1.f / sqrtf(ss) : 1.f;
+    if (lane < D) {
+      qs[qq][lane] = v * in;
+      if (g == 0 && qq < nq) {
+        qn[(q0 + qq) * D + lane] = v * in;
+        qb[(q0 + qq) * D + lane] = (bf16)(v * in);
+      }
+    }
+    if (g == 0 && qq < nq && lane == 0) qcnt[q0 + qq] = 0;
+  }
+  __syncthreads();
+  // the row tiles' A fragments (bf16, as scan4 rounds them)
+  bf16x8 a[U][KS];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if constexpr (PK) {
+        a[u][ks] = x[u][ks];
+      } else {
+        const float4 p = x[u][ks][0], v = x[u][ks][1];
+        const float sc = iv[u];
+        a[u][ks] = bf16x8{(bf16)(p.x * sc), (bf16)(p.y * sc), (bf16)(p.z * sc), (bf16)(p.w * sc),
+                          (bf16)(v.x * sc), (bf16)(v.y * sc), (bf16)(v.z * sc), (bf16)(v.w * sc)};
+      }
+    }
+  for (int gr = 0; gr < ngr; ++gr) {
+    // B fragment of lane (c = r16, gl): query 16 gr + c's k-chunk [32 ks + 8 gl, +8)
+    bf16x8 bq[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const float4 lo = *reinterpret_cast<const float4*>(&qs[16 * gr + r16][ks * 32 + 8 * gl]);
+      const float4 hi = *reinterpret_cast<const float4*>(&qs[16 * gr + r16][ks * 32 + 8 * gl + 4]);
+      bq[ks] = bf16x8{(bf16)lo.x, (bf16)lo.y, (bf16)lo.z, (bf16)lo.w, (bf16)hi.x, (bf16)hi.y, (bf16)hi.z, (bf16)hi.w};
+    }
+    // best coarse cosine of each query over the block's rows
+    float best = -FLT_MAX;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[u][ks], bq[ks], acc, 0, 0, 0);
+      // lane (c, gl): rows r0 + 16 u + 4 gl + i of query c
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (r0 + 16 * u + 4 * gl + i < S) best = fmaxf(best, acc[i]);
+    }
+    best = fmaxf(best, __shfl_xor(best, 16, 64));
+    best = fmaxf(best, __shfl_xor(best, 32, 64));
+    if (lane < 16) wbest[w][16 * gr + lane] = best;
+  }
+  __syncthreads();
+  if (threadIdx.x < nq) {
+    const int c = threadIdx.x;
+    const float bc = fmaxf(fmaxf(wbest[0][c], wbest[1][c]), fmaxf(wbest[2][c], wbest[3][c]));
+    // (clamped at 0, which only raises a minimum and so keeps the bound valid)
+    mins[(q0 + c) * B5_G + g] = fmaxf(1.f - bc, 0.f);
+  }
+}
+
+// more than V4_MQ queries: one wave per query merges its minima into thr0
+__global__ __launch_bounds__(256) void bound5_merge_kernel(const float* __restrict__ mins, int ng, int64_t Q,
+                                                           int k, float* thr0) {
+  const int64_t qq = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (qq >= Q) return;
+  const Mins2 m[1] = {v4_load_mins(mins + qq * B5_G, ng, threadIdx.x & 63)};
+  float t[1];
+  v4_kth_bounds<1>(m, ng, k, t);
+  if ((threadIdx.x & 63) == 0) thr0[qq] = t[0];
+}
+
 // Admissions go to a wave-private LDS list whose fill count is wave-uniform
 // (ballots + mbcnt, no atomic at all inside the loop: a returning global
 // atomic there put its contended round trip in every tile, a returning LDS
@@ -703,7 +871,8 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
                                                     const bf16* __restrict__ qb,
                                                     const float* __restrict__ thr0,
                                                     const float* __restrict__ qn, int64_t Q, int* qcnt,
-                                                    int* rows, float* dists) {
+                                                    int* rows, float* dists,
+                                                    const float* __restrict__ bmins, int ng, int k) {
   constexpr int D = KS * 32;
   // up to 4 query blocks the B fragments live in registers; beyond that
   // (64+ KS x 4 VGPRs) in LDS, stored in fragment order -- entry (b, ks,
@@ -714,6 +883,7 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
   __shared__ int lq[V4_LIST];     // admitted (query, row) pairs of the block
   __shared__ int lr[V4_LIST];
   __shared__ int qn_[NQB * 16];   // per-query counts, then this block's bases
+  __shared__ float thl[NQB * 16]; // (bmins) the block's admission bounds
   __shared__ int wcnt[4];
   __shared__ bf16x8 bqs[BL ? NQB * KS * 64 : 1];
   const int64_t qc0 = (int64_t)blockIdx.y * (NQB * 16);
@@ -742,6 +912,14 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
       }
     }
   };
+  // (bound5 minima to merge: loaded before everything else, so the merge
+  // waits for them alone and runs under the row tiles' loads)
+  constexpr int MWMAX = NQB * 16 <= V4_MQ ? NQB * 16 / 4 : 1;
+  Mins2 mm[MWMAX];
+  if constexpr (NQB * 16 <= V4_MQ) if (bmins) {
+#pragma unroll
+    for (int j = 0; j < MWMAX; ++j) mm[j] = v4_load_mins(bmins + (qc0 + min(w + 4 * j, nq - 1)) * B5_G, ng, lane);
+  }
   const int64_t first = r0 + 16 * w;
 #pragma unroll
   for (int u = 0; u < PF; ++u) load(first + 64 * u, x[u], iv[u]);
@@ -764,10 +942,31 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
         bq[b][ks] = qi < nq ? v : bf16x8{};
       }
     }
-    const float t = thr0[qs];
-    // a row passes iff its coarse cosine is >= 1 - bound; the 1e-6 below
-    // covers the rounding of 1 - bound (query slots past nq: 2, never)
-    th[b] = qi < nq ? (1.f - (t + V4_EPS)) - 1e-6f : 2.f;
+    if (!bmins) {
+      const float t = thr0[qs];   // (bound5_merge_kernel's)
+      // a row passes iff its coarse cosine is >= 1 - bound; the 1e-6 below
+      // covers the rounding of 1 - bound (query slots past nq: 2, never)
+      th[b] = qi < nq ? (1.f - (t + V4_EPS)) - 1e-6f : 2.f;
+    }
+  }
+  // few queries (V4_MQ: NQB = 2): merge their bound5 minima here, a wave per query
+  if constexpr (NQB * 16 <= V4_MQ) if (bmins) {
+    auto merge = [&](auto mw_c) {
+      constexpr int MW = decltype(mw_c)::value;   // queries per wave
+      Mins2 m2[MW];
+#pragma unroll
+      for (int j = 0; j < MW; ++j) m2[j] = mm[j];
+      float tj[MW];
+      v4_kth_bounds<MW>(m2, ng, k, tj);
+#pragma unroll
+      for (int j = 0; j < MW; ++j) {
+        const int qq = w + 4 * j;
+        if (qq < nq && lane == 0) thl[qq] = tj[j];
+      }
+    };
+    if (nq <= 4) merge(std::integral_constant<int, 1>{});
+    else if (nq <= 16) merge(std::integral_constant<int, 4>{});
+    else merge(std::integral_constant<int, NQB * 16 / 4>{});
   }
   if constexpr (BL) {
     constexpr int PER = NQB * KS * 64 / 256;
@@ -782,6 +981,13 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
   }
   for (int i = threadIdx.x; i < NQB * 16; i += 256) qn_[i] = 0;
   __syncthreads();
+  if constexpr (NQB * 16 <= V4_MQ) if (bmins) {
+#pragma unroll
+    for (int b = 0; b < NQB; ++b) {
+      const int qi = 16 * b + r16;
+      th[b] = qi < nq ? (1.f - (thl[qi] + V4_EPS)) - 1e-6f : 2.f;
+    }
+  }
   for (int64_t b0 = first; b0 < r1; b0 += 64 * PF) {
 #pragma unroll
     for (int u = 0; u < PF; ++u) {
@@ -996,16 +1202,12 @@ __device__ void exact_query_topk(const float* __restrict__ tab, const float* __r
 
 // One block per query: the exact distances of its admitted rows (computed
 // by scan4's epilogue), the k-th smallest by block_select_kth, then a bitonic
-// sort of the rows at or under the selected bin by (distance, row).  SMP: the
-// pass over the V4_S-row sample -- its exact k-th distance becomes the
-// query's admission bound thr0 for the table scan (left at the 512-row bound
-// when the sample list overflowed), and the list count is reset for it.
-// Otherwise a query whose list overflowed takes exact_query_topk (DV = d / 4).
-template <bool SMP, int DV>
-__global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__ dists, int* qcnt,
+// sort of the rows at or under the selected bin by (distance, row).  A query
+// whose list overflowed takes exact_query_topk (DV = d / 4).
+template <int DV>
+__global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__ dists, const int* qcnt,
                                                        const int* rows, int k, int64_t* idx,
-                                                       float* dist, float* thr0,
-                                                       const float* __restrict__ tab,
+                                                       float* dist, const float* __restrict__ tab,
                                                        const float* __restrict__ inv, int64_t N,
                                                        const float* __restrict__ qn) {
   __shared__ float dl[V4_CAP];
@@ -1015,12 +1217,8 @@ __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__
   static_assert(V4_CAP >= 2 * B4_T, "exact fallback lists live in dl");
   const int64_t qq = blockIdx.x;
   auto fail = [&]() {
-    if constexpr (SMP) {
-      if (threadIdx.x == 0) qcnt[qq] = 0;   // pass 2 runs under the 512-row bound
-    } else {
-      __syncthreads();   // (dl is reused)
-      exact_query_topk<DV>(tab, inv, N, qn + qq * DV * 4, k, dl, idx + qq * k, dist + qq * k);
-    }
+    __syncthreads();   // (dl is reused)
+    exact_query_topk<DV>(tab, inv, N, qn + qq * DV * 4, k, dl, idx + qq * k, dist + qq * k);
   };
   const int n = qcnt[qq];
   if (n > V4_CAP || n < k) {   // overflow (fewer than k admitted rows only when N < k)
@@ -1044,22 +1242,27 @@ __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__
     fail();
     return;
   }
+  if (nv <= 64) {   // (the usual case) one wave's register sort, no more barriers
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      float d = lane < nv ? cd[lane] : FLT_MAX;
+      int i = lane < nv ? ci[lane] : INT_MAX;
+      wave_sort64(d, i, lane);
+      if (lane < k) {
+        idx[qq * k + lane] = (int64_t)i;
+        dist[qq * k + lane] = d;
+      }
+    }
+    return;
+  }
   int n2 = 2;
   while (n2 < nv) n2 <<= 1;
   for (int t = nv + threadIdx.x; t < n2; t += B4_T) { cd[t] = FLT_MAX; ci[t] = INT_MAX; }
   __syncthreads();
   bitonic<B4_T>(cd, ci, n2);
-  if constexpr (SMP) {
-    if (threadIdx.x == 0) {
-      const float kd = cd[k - 1];
-      thr0[qq] = kd < 2.5f ? kd + TH_MARGIN : FLT_MAX;
-      qcnt[qq] = 0;
-    }
-  } else {
-    for (int t = threadIdx.x; t < k; t += B4_T) {
-      idx[qq * k + t] = (int64_t)ci[t];
-      dist[qq * k + t] = cd[t];
-    }
+  for (int t = threadIdx.x; t < k; t += B4_T) {
+    idx[qq * k + t] = (int64_t)ci[t];
+    dist[qq * k + t] = cd[t];
   }
 }
 
@@ -1371,9 +1574,11 @@ bool use_v4(int64_t N, int64_t Q, int d, int k) {
 
 // v4 scratch after the v2 layout (cands | qn [Q][d] | thr0 [Q]): bf16
 // queries [Q][d] | per-query counts [Q] | admitted rows [Q][V4_CAP]
-// | their exact distances [Q][V4_CAP]
+// | their exact distances [Q][V4_CAP] | the bound's block minima
+// [Q][B5_G]
 size_t v4_extra(int64_t Q, int d) {
-  return rup((size_t)Q * d * 2, 256) + rup((size_t)Q * 4 + 4, 256) + 2 * (size_t)Q * V4_CAP * 4 + 256;
+  return rup((size_t)Q * d * 2, 256) + rup((size_t)Q * 4 + 4, 256) + 2 * (size_t)Q * V4_CAP * 4 +
+         rup((size_t)Q * B5_G * 4, 256) + 256;
 }
 
 size_t topk_ws_d(int64_t N, int64_t Q, int k, int d) {
@@ -1432,6 +1637,7 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
     bf16* qb = nullptr;
     int *qcnt = nullptr, *rows = nullptr;   // v4 scratch
     float* dists = nullptr;
+    float* bmins = nullptr;             // v4 bound: block minima
     if (v4) {
       char* x = (char*)ws + rup(rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4, 256);
       qb = (bf16*)x;
@@ -1440,20 +1646,15 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       x += rup((size_t)Q * 4 + 4, 256);
       rows = (int*)x;
       dists = (float*)(rows + Q * V4_CAP);
+      x += 2 * (size_t)Q * V4_CAP * 4;
+      bmins = (float*)x;
     }
-    {   // (v4: also its bf16 queries and zeroed list counts)
+    if (!v4) {
       switch (d / 4) {
-// (v4 at Q >= 128: a 1024-row first bound halves pass 1's admissions -- Q =
-// 256 131 vs 134 us; below, the longer kth_bound block costs more than it
-// saves, +3 us at Q <= 32: profiles/lab/r04zz_knn_rpb_ab.txt)
 #define CASEK(n)                                                                             \
   case n:                                                                                    \
-    if (v4 && Q >= 128)                                                                      \
-      hipLaunchKernelGGL((kth_bound_kernel<n, 2 * TH_S>), dim3((unsigned)Q), dim3(256), 0, s, \
-                         t, inv, N, q, qn, k, thr0, qb, qcnt);                               \
-    else                                                                                     \
-      hipLaunchKernelGGL(kth_bound_kernel<n>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, \
-                         q, qn, k, thr0, qb, qcnt);                                          \
+    hipLaunchKernelGGL(kth_bound_kernel<n>, dim3((unsigned)Q), dim3(256), 0, s, t, inv, N, q, qn, k, \
+                       thr0);                                                                          \
     break;
         CASEK(1) CASEK(2) CASEK(3) CASEK(4) CASEK(5) CASEK(6) CASEK(7) CASEK(8)
         CASEK(9) CASEK(10) CASEK(11) CASEK(12) CASEK(13) CASEK(14) CASEK(15) CASEK(16)
@@ -1463,21 +1664,44 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
     }
     if (v4) {
       // query blocks of 16: NQB per launch row (the table is read once per
-      // NQB * 16 queries); the sample pass takes at most V4_SNQ of them
+      // NQB * 16 queries)
       const int nqb = (int)std::min<int64_t>(cdiv(Q, 16), V4_QC / 16);
       const int NQ = nqb <= 2 ? 2 : nqb <= 4 ? 4 : nqb <= 8 ? 8 : 16;
-      const int NQS = std::min(NQ, V4_SNQ);
-      // one or two row tiles per wave: the sample pass is latency-bound (two
-      // when the block stages at most 4 query blocks: Q = 1 55.5 vs 57.3 us,
-      // Q = 32 64.1 vs 65.0; at 16 query blocks one tile, 149 vs 146 us at two)
-      const int RPB_S = NQS <= 4 ? 128 : 64;
-      const int64_t NS = std::min<int64_t>(N, V4_S);   // sample rows
-      const dim3 gs((unsigned)cdiv(NS, RPB_S), (unsigned)cdiv(Q, NQS * 16));
       const int rpb = v4_rpb(NQ, N);
       const dim3 g4((unsigned)cdiv(N, rpb), (unsigned)cdiv(Q, NQ * 16));
+      // the admission bound from the first V4_S rows (bound5_kernel), its
+      // minima merged by scan4 itself up to V4_MQ queries
+      const int ng = (int)cdiv(std::min<int64_t>(N, V4_S), B5_C);
+      const bool merge4 = Q <= V4_MQ;
+      {
+        const int qg = merge4 ? 1 : B5_QG;
+        const dim3 gb((unsigned)ng, (unsigned)cdiv(Q, 16 * qg));
+#define BOUND5(ks, pk)                                                                                         \
+  do {                                                                                                         \
+    if (merge4)                                                                                                \
+      hipLaunchKernelGGL((bound5_kernel<ks, pk, 1>), gb, dim3(256), 0, s, t, inv, tb, N, q, Q, qn, qb, qcnt, bmins); \
+    else                                                                                                       \
+      hipLaunchKernelGGL((bound5_kernel<ks, pk, B5_QG>), gb, dim3(256), 0, s, t, inv, tb, N, q, Q, qn, qb, qcnt,     \
+                         bmins);                                                                               \
+  } while (0)
+        if (d == 32) {
+          if (tb) BOUND5(1, true);
+          else BOUND5(1, false);
+        } else {
+          if (tb) BOUND5(2, true);
+          else BOUND5(2, false);
+        }
+#undef BOUND5
+        DCNR_LAUNCH_CHECK();
+        if (!merge4) {
+          hipLaunchKernelGGL(bound5_merge_kernel, dim3((unsigned)cdiv(Q, 4)), dim3(256), 0, s, bmins, ng, Q, k,
+                             thr0);
+          DCNR_LAUNCH_CHECK();
+        }
+      }
 #define SCAN4(ks, nq, pk, g, n, rp)                                                                    \
   hipLaunchKernelGGL((scan4_kernel<ks, nq, pk>), g, dim3(256), 0, s, t, inv, tb, n, rp, qb, thr0, qn, \
-                     Q, qcnt, rows, dists)
+                     Q, qcnt, rows, dists, merge4 ? bmins : nullptr, ng, k)
 #define CASE4(ks, nq, sel, g, n, rp)                                  \
   if (d == 32 * ks && sel == nq) {                                    \
     if (tb) SCAN4(ks, nq, true, g, n, rp);                            \
@@ -1487,27 +1711,15 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
   CASE4(1, 2, sel, g, n, rp) CASE4(1, 4, sel, g, n, rp) CASE4(1, 8, sel, g, n, rp)         \
   CASE4(1, 16, sel, g, n, rp) CASE4(2, 2, sel, g, n, rp) CASE4(2, 4, sel, g, n, rp)        \
   CASE4(2, 8, sel, g, n, rp) CASE4(2, 16, sel, g, n, rp)
-      // pass 1 over the first V4_S rows under the 512-row bound (~2% of them
-      // admitted): their exact k-th distance -> thr0, the admission bound of
-      // pass 2 over the whole table
-      CASES4(NQS, gs, NS, RPB_S)
+      CASES4(NQ, g4, N, rpb)
       DCNR_LAUNCH_CHECK();
-      if (NS < N) {
-        hipLaunchKernelGGL((rescore_kernel<true, 0>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows,
-                           k, nullptr, nullptr, thr0, t, inv, N, qn);
-        DCNR_LAUNCH_CHECK();
-        CASES4(NQ, g4, N, rpb)
-        DCNR_LAUNCH_CHECK();
-      }
-      // (a table of at most V4_S rows: pass 1 covered every row under a valid
-      // bound, so its lists already hold the answer)
       // (a query whose list overflowed scans the table exactly in its block)
       if (d == 32)
-        hipLaunchKernelGGL((rescore_kernel<false, 8>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows,
-                           k, idx, dist, nullptr, t, inv, N, qn);
+        hipLaunchKernelGGL(rescore_kernel<8>, dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k, idx,
+                           dist, t, inv, N, qn);
       else
-        hipLaunchKernelGGL((rescore_kernel<false, 16>), dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows,
-                           k, idx, dist, nullptr, t, inv, N, qn);
+        hipLaunchKernelGGL(rescore_kernel<16>, dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k, idx,
+                           dist, t, inv, N, qn);
       DCNR_LAUNCH_CHECK();
 #undef CASES4
 #undef CASE4

@@ -11,7 +11,7 @@ dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 tab = torch.randn((1_000_000, 64), generator=g, device=dev)
 nn = dcnr.NearestNeighbors(metric="cosine").fit(tab)
-for Q in (32, 256):
+for Q in (1, 32, 256):
     q = tab[torch.randint(0, 1_000_000, (Q,), generator=g, device=dev)]
     for _ in range(12):
         nn.kneighbors_device(q, 11)

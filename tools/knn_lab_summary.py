@@ -6,7 +6,7 @@ for v in sys.argv[2:]:
     agg = collections.defaultdict(list)
     for r in rows:
         n = r['Kernel_Name'].replace('void ', '').replace('dcnr::(anonymous namespace)::', '')
-        if not n.startswith(('scan4', 'rescore')): continue
+        if not n.startswith(('scan4', 'rescore', 'bound5')): continue
         n = re.sub(r'\(.*', '', n)
         agg[(n, r['Grid_Size_X'], r['Grid_Size_Y'])].append((int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3)
     print(v, '  '.join('%s[%sx%s] %.1f' % (k[0], k[1], k[2], sum(t[2:]) / len(t[2:])) for k, t in sorted(agg.items())))

@@ -4,7 +4,7 @@ import csv
 import re
 import sys
 
-KN = ('kth', 'scan', 'rescore', 'merge', 'v4_prep')
+KN = ('kth', 'bound5', 'scan', 'rescore', 'merge', 'v4_prep')
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Start_Timestamp']))
 every = int(sys.argv[2]) if len(sys.argv) > 2 else 13
 seq = []
@@ -18,7 +18,7 @@ for r in rows:
                     r['Grid_Size_X'], r['Grid_Size_Y'], r['VGPR_Count'], int(r['Start_Timestamp'])))
 calls, cur = [], []
 for s in seq:
-    if s[0].startswith('kth') and cur:
+    if s[0].startswith(('kth', 'bound5')) and cur:
         calls.append(cur)
         cur = []
     cur.append(s)
