@@ -1220,21 +1220,26 @@ __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__
     __syncthreads();   // (dl is reused)
     exact_query_topk<DV>(tab, inv, N, qn + qq * DV * 4, k, dl, idx + qq * k, dist + qq * k);
   };
+  const int* rl = rows + qq * V4_CAP;
+  const float* dq = dists + qq * V4_CAP;
+  // the list's first B4_T entries are read beside its count (the slots
+  // exist whatever the count; the ones past it are ignored): one round trip
+  const float d0 = dq[threadIdx.x];
+  const int i0 = rl[threadIdx.x];
   const int n = qcnt[qq];
   if (n > V4_CAP || n < k) {   // overflow (fewer than k admitted rows only when N < k)
     fail();
     return;
   }
   if (threadIdx.x == 0) cnt = 0;
-  const int* rl = rows + qq * V4_CAP;
-  const float* dq = dists + qq * V4_CAP;
-  for (int e = threadIdx.x; e < n; e += B4_T) dl[e] = dq[e];
+  if ((int)threadIdx.x < n) dl[threadIdx.x] = d0;
+  for (int e = threadIdx.x + B4_T; e < n; e += B4_T) dl[e] = dq[e];
   __syncthreads();
   const unsigned tk = block_select_kth<B4_T>(dl, n, k);   // upper edge of the k-th's bin
   for (int e = threadIdx.x; e < n; e += B4_T)
     if (__float_as_uint(dl[e]) <= tk) {
       const int pos = atomicAdd(&cnt, 1);
-      if (pos < V4_SCAP) { cd[pos] = dl[e]; ci[pos] = rl[e]; }
+      if (pos < V4_SCAP) { cd[pos] = dl[e]; ci[pos] = e < B4_T ? i0 : rl[e]; }
     }
   __syncthreads();
   const int nv = cnt;
