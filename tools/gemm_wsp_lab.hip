@@ -1,6 +1,8 @@
 // LAB (not built into libdcnr): the round-5 pipelined forward GEMM, kept for
-// reference -- faster on the BIAS epilogue (67 vs 72 us) but nondeterministic
-// inside the full train step; build it with
+// reference -- 67 vs 72 us on the BIAS epilogue and 3.858 vs 3.876 ms per
+// step, but inside the train step the last X tile of a block now and then
+// reads a few stale rows when a side-stream kernel shares its CUs (DESIGN.md
+// section 8, round 5; profiles/lab/r05_gemm_wsp_lab.txt).  Build it with
 // tools/lab_sed.sh-style one-file lab builds only.
 // Pipelined weight-stationary GEMM for the bf16 deep tower's train forward
 // (gfx950): the initial Linear and both Linears of every ResBlock
@@ -234,7 +236,7 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
 #pragma unroll
     for (int kt = 0; kt < WP_KT; ++kt) {
       if (kt < WP_DPW) piece(td, kt);
-      if (kt == WP_KT - 2) {
+      if (kt == WP_KT - 4) {
         // tile i+1 landed (every wave's pieces) and every wave is past tile
         // i-1 (whose buffer tile i+3 refills).  Younger than tile i+1's DMAs:
         // this k-loop's 8 pieces and its first row block's 2 stores
@@ -243,6 +245,13 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
         else
           asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(WP_DPW) : "memory");
       }
+      // ... and tile i+1 is first read one barrier later (from the reads of
+      // k-step 14 on): an LDS-DMA write is ordered for another wave's ds_read
+      // only a full phase after the wait that retires it (cdna_hip_programming.md,
+      // "Read a staged buffer one phase AFTER the wait"; reading right behind
+      // the wait's own barrier returned stale rows now and then once other
+      // kernels shared the CU)
+      if (kt == WP_KT - 2) asm volatile("s_barrier" ::: "memory");
       if (kt + 2 < WP_KT) {
         xf[(kt + 2) & 3][0] = xrd(xb, kt + 2, 0);
         xf[(kt + 2) & 3][1] = xrd(xb, kt + 2, 1);
@@ -321,6 +330,11 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
       if (n < a.N) a.part[((int64_t)group * 2 + k) * a.N + n] = x[0];
     }
   }
+  // the LDS-DMAs of the two tiles past the last (zeros into buffers this
+  // block never reads again) may still be landing: the workgroup's LDS must
+  // not be handed to the next workgroup on this CU -- of this launch, or of a
+  // kernel running beside it on another stream -- before they have
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 template <bool STATS>
