@@ -18,7 +18,7 @@ def load(path, counter):
         if m:
             n = n[m.end():m.end() + int(m.group(1))]
         n = re.sub(r"\(.*", "", n)
-        if not n.startswith(("kth", "scan", "rescore", "merge")):
+        if not n.startswith(("kth", "bound5", "scan", "rescore", "merge")):
             continue
         per[(n, int(r["Grid_Size"]))].append(float(r["Counter_Value"]) * 1024.0)
     return per
