@@ -606,6 +606,25 @@ def main():
         except ValueError as e:   # layout not shard-aligned
             other_exchange = {"exchange": trainer.exchange, "error": str(e)}
         trainer.exchange = keep
+    # N > 1: the time each exchange adds after the backward's last kernel
+    # (exchange + AdamW, CUDA events around them: VERDICT r04 item 7), max
+    # over ranks, from K more steps per exchange outside the timed region
+    exchange_window = None
+    if world > 1:
+        exchange_window = {}
+        keep = trainer.exchange
+        for ex in ((keep, "sparse" if keep == "dense" else "dense") if trainer.shard else (keep,)):
+            trainer.exchange = ex
+            trainer.step_events = []
+            try:
+                timed(False)
+                w = torch.tensor([trainer.exchange_window_ms()], device=dev, dtype=torch.float64)
+                dist.all_reduce(w, op=dist.ReduceOp.MAX)
+                exchange_window[ex + "_ms"] = float(w.item())
+            except ValueError:
+                pass
+            trainer.step_events = None
+        trainer.exchange = keep
 
     # scored pairs/s: eval-mode forward (running-stat BN, no dropout) per GPU
     model.eval()
@@ -752,6 +771,7 @@ def main():
             "scored_pairs_per_sec": pairs_per_s,
             "scored_pairs_roofline": eval_roof,
             "other_exchange": other_exchange,
+            "exchange_window_after_backward": exchange_window,
             "final_loss": final_loss,
             "roofline": roof,
             "roofline_by_class": table,
@@ -795,6 +815,8 @@ def main():
             "request_ms": None if cfg5 is None else cfg5.get("request_ms"),
             "cpu_baseline_samples_per_sec": out.get("cpu_baseline", {}).get("value"),
         }
+        if exchange_window:
+            out["summary"]["exchange_window_ms"] = exchange_window
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

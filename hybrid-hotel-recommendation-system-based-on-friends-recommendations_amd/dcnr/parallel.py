@@ -176,8 +176,11 @@ class SparseExchange:
         and the all-reduce of elements [dense_lo, dense_hi) (the small
         categorical tables) copied into the shard.
 
-    Rows no rank touched have an exactly-zero gradient (the backward
-    zero-fills them), so the shard equals the dense reduce-scatter's sum."""
+    Only touched rows are read from ``gflat`` and the shard starts from zero,
+    so rows no rank touched are exactly zero in it -- the dense
+    reduce-scatter's sum -- whether the backward zero-filled the tables or
+    wrote only the touched rows (FusedTrainer's row-map step); the
+    categorical range must hold the dense gradient (zeroed where untouched)."""
 
     def __init__(self, width: int, dense_lo: int, dense_hi: int, group=None, ops=None):
         self.width, self.dense_lo, self.dense_hi, self.group = width, dense_lo, dense_hi, group

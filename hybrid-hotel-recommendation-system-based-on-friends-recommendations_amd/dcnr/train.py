@@ -38,6 +38,9 @@ byte map (DCNR_FLAG_ROW_MAP), and the optimizer launch reads unmarked rows'
 gradients as exactly 0 (dcnr_adam_step_rows): the same parameters bit for bit,
 without the zero fill and without reading the untouched rows' gradients.  The
 tables' ``.grad`` rows a step did not touch then hold stale values.
+world > 1 with exchange="sparse" (same opt-out): the same backward, since the
+exchange reads only the touched rows of the user and item tables; the small
+categorical tables, all-reduced densely, are zeroed before it.
 """
 from __future__ import annotations
 
@@ -119,8 +122,11 @@ class FusedTrainer:
         self._grads = [p.grad for p in model.param_tensors()]   # views into gflat
         # world 1: the row-map step (module docstring)
         self.row_map = self.world == 1 and not dense_table_grads
+        self.dense_table_grads = dense_table_grads
         self._flags = _lib.FLAG_ROW_MAP if self.row_map else 0
         self._rows_cache = None
+        # a list: step() appends (backward end, step end) CUDA events to it
+        self.step_events = None
         if sync_bn and self.world > 1:
             from .parallel import install_sync_bn
             install_sync_bn(model, process_group)
@@ -134,8 +140,10 @@ class FusedTrainer:
         y = y.reshape(-1).to(torch.float32).contiguous()
         seed = dropout_seed(user.device)
         model._index_watch.poll()
+        sparse_rows = self._sparse_rows()
+        flags = self._flags | (_lib.FLAG_ROW_MAP if sparse_rows else 0)
         logits, self._ws = run_forward(model, True, seed, user, item, cat, num, self._ws,
-                                       extra_flags=self._flags)
+                                       extra_flags=flags)
         self._B = user.shape[0]
         if self.exchange == "sparse" and self._sparse is not None:
             # the touched rows come from the forward's id sort: their counts
@@ -144,10 +152,16 @@ class FusedTrainer:
         # grad_scale 1/world: the SUM all-reduce then yields the global mean gradient
         loss, dz = bce_with_logits(logits, y, True, 1.0 / self.world)
         self._dense_work = None
+        if sparse_rows:
+            # the categorical tables go through a dense all-reduce: zero them
+            # (1.5 MB at the bench shape); the row map leaves their untouched
+            # rows unwritten
+            lay = self._sparse_layout
+            self.gflat[lay["dense_lo"]:lay["dense_hi"]].zero_()
         try:
             run_backward(model, user, item, cat, num, dz, self._ws, self._grads, seed,
                          accumulate=False, grad_ready=self._grad_ready_cb,
-                         extra_flags=self._flags)
+                         extra_flags=flags)
         except RuntimeError:
             # the hook may have started the dense all-reduce before the
             # failure: let it finish before anyone writes gflat again
@@ -163,12 +177,38 @@ class FusedTrainer:
             raise
         # the all-reduce this step's backward started (None: start it now)
         dense, self._dense_work = self._dense_work, None
+        marks = self.step_events
+        if marks is not None:   # the backward's last kernel is enqueued
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
         if self.row_map:
             self.step_count += 1
             self._adam_rows(self.step_count)
         else:
             self._exchange_and_update(None, None, dense)
+        if marks is not None:
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            marks.append((e0, e1))
         return (loss, logits) if return_logits else loss
+
+    def exchange_window_ms(self):
+        """Mean time between the end of the backward and the end of the step
+        (exchange + optimizer: what the step adds after its last backward
+        kernel) over the steps recorded since ``step_events = []``."""
+        marks = self.step_events or []
+        if not marks:
+            return None
+        marks[-1][1].synchronize()
+        return sum(a.elapsed_time(b) for a, b in marks) / len(marks)
+
+    def _sparse_rows(self):
+        """world > 1 with the sparse exchange: the backward writes only the
+        rows the batch touched (DCNR_FLAG_ROW_MAP, no 142 MB zero fill); the
+        exchange packs exactly those rows, and the owner's accumulate starts
+        its shard from zero, so the shard is the same sum bit for bit."""
+        return (self.world > 1 and self.exchange == "sparse" and self._sparse is not None
+                and not self.dense_table_grads)
 
     def _row_segments(self):
         """dcnr_adam_step_rows' tensor list over the flat buffers: each table

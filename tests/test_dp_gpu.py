@@ -262,9 +262,15 @@ def _worker_sparse(rank, world, port, cfg_name="toy", sync_bn=True):
         torch.cuda.set_device(dev)
         lo, hi = rank * nb // world, (rank + 1) * nb // world
         flats = []
-        for exchange in ("dense", "sparse"):
+        # "sparse" writes only the touched table rows in the backward (row
+        # map, no zero fill); "sparse-zerofill" keeps the zero-filled tables
+        runs = ("dense", "sparse") + (("sparse-zerofill",) if cfg_name == "toy" else ())
+        for run in runs:
+            exchange = run.split("-")[0]
             m = _model(dev, "bf16", dropout=0.6, cfg=cfg)
-            tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, sync_bn=sync_bn, exchange=exchange)
+            tr = dcnr.FusedTrainer(m, lr=1e-3, weight_decay=1e-4, sync_bn=sync_bn, exchange=exchange,
+                                   dense_table_grads=run.endswith("zerofill"))
+            assert tr._sparse_rows() == (run == "sparse")
             gen = torch.cuda.default_generators[0]
             gen.set_offset(0)                      # the same dropout seeds in both runs
             for step in range(2):
@@ -290,7 +296,8 @@ def _worker_sparse(rank, world, port, cfg_name="toy", sync_bn=True):
             torch.cuda.empty_cache()
         # world 2: the owner's rank-order sum (0 + g_0) + g_1 is the dense
         # reduce-scatter's g_0 + g_1: every parameter bit-identical
-        assert torch.equal(flats[0], flats[1])
+        for f in flats[1:]:
+            assert torch.equal(flats[0], f)
     finally:
         dist.destroy_process_group()
 

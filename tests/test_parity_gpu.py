@@ -586,6 +586,47 @@ def test_cosine_knn_v2_v4_same_answer(dev, N, d):
         assert torch.equal(i1[0], i40[r]) and torch.equal(d1[0], d40[r]), r
 
 
+@pytest.mark.parametrize("N,Q,d", [(11, 2, 64), (12, 40, 32), (600, 3, 64), (5633, 33, 64),
+                                   (65537, 17, 32), (70001, 40, 64), (3001, 5, 36), (65536, 1, 64)])
+def test_cosine_knn_small_and_ragged_tables(dev, N, Q, d):
+    """Ragged shapes around scan v4's fixed sizes (empty / ragged
+    inputs): tables of exactly k rows, fewer than k bound blocks of B5_C rows
+    (the admission bound is then +inf and every row is rescored exactly),
+    one row past the V4_S bound sample, row counts that are no multiple of any
+    block size, query counts that straddle the 16-query MFMA tile and the
+    32-query in-scan merge, a d that takes scan v2 (36), and a single query
+    (scan v2 below V4_Q1_N rows): every list against a torch fp32 brute force,
+    sorted by (distance, row)."""
+    import dcnr
+    k = 11
+    g = torch.Generator(device=dev).manual_seed(N + Q + d)
+    table = torch.randn(N, d, device=dev, generator=g)
+    q = torch.randn(Q, d, device=dev, generator=g)
+    nn_ = dcnr.NearestNeighbors(metric="cosine").fit(table)
+    dist_, idx = nn_.kneighbors_device(q, k)
+    dist_, idx = dist_.cpu().numpy(), idx.cpu().numpy()
+    tn = table / table.norm(dim=1, keepdim=True)
+    qn = q / q.norm(dim=1, keepdim=True)
+    ref_d, ref_i = torch.topk(1.0 - qn @ tn.T, k, dim=1, largest=False)
+    ref_d, ref_i = ref_d.cpu().numpy(), ref_i.cpu().numpy()
+    np.testing.assert_allclose(dist_, ref_d, rtol=0, atol=2e-6)
+    for r in range(Q):
+        near = np.diff(ref_d[r]) <= 2e-6
+        iso = np.ones(k, bool)
+        iso[1:] &= ~near
+        iso[:-1] &= ~near
+        np.testing.assert_array_equal(idx[r][iso], ref_i[r][iso])
+        key = list(zip(dist_[r].tolist(), idx[r].tolist()))
+        assert key == sorted(key)
+    if N == k:   # every row, in distance order
+        assert all(sorted(row) == list(range(N)) for row in idx.tolist())
+    d0, i0 = nn_.kneighbors_device(q[:0], k)   # no queries: empty lists
+    assert tuple(d0.shape) == (0, k) and tuple(i0.shape) == (0, k)
+    if N < 64:   # sklearn's error for n_neighbors > n_samples_fit
+        with pytest.raises(ValueError):
+            nn_.kneighbors_device(q, N + 1)
+
+
 @pytest.mark.parametrize("Q,dim", [(32, 64), (256, 64), (40, 32)])
 def test_cosine_knn_v4_overflow_falls_back_exact(dev, Q, dim):
     """More than V4_CAP rows inside one query's admission bound (12000 rows
