@@ -1613,6 +1613,7 @@ dcnr_status dcnr_row_inv_norms(const float* table, int64_t N, int32_t d, float* 
 }
 
 size_t dcnr_cosine_topk_workspace_size(int64_t N, int64_t Q, int32_t k) {
+  if (N < 1 || Q < 1 || k < 1) return 256;   // nothing to plan (cosine_topk returns or rejects)
   return topk_ws(N, Q, k) + 256;
 }
 
@@ -1680,6 +1681,7 @@ dcnr_status dcnr_linear_bf16(const void* X, int64_t ldx, int64_t M, int32_t K, c
 }
 
 size_t dcnr_linear_wgrad_workspace_size(int32_t N, int32_t K, int64_t B) {
+  if (N < 1 || K < 1 || B < 1) return 0;   // (dcnr_linear_wgrad_bf16 rejects these shapes)
   return (size_t)gemm_dw_splits(N, K, B) * (size_t)N * (size_t)K * sizeof(float);
 }
 

@@ -43,6 +43,21 @@ def test_input_dim_and_workspace_queries():
     # train workspace holds >= 3 activations per res block + x0 (bf16 halves it)
     mb = our_model(gc.CFG3R, precision="bf16")
     assert mb.workspace_bytes(131072, 1) < tr
+    assert m.workspace_bytes(0, 0) >= 0 and m.workspace_bytes(1, 1) > 0
+
+
+def test_size_queries_take_empty_shapes():
+    """The host-only size queries at zero / tiny shapes (no queries, no rows,
+    a table of k rows) return instead of dividing by zero."""
+    from dcnr import _lib
+    lib = _lib.load()
+    for N, Q, k in [(11, 0, 11), (0, 5, 11), (0, 0, 1), (11, 2, 11), (1, 1, 1), (65537, 33, 64)]:
+        assert lib.dcnr_cosine_topk_workspace_size(N, Q, k) >= 0
+    assert lib.dcnr_cosine_topk_workspace_size(1_000_000, 256, 11) > lib.dcnr_cosine_topk_workspace_size(
+        1_000_000, 1, 11)
+    for N, K, B in [(0, 64, 100), (64, 0, 100), (64, 64, 0), (256, 256, 131072)]:
+        assert lib.dcnr_linear_wgrad_workspace_size(N, K, B) >= 0
+    assert lib.dcnr_linear_wgrad_workspace_size(256, 256, 131072) > 0
 
 
 @pytest.mark.parametrize("fname,cfg", [("f1_cfg1_eval.npz", gc.CFG1), ("f3_cfg3r_train.npz", gc.CFG3R),
