@@ -1630,7 +1630,8 @@ dcnr_status dcnr_cosine_topk_packed(const float* table, const float* inv_norms, 
                                     int64_t N, int32_t d, const float* queries, int64_t Q, int32_t k,
                                     int64_t* idx, float* dist, void* ws, size_t ws_bytes,
                                     dcnr_stream_t stream) {
-  if (!table || !inv_norms || !queries || !idx || !dist || (Q > 0 && !ws)) {
+  // (no queries: the query and output pointers may be null)
+  if (!table || !inv_norms || (Q > 0 && (!queries || !idx || !dist || !ws))) {
     set_error("dcnr_cosine_topk: null argument");
     return DCNR_BAD_ARG;
   }

@@ -89,6 +89,9 @@ class NearestNeighbors:
         if k <= 0:
             raise ValueError(f"Expected n_neighbors > 0. Got {k}")
         q = torch.as_tensor(np.asarray(X, dtype=np.float32)) if not torch.is_tensor(X) else X
+        if q.shape[0] == 0:   # sklearn's check_array
+            raise ValueError(f"Found array with 0 sample(s) (shape={tuple(q.shape)}) while a minimum "
+                             "of 1 is required by NearestNeighbors.")
         dist, idx = self.kneighbors_device(q, k)
         idx_np = idx.cpu().numpy()
         if return_distance:
@@ -174,6 +177,9 @@ class ShardedNearestNeighbors:
         if k <= 0:
             raise ValueError(f"Expected n_neighbors > 0. Got {k}")
         q = torch.as_tensor(np.asarray(X, dtype=np.float32)) if not torch.is_tensor(X) else X
+        if q.shape[0] == 0:   # sklearn's check_array
+            raise ValueError(f"Found array with 0 sample(s) (shape={tuple(q.shape)}) while a minimum "
+                             "of 1 is required by NearestNeighbors.")
         dist_, idx = self.kneighbors_device(q, k)
         idx_np = idx.cpu().numpy()
         if return_distance:

@@ -622,6 +622,8 @@ def test_cosine_knn_small_and_ragged_tables(dev, N, Q, d):
         assert all(sorted(row) == list(range(N)) for row in idx.tolist())
     d0, i0 = nn_.kneighbors_device(q[:0], k)   # no queries: empty lists
     assert tuple(d0.shape) == (0, k) and tuple(i0.shape) == (0, k)
+    with pytest.raises(ValueError):   # sklearn's check_array on the host API
+        nn_.kneighbors(np.zeros((0, d), np.float32), n_neighbors=k)
     if N < 64:   # sklearn's error for n_neighbors > n_samples_fit
         with pytest.raises(ValueError):
             nn_.kneighbors_device(q, N + 1)
