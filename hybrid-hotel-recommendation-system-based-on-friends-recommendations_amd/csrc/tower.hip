@@ -173,10 +173,15 @@ __device__ __forceinline__ void epi_piece(const Pend& pd, int p, u32x4& w0, u32x
     v1 += hi16(r);
   }
   if constexpr (MODE >= 1) {
-    v0 = fmaxf(v0, 0.f);
-    v1 = fmaxf(v1, 0.f);
+    // ReLU on the packed pair: bf16 rounding keeps the sign, so
+    // max(bf16(v), 0) as two int16 lanes (v_pk_max_i16: negatives and -0
+    // -> +0) is bf16(max(v, 0)) -- one instruction instead of two v_max_f32
+    typedef short s16x2 __attribute__((ext_vector_type(2)));
+    const s16x2 r = __builtin_elementwise_max(__builtin_bit_cast(s16x2, pk2(v0, v1)), s16x2{0, 0});
+    w[2 * ob + hf] = __builtin_bit_cast(uint32_t, r);
+  } else {
+    w[2 * ob + hf] = pk2(v0, v1);
   }
-  w[2 * ob + hf] = pk2(v0, v1);
 }
 
 // One slice (step): the k-loop of 2 output blocks x 2 sample blocks into
