@@ -186,7 +186,8 @@ __device__ __forceinline__ void epi_piece(const Pend& pd, int p, u32x4& w0, u32x
 
 // One slice (step): the k-loop of 2 output blocks x 2 sample blocks into
 // `cur`, with the previous slice's epilogue (`pend`, PEND) in its first 8
-// k-steps; then the slice's constants into `cur`.  p0/p1: the previous
+// k-steps and the next slice's LDS-DMA pieces on its odd ones; then the
+// slice's constants into `cur`.  p0/p1: the previous
 // slice's output fragments.
 template <int KT, int MODE, bool PEND, class Dma>
 __device__ __forceinline__ void tw_slice(const char* sl, int g, int lane, const u32x4 (&in)[16][2],
@@ -208,7 +209,10 @@ __device__ __forceinline__ void tw_slice(const char* sl, int g, int lane, const 
       af[(kt + 2) % 3][0] = rd(0, kt + 2);
       af[(kt + 2) % 3][1] = rd(1, kt + 2);
     }
-    dma(kt);
+    // the DMA pieces on odd k-steps, so they spread over the whole slice
+    // (issue-bound at one wave per SIMD: on k-steps 0..8 beside the epilogue
+    // pieces 2-3 % slower, profiles/lab/r05_tower_ablation.txt)
+    if (kt & 1) dma(kt >> 1);
 #pragma unroll
     for (int ob = 0; ob < 2; ++ob)
 #pragma unroll
@@ -225,8 +229,8 @@ __device__ __forceinline__ void tw_slice(const char* sl, int g, int lane, const 
     }
     __builtin_amdgcn_sched_barrier(0);
   }
-  // (short k-loops, KT < 9: the DMA and epilogue pieces left over)
-  for (int d = KT; d <= TW_KT0 / 2; ++d) dma(d);
+  // (short k-loops: the DMA and epilogue pieces left over)
+  for (int d = KT / 2; d <= TW_KT0 / 2; ++d) dma(d);
   if constexpr (PEND) {
 #pragma unroll
     for (int p = KT; p < 8; ++p) epi_piece<MODE>(pend, p, p0, p1);
@@ -287,7 +291,7 @@ __global__ __launch_bounds__(TW_NT, 1) void tower_kernel(TowerArgs a) {
     i_slot = i_slot + 1 == TW_NSLOT ? 0 : i_slot + 1;
   };
   // piece d of the slice being issued (d == pieces: its constants), one per
-  // k-step of the consuming slice: each LDS-DMA's issue cost then sits
+  // odd k-step of the consuming slice: each LDS-DMA's issue cost then sits
   // beside MFMAs instead of in a burst after the barrier
   auto issue_piece = [&](int d) {
     const int pcs = NKT == TW_KT0 ? TW_KT0 / 2 : i_pcs;
