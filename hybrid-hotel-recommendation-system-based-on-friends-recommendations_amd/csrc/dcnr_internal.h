@@ -70,19 +70,17 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
 // Inline asm on purpose: hipcc tracks builtin LDS-DMAs as pending LDS writes
 // and drains them (vmcnt(0)) before every ds_read, which would serialise a stage ring;
 // the caller's counted vmcnt waits are the only synchronisation.
-// M0 is saved and restored inside the statement (it is compiler-reserved).
+// M0 (compiler-reserved) is an input operand ("{m0}"): the compiler sets it
+// before the statement and knows it changed -- no save / restore inside the
+// asm, which cost the fused tower 3 % (profiles/lab/r05_tower_ablation.txt).
 // (Default cache policy: the nt policy measured 4.06 -> 4.17 ms per step,
 // profiles/lab/r03ae_dma_nt_ab.txt.)
 __device__ __forceinline__ void dma16(u32x4 rsrc, int off, uint32_t lds_dst) {
-  uint32_t keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(off), "s"(rsrc), "s"(lds_dst)
+      "buffer_load_dwordx4 %0, %1, 0 offen lds"
+      :
+      : "v"(off), "s"(rsrc), "{m0}"(lds_dst)
       : "memory");
 }
 
@@ -90,15 +88,11 @@ __device__ __forceinline__ void dma16(u32x4 rsrc, int off, uint32_t lds_dst) {
 // stream of pieces then costs one VGPR per lane pattern however many pieces
 // a wave issues.
 __device__ __forceinline__ void dma16s(u32x4 rsrc, int voff, int soff, uint32_t lds_dst) {
-  uint32_t keep;
   asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rsrc), "s"(lds_dst), "s"(soff)
+      "buffer_load_dwordx4 %0, %1, %3 offen lds"
+      :
+      : "v"(voff), "s"(rsrc), "{m0}"(lds_dst), "s"(soff)
       : "memory");
 }
 
