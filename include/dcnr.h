@@ -315,7 +315,9 @@ size_t dcnr_cosine_topk_workspace_size(int64_t N, int64_t Q, int32_t k);
 
 /* k nearest rows of `table` [N,d] to each query [Q,d] by cosine distance
  * dist = clip(1 - <q/|q|, x/|x|>, 0, 2) (fp32), ascending; ties by lower
- * row index.  idx int64 [Q,k], dist fp32 [Q,k].  1 <= k <= 64. */
+ * row index.  idx int64 [Q,k], dist fp32 [Q,k].  1 <= k <= min(64, N).
+ * Q = 0 returns DCNR_OK without touching the query / output / workspace
+ * pointers (which may then be NULL). */
 dcnr_status dcnr_cosine_topk(const float* table, const float* inv_norms, int64_t N, int32_t d,
                              const float* queries, int64_t Q, int32_t k, int64_t* idx,
                              float* dist, void* ws, size_t ws_bytes, dcnr_stream_t stream);
