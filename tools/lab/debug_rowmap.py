@@ -6,7 +6,7 @@ import sys
 
 import torch
 
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..",
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..",
                                 "hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd"))
 import dcnr  # noqa: E402
 

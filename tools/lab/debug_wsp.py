@@ -2,7 +2,7 @@
 fixed data with the output pre-filled with NaN: unwritten or nondeterministic
 elements, by row / column pattern."""
 import os, sys
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd"))
 import torch
 from dcnr import _lib

@@ -1,14 +1,14 @@
 """Lab: which stage of the train step differs run to run with gemm_wsp in the
 forward (tests/test_embed_bwd_gpu.py's flaky pair, same config and batch).
 Prints, per repeat, the stored tensors and gradients that differ from the
-first run.  python tools/debug_wsp2.py [repeats]"""
+first run.  python tools/lab/debug_wsp2.py [repeats]"""
 import os
 import sys
 
 import numpy as np
 import torch
 
-ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..")
 sys.path.insert(0, os.path.join(ROOT, "hybrid-hotel-recommendation-system-based-on-friends-recommendations_amd"))
 import dcnr  # noqa: E402
 from dcnr import _lib  # noqa: E402
@@ -71,6 +71,11 @@ for r in range(reps):
         if not torch.equal(st[k], ref[1][k]):
             nz = (st[k] != ref[1][k]).nonzero().flatten()
             diff.append(f"{k}[{nz.numel()} bytes from byte {int(nz[0])}]")
+            if k == "h":   # bf16 [B][256]: rows, row within its 32-row tile, column waves
+                e = torch.unique(nz // 2)
+                rows = torch.unique(e // 256).tolist()
+                print(f"   h rows {rows} (row % 32: {sorted({r % 32 for r in rows})}, tile {sorted({r // 32 for r in rows})}), "
+                      f"column waves {sorted({int(c) // 64 for c in (e % 256).tolist()})}, {e.numel()} elements", flush=True)
     diff += [nm for nm, a, b in zip(names, gr, ref[2]) if not torch.equal(a, b)]
     bad_any |= bool(diff)
     print(f"rep {r}: {'OK' if not diff else 'DIFF ' + ', '.join(diff[:12])}", flush=True)

@@ -30,6 +30,17 @@
 //    tile's first fragments are read: no exposed LDS latency at tile starts.
 #include "dcnr_internal.h"
 
+// round-6 lab variants (tools/lab/r06_wsp.sh): 0 = as shipped in round 5;
+// 1 = no DMAs past the last tile (waits count the stores only there);
+// 2 = the zero DMAs kept, vmcnt(0) at the waits of the last two tiles;
+// 3 = past the last tile, re-load the last real tile instead of zeros;
+// 6 = tile i in ring buffer (i + 1) % 4 (does a failure follow the LDS
+// address or the schedule?); 7 = a tile's 8 pieces issued in reverse order
+#ifndef WSP_VAR
+#define WSP_VAR 0
+#endif
+#define WSP_ROT (WSP_VAR == 6 ? 1 : 0)
+
 namespace dcnr {
 namespace {
 
@@ -89,12 +100,14 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
   const int rbase = wave * WP_DPW * rstride;
   struct TileDma { u32x4 rs; uint32_t dst; };
   auto tile_dma = [&](int i) {
+    const int dst_i = i;
+    if (WSP_VAR == 3 && i >= ntl) i = ntl - 1;
     const bool live = i < ntl;
     const int64_t m0 = (group + (int64_t)(live ? i : 0) * groups) * WP_TM;
     const int64_t rows = live ? a.M - m0 : 0;
     TileDma t;
     t.rs = rsrc_words(a.X + m0 * a.ldx, rows > 0 ? rows * a.ldx * 2 : 0);
-    t.dst = lbase + (uint32_t)((i & (WP_NB - 1)) * WP_TILE + wave * WP_DPW * WP_P);
+    t.dst = lbase + (uint32_t)(((dst_i + WSP_ROT) & (WP_NB - 1)) * WP_TILE + wave * WP_DPW * WP_P);
     return t;
   };
   auto piece = [&](const TileDma& t, int d) {
@@ -214,7 +227,7 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
   f32x4 accA[2][4], accB[2][4];
   bf16x8 xf[4][2];
   if (ntl > 0) {
-    const char* x0b = lds + rowoff;
+    const char* x0b = lds + WSP_ROT * WP_TILE + rowoff;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       xf[kt][0] = xrd(x0b, kt, 0);
@@ -225,8 +238,8 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
   // of tile i+2 in its first 8 k-steps
   auto body = [&](auto prev_c, int i, f32x4 (&cur)[2][4], const f32x4 (&prv)[2][4]) {
     constexpr bool PREV = decltype(prev_c)::value;
-    const char* xb = lds + (i & (WP_NB - 1)) * WP_TILE + rowoff;
-    const char* xn = lds + ((i + 1) & (WP_NB - 1)) * WP_TILE + rowoff;
+    const char* xb = lds + ((i + WSP_ROT) & (WP_NB - 1)) * WP_TILE + rowoff;
+    const char* xn = lds + ((i + 1 + WSP_ROT) & (WP_NB - 1)) * WP_TILE + rowoff;
     const int64_t mp = (group + (int64_t)(i - 1) * groups) * WP_TM;
     const TileDma td = tile_dma(i + 2);
 #pragma unroll
@@ -235,8 +248,11 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
       for (int cb = 0; cb < 4; ++cb) cur[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < WP_KT; ++kt) {
-      if (kt < WP_DPW) piece(td, kt);
-      if (kt == WP_KT - 4) {
+      if (kt < WP_DPW && (WSP_VAR != 1 || i + 2 < ntl)) piece(td, WSP_VAR == 7 ? WP_DPW - 1 - kt : kt);
+      if (kt == WP_KT - 4 && (WSP_VAR == 1 || WSP_VAR == 2) && i + 2 >= ntl) {
+        if (WSP_VAR == 1 && PREV) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      } else if (kt == WP_KT - 4) {
         // tile i+1 landed (every wave's pieces) and every wave is past tile
         // i-1 (whose buffer tile i+3 refills).  Younger than tile i+1's DMAs:
         // this k-loop's 8 pieces and its first row block's 2 stores

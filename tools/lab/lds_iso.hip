@@ -3,7 +3,7 @@
 // or by LDS-DMA (buffer_load ... lds, M0 = its own LDS address) -- and
 // re-checks it while kernel B (32 KB, many blocks, another stream) does the
 // same with its own pattern.  Counts words that changed under either.
-//   hipcc --offload-arch=gfx950 -O3 -o tools/lab_bin/lds_iso tools/lds_iso.hip
+//   hipcc --offload-arch=gfx950 -O3 -o tools/lab_bin/lds_iso tools/lab/lds_iso.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

@@ -3,7 +3,7 @@
 // 32x32x16) on operands loaded once from random data (all-zero operands
 // draw less power and clock higher than real tiles).  The ceiling the
 // production kernels' "fraction of the nominal 2.5 PF/s" is read against.
-//   hipcc --offload-arch=gfx950 -O3 -mllvm -amdgpu-mfma-vgpr-form -o tools/lab_bin/mfma_peak tools/mfma_peak.hip
+//   hipcc --offload-arch=gfx950 -O3 -mllvm -amdgpu-mfma-vgpr-form -o tools/lab_bin/mfma_peak tools/lab/mfma_peak.hip
 // (without the flag the compiler shuffles the 16x16 accumulators through
 // ~50 AGPR moves per 8 MFMAs: a broken measurement)
 //   tools/lab_bin/mfma_peak

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU round-trip (from the repo root on the box): GPU tests, the kNN probe
 # under rocprofv3 --stats, the gemm_ws lab clock passes, the default bench.
-#   bash tools/r03_check.sh <tag>
+#   bash tools/lab/r03_check.sh <tag>
 set -o pipefail
 R=gpurun_out/${1:-r03x}
 mkdir -p $R

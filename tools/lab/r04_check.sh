@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU round-trip (from the repo root on the box): GPU tests, then the
-# default bench line.   bash tools/r04_check.sh <tag> [pytest -k expr]
+# default bench line.   bash tools/lab/r04_check.sh <tag> [pytest -k expr]
 set -o pipefail
 R=gpurun_out/${1:-r04x}
 mkdir -p $R

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Tower lab variants + fold probe + GPU tests + bench in one box visit.
-#   bash tools/r04_lab.sh <tag> "<variants>"
+#   bash tools/lab/r04_lab.sh <tag> "<variants>"
 set -o pipefail
 R=gpurun_out/$1
 mkdir -p $R

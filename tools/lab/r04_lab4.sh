@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU tests, tower probes (default library + lab variants), bench line.
-#   bash tools/r04_lab4.sh <tag> "<lab variants>"
+#   bash tools/lab/r04_lab4.sh <tag> "<lab variants>"
 set -o pipefail
 R=gpurun_out/$1
 mkdir -p $R

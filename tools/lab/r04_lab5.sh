@@ -1,7 +1,7 @@
 #!/bin/bash
 # Tower lab round: probes of lab variants (default library first), then the
 # eval-tower tests with the variants that must stay correct.
-#   bash tools/r04_lab5.sh <tag> "<probe variants>" "<test variants>"
+#   bash tools/lab/r04_lab5.sh <tag> "<probe variants>" "<test variants>"
 set -o pipefail
 R=gpurun_out/$1
 mkdir -p $R

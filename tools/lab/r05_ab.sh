@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU tests of the given files, then a step A/B against lab variants
-#   bash tools/r05_ab.sh <tag> "<test files>" "<variants>" [rounds]
+#   bash tools/lab/r05_ab.sh <tag> "<test files>" "<variants>" [rounds]
 set -o pipefail
 R=gpurun_out/$1; mkdir -p $R
 export TMPDIR=/tmp

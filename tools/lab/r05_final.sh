@@ -2,7 +2,7 @@
 # Round-5 final set on one box: GPU suite, smoke, the round profile
 # (bench + kernel trace + PMC traffic, tools/profile_round.sh), and the kNN
 # PMC passes over tools/knn_lab.py (Q = 1 / 32 / 256).
-#   bash tools/r05_final.sh <tag> [part]   part: 1 = tests + smoke + knn PMC, 2 = profile_round
+#   bash tools/lab/r05_final.sh <tag> [part]   part: 1 = tests + smoke + knn PMC, 2 = profile_round
 set -o pipefail
 R=gpurun_out/$1; mkdir -p $R
 export TMPDIR=/tmp

@@ -1,5 +1,5 @@
 #!/bin/bash
-# bench_gemm.py for the default library and lab variants: bash tools/r05_gemm_probe.sh <tag> "<variants>"
+# bench_gemm.py for the default library and lab variants: bash tools/lab/r05_gemm_probe.sh <tag> "<variants>"
 set -o pipefail
 R=gpurun_out/$1; mkdir -p $R
 timeout -k 10 120 python -u tools/bench_gemm.py > $R/gemm_base.log 2>&1 || exit 1

@@ -1,7 +1,7 @@
 #!/bin/bash
 # kNN round-5 check: the kNN GPU tests, the probe's per-call times, and a
 # rocprofv3 kernel trace of the probe split per call.
-#   bash tools/r05_knn.sh <tag> [variant-lib-name]
+#   bash tools/lab/r05_knn.sh <tag> [variant-lib-name]
 set -o pipefail
 R=gpurun_out/$1; mkdir -p $R
 export TMPDIR=/tmp

@@ -7,5 +7,5 @@ R=gpurun_out/r05m0i; mkdir -p $R
 ROOT=$(pwd)
 DCNR_LIB=$ROOT/tools/lab_bin/libdcnr_m0all.so timeout -k 10 700 python -u -m pytest -x -q --timeout 120 \
   --timeout-method thread -m gpu tests > $R/m0all_tests.log 2>&1 || exit 1
-TWOUT=r05m0i/tw VARIANTS="base m0t" bash tools/r05_tw.sh || exit 1
+TWOUT=r05m0i/tw VARIANTS="base m0t" bash tools/lab/r05_tw.sh || exit 1
 bash tools/ab_bench.sh $R/ab 2 base m0all

@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counters of tools/bench_gemm.py for the default library and lab variants
-#   bash tools/r05_sq.sh <tag> "<variants>"
+#   bash tools/lab/r05_sq.sh <tag> "<variants>"
 set -o pipefail
 T=$1
 SQ_PROG="tools/bench_gemm.py" bash tools/sq_counters.sh $T/base || exit 1

@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5: the pipelined forward GEMM (gemm_wsp.hip) -- parity, kernel A/B, step A/B
-#   bash tools/r05_wsp.sh <tag> "<kernel variants>" "<step variants>"
+#   bash tools/lab/r05_wsp.sh <tag> "<kernel variants>" "<step variants>"
 set -o pipefail
 R=gpurun_out/$1; mkdir -p $R
 export TMPDIR=/tmp

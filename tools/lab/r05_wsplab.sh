@@ -3,4 +3,4 @@
 # base (wsp), wsplds (wsp alone on its CU: 160 KB LDS), sortmain (the forward's
 # id sort on the main stream), nowsp (gemm_ws)
 set -o pipefail
-bash tools/r05_flaky.sh $1 "base wsplds sortmain nowsp"
+bash tools/lab/r05_flaky.sh $1 "base wsplds sortmain nowsp"

@@ -1,6 +1,6 @@
 // LAB (not built into libdcnr): the fused eval tower on v_mfma_f32_32x32x16_bf16,
 // measured 5 % slower than csrc/tower.hip (profiles/lab/r05_tower_ablation.txt).
-// Build as a replacement of tower.o (tools/r05_m32.sh, -mllvm -amdgpu-mfma-vgpr-form).
+// Build as a replacement of tower.o (tools/lab/r05_m32.sh, -mllvm -amdgpu-mfma-vgpr-form).
 // Fused eval deep tower (gfx950): the eval forward's whole deep tower --
 // initial Linear, R ResBlocks (Linear -> BN(running stats) -> ReLU ->
 // Linear -> BN -> + residual -> ReLU) and the deep head dot -- in ONE
