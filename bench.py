@@ -534,6 +534,16 @@ def main():
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    # N > 1: which backend the ranks run and which device each one drives,
+    # so a driver SCALE line shows whether RCCL saw N distinct GPUs
+    ranks_info = None
+    if world > 1:
+        props = torch.cuda.get_device_properties(dev)
+        mine = {"rank": rank, "local_rank": local, "device": f"cuda:{local}", "name": props.name,
+                "pci_bus_id": getattr(props, "pci_bus_id", None),
+                "uuid": str(getattr(props, "uuid", "")) or None}
+        ranks_info = [None] * world
+        dist.all_gather_object(ranks_info, mine)
     import dcnr
     from dcnr import _lib
 
@@ -761,6 +771,9 @@ def main():
                        "batch_per_gpu": B, "global_batch": world * B,
                        "tables": "1M x 32 users, 100k x 32 hotels, 12 x 1000 x 32 cat, 8 dense",
                        "deep": "3 cross + 4 x 512 residual", "parallelism": f"dp{world}",
+                       "backend": dist.get_backend() if world > 1 else None,
+                       "rank_devices": None if world == 1 else
+                       [f'{r["device"]} bus {r["pci_bus_id"]}' for r in ranks_info],
                        "exchange": "none" if world == 1 else (
                            "dense params: all-reduce started in the backward (overlapped); "
                            "user/item tables: touched rows all_to_all to the shard owners + "
@@ -768,6 +781,9 @@ def main():
                            if args.exchange == "sparse"
                            else "dense params: all-reduce started in the backward (overlapped); "
                                 "tables: reduce-scatter + sharded AdamW + all-gather")},
+            "distributed": None if world == 1 else {
+                "backend": dist.get_backend(), "world_size": world, "ranks": ranks_info,
+                "distinct_devices": len({(r["pci_bus_id"], r["uuid"], r["local_rank"]) for r in ranks_info})},
             "scored_pairs_per_sec": pairs_per_s,
             "scored_pairs_roofline": eval_roof,
             "other_exchange": other_exchange,

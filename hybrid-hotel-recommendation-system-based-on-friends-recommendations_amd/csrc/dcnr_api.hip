@@ -1586,7 +1586,7 @@ dcnr_status dcnr_adam_step_rows(int32_t n_tensors, float* const* params, const f
   }
   double nbytes = 0;
   for (int i = 0; i < n_tensors; ++i) {
-    if (row_map[i] && (row_width[i] < 1 || numel[i] % row_width[i] || numel[i] >= (int64_t(1) << 32))) {
+    if (row_map[i] && (row_width[i] < 1 || numel[i] % row_width[i])) {
       set_error("dcnr_adam_step_rows: tensor %d: %lld elements in rows of %d", i, (long long)numel[i],
                 row_width[i]);
       return DCNR_BAD_ARG;

@@ -138,6 +138,13 @@ __device__ __forceinline__ bool last_arriver(int* counter, int n_arrivals, int* 
   return *flag != 0;
 }
 
+// ReLU (train.py:117, 122) with one NaN rule for every path: max over the
+// value's bits as a signed integer, which is what the fused eval tower's
+// packed-int16 max on the bf16 activation does (tower.hip) -- +NaN (the NaN
+// arithmetic yields here) and +inf pass, as torch.relu passes NaN; -0, -inf
+// and a negative-signed NaN give +0.  (fmaxf would map every NaN to 0.)
+__device__ __forceinline__ float relu_f(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -369,6 +376,10 @@ struct NtArgs {
   int nslices, groups; int64_t mtiles;   // filled by gemm_ws
 };
 bool gemm_ws_supported(int64_t K, int64_t N);
+// the train forward's BIAS / BIAS_STATS epilogues at 256 < K <= 512: the
+// pipelined one-wave-per-SIMD variant (gemm_wsp.hip), taken by gemm_ws
+bool gemm_wsp_supported(int epi, int64_t K, int64_t N);
+dcnr_status gemm_wsp(int epi, const NtArgs& a, hipStream_t s, int* nparts);
 // nparts (stats epilogues): rows of part written (the nchunks of reduce_fused)
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
 // head partials of NT_EPI_BN_RESID_RELU_HEAD: rows of headp written (0: unsupported shape)

@@ -217,7 +217,7 @@ template <typename T> struct BnReluDropOp {  // a = dropout(relu(t*sc+sh))
   __device__ void load(int64_t r, int c, Reg& q) const { ldv<T>(t + r * ld + c, q.x); }
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&)[1][VE<T>]) const {
 #pragma unroll
-    for (int v = 0; v < VE<T>; ++v) q.x[v] = fmaxf(q.x[v] * k.sc[v] + k.sh[v], 0.f);
+    for (int v = 0; v < VE<T>; ++v) q.x[v] = relu_f(q.x[v] * k.sc[v] + k.sh[v]);
     if (drop) apply_dropout<VE<T>>(seed, layer, r, c, thresh, inv_keep, q.x);
     stv<T, true>(a + r * ld + c, q.x);
     if (bits) store_pos_bits<T>(bits, r, ld >> 3, c, q.x);
@@ -236,7 +236,7 @@ template <typename T> struct BnAddReluOp {   // out = relu(t*sc+sh + x)
   }
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&)[1][VE<T>]) const {
 #pragma unroll
-    for (int v = 0; v < VE<T>; ++v) q.a[v] = fmaxf(q.a[v] * k.sc[v] + k.sh[v] + q.b[v], 0.f);
+    for (int v = 0; v < VE<T>; ++v) q.a[v] = relu_f(q.a[v] * k.sc[v] + k.sh[v] + q.b[v]);
     stv<T, true>(out + r * ld + c, q.a);
     if (bits) store_pos_bits<T>(bits, r, ld >> 3, c, q.a);
   }
@@ -264,7 +264,7 @@ template <typename T> struct BnAddReluHeadOp {
     float d = 0.f;
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      q.a[v] = fmaxf(q.a[v] * k.sc[v] + k.sh[v] + q.b[v], 0.f);
+      q.a[v] = relu_f(q.a[v] * k.sc[v] + k.sh[v] + q.b[v]);
       d += (float)(T)q.a[v] * k.wf[v];   // the stored (rounded) activation, as row_dot reads it
     }
     if (out) stv<T, true>(out + r * ld + c, q.a);   // (train: null, the backward rebuilds it)
@@ -300,7 +300,7 @@ template <typename T, bool HAS_G, bool REBUILD = false> struct Bwd2StatsOp {
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[3][VE<T>]) const {
     if constexpr (REBUILD) {
 #pragma unroll
-      for (int v = 0; v < VE<T>; ++v) q.o[v] = (float)(T)fmaxf(q.t[v] * k.sc[v] + k.sh[v] + q.o[v], 0.f);
+      for (int v = 0; v < VE<T>; ++v) q.o[v] = (float)(T)relu_f(q.t[v] * k.sc[v] + k.sh[v] + q.o[v]);
     }
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {

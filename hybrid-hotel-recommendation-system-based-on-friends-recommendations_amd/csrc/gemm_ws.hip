@@ -281,7 +281,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
         }
         if constexpr (HAS_SS) {
 #pragma unroll
-          for (int d = 0; d < 2; ++d) v[d] = f2v{fmaxf(v[d][0], 0.f), fmaxf(v[d][1], 0.f)};
+          for (int d = 0; d < 2; ++d) v[d] = f2v{relu_f(v[d][0]), relu_f(v[d][1])};
         }
         if constexpr (EPI == NT_EPI_DROP_BN) {
           v[0] *= a.hscale;
@@ -524,6 +524,7 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
     set_error("gemm_ws: unsupported K=%d N=%d / missing epilogue operand", a.K, a.N);
     return DCNR_UNSUPPORTED_SHAPE;
   }
+  if (gemm_wsp_supported(epi, a.K, a.N)) return gemm_wsp(epi, a, s, nparts);
   switch (epi) {
     case NT_EPI_BIAS: return dispatch_ws<NT_EPI_BIAS>(a, s, nparts);
     case NT_EPI_F32: return dispatch_ws<NT_EPI_F32>(a, s, nparts);

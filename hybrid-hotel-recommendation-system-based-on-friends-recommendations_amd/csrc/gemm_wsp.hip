@@ -1,9 +1,3 @@
-// LAB (not built into libdcnr): the round-5 pipelined forward GEMM, kept for
-// reference -- 67 vs 72 us on the BIAS epilogue and 3.858 vs 3.876 ms per
-// step, but inside the train step the last X tile of a block now and then
-// reads a few stale rows when a side-stream kernel shares its CUs (DESIGN.md
-// section 8, round 5; profiles/lab/r05_gemm_wsp_lab.txt).  Build it with
-// tools/lab_sed.sh-style one-file lab builds only.
 // Pipelined weight-stationary GEMM for the bf16 deep tower's train forward
 // (gfx950): the initial Linear and both Linears of every ResBlock
 // (train.py:143, 105, 109 under :161-165),
@@ -28,18 +22,15 @@
 //    k-steps between the MFMAs (1-2 VALU per MFMA gap);
 //  * one barrier per tile, two k-steps before its end, after which the next
 //    tile's first fragments are read: no exposed LDS latency at tile starts.
+//
+// The C stores use a per-tile buffer descriptor and a constant 0 soffset,
+// never an SGPR soffset: hipcc's hazard recognizer (ROCm 7.2) leaves out the
+// two wait states a >64-bit MUBUF store needs before its data VGPRs are
+// rewritten when the store has a REGISTER soffset, and the round-5 version
+// of this kernel (soffset = the tile's row offset) then stored the next
+// values of 4 lanes of one 16-B store now and then, whenever the memory
+// pipeline was backed up.
 #include "dcnr_internal.h"
-
-// round-6 lab variants (tools/lab/r06_wsp.sh): 0 = as shipped in round 5;
-// 1 = no DMAs past the last tile (waits count the stores only there);
-// 2 = the zero DMAs kept, vmcnt(0) at the waits of the last two tiles;
-// 3 = past the last tile, re-load the last real tile instead of zeros;
-// 6 = tile i in ring buffer (i + 1) % 4 (does a failure follow the LDS
-// address or the schedule?); 7 = a tile's 8 pieces issued in reverse order
-#ifndef WSP_VAR
-#define WSP_VAR 0
-#endif
-#define WSP_ROT (WSP_VAR == 6 ? 1 : 0)
 
 namespace dcnr {
 namespace {
@@ -100,14 +91,12 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
   const int rbase = wave * WP_DPW * rstride;
   struct TileDma { u32x4 rs; uint32_t dst; };
   auto tile_dma = [&](int i) {
-    const int dst_i = i;
-    if (WSP_VAR == 3 && i >= ntl) i = ntl - 1;
     const bool live = i < ntl;
     const int64_t m0 = (group + (int64_t)(live ? i : 0) * groups) * WP_TM;
     const int64_t rows = live ? a.M - m0 : 0;
     TileDma t;
     t.rs = rsrc_words(a.X + m0 * a.ldx, rows > 0 ? rows * a.ldx * 2 : 0);
-    t.dst = lbase + (uint32_t)(((dst_i + WSP_ROT) & (WP_NB - 1)) * WP_TILE + wave * WP_DPW * WP_P);
+    t.dst = lbase + (uint32_t)((i & (WP_NB - 1)) * WP_TILE + wave * WP_DPW * WP_P);
     return t;
   };
   auto piece = [&](const TileDma& t, int d) {
@@ -154,7 +143,6 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
     for (int kt = 0; kt < WP_KT; ++kt) asm volatile("" : "+a"(wf[cb][kt]));
   __syncthreads();
 
-  const __amdgpu_buffer_rsrc_t cr = buf_rsrc(a.C, a.M * a.ldc * 2);
   // per-lane column partials [sum, sum2][cb][column r], over all tiles
   float st[2][4][4];
 #pragma unroll
@@ -201,8 +189,10 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
     }
   };
   // store offsets: lane part (row l15 of the block, its 8 columns; columns
-  // past N at an out-of-range offset) + the tile's first row as the SGPR
-  // offset; rows past M fall outside the descriptor (M rows): no masks
+  // past N at an out-of-range offset) into a descriptor that starts at the
+  // tile's first row and ends at row M (rows past M are dropped: no masks);
+  // soffset 0 (see the file header: an SGPR soffset hides the store-data
+  // hazard from the compiler)
   int svo[2][2];
 #pragma unroll
   for (int pr = 0; pr < 2; ++pr)
@@ -212,13 +202,14 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
       svo[pr][rb] = n < a.N ? (int)(((int64_t)(rb * 16 + l15) * a.ldc + n) * 2) : OOR;
     }
   auto epi_store = [&](int64_t mp, int rb) {
-    const int so = __builtin_amdgcn_readfirstlane((int)(mp * a.ldc * 2));
+    const __amdgpu_buffer_rsrc_t ct = buf_rsrc(reinterpret_cast<const bf16*>(a.C) + mp * a.ldc,
+                                               (a.M - mp) * a.ldc * 2);
 #pragma unroll
     for (int pr = 0; pr < 2; ++pr) {
       auto s0 = __builtin_amdgcn_permlane16_swap(ow[2 * pr][0], ow[2 * pr + 1][0], false, false);
       auto s1 = __builtin_amdgcn_permlane16_swap(ow[2 * pr][1], ow[2 * pr + 1][1], false, false);
       const u32x4 sv = {s0[0], s1[0], s0[1], s1[1]};
-      __builtin_amdgcn_raw_buffer_store_b128(sv, cr, svo[pr][rb], so, 0);
+      __builtin_amdgcn_raw_buffer_store_b128(sv, ct, svo[pr][rb], 0, 0);
     }
   };
 
@@ -227,7 +218,7 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
   f32x4 accA[2][4], accB[2][4];
   bf16x8 xf[4][2];
   if (ntl > 0) {
-    const char* x0b = lds + WSP_ROT * WP_TILE + rowoff;
+    const char* x0b = lds + rowoff;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) {
       xf[kt][0] = xrd(x0b, kt, 0);
@@ -238,8 +229,8 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
   // of tile i+2 in its first 8 k-steps
   auto body = [&](auto prev_c, int i, f32x4 (&cur)[2][4], const f32x4 (&prv)[2][4]) {
     constexpr bool PREV = decltype(prev_c)::value;
-    const char* xb = lds + ((i + WSP_ROT) & (WP_NB - 1)) * WP_TILE + rowoff;
-    const char* xn = lds + ((i + 1 + WSP_ROT) & (WP_NB - 1)) * WP_TILE + rowoff;
+    const char* xb = lds + (i & (WP_NB - 1)) * WP_TILE + rowoff;
+    const char* xn = lds + ((i + 1) & (WP_NB - 1)) * WP_TILE + rowoff;
     const int64_t mp = (group + (int64_t)(i - 1) * groups) * WP_TM;
     const TileDma td = tile_dma(i + 2);
 #pragma unroll
@@ -248,11 +239,8 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
       for (int cb = 0; cb < 4; ++cb) cur[rb][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < WP_KT; ++kt) {
-      if (kt < WP_DPW && (WSP_VAR != 1 || i + 2 < ntl)) piece(td, WSP_VAR == 7 ? WP_DPW - 1 - kt : kt);
-      if (kt == WP_KT - 4 && (WSP_VAR == 1 || WSP_VAR == 2) && i + 2 >= ntl) {
-        if (WSP_VAR == 1 && PREV) asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-      } else if (kt == WP_KT - 4) {
+      if (kt < WP_DPW) piece(td, kt);
+      if (kt == WP_KT - 4) {
         // tile i+1 landed (every wave's pieces) and every wave is past tile
         // i-1 (whose buffer tile i+3 refills).  Younger than tile i+1's DMAs:
         // this k-loop's 8 pieces and its first row block's 2 stores
@@ -262,11 +250,8 @@ __global__ __launch_bounds__(WP_NT, 1) void gemm_wsp_kernel(NtArgs a) {
           asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(WP_DPW) : "memory");
       }
       // ... and tile i+1 is first read one barrier later (from the reads of
-      // k-step 14 on): an LDS-DMA write is ordered for another wave's ds_read
-      // only a full phase after the wait that retires it (cdna_hip_programming.md,
-      // "Read a staged buffer one phase AFTER the wait"; reading right behind
-      // the wait's own barrier returned stale rows now and then once other
-      // kernels shared the CU)
+      // k-step 14 on): cdna_hip_programming.md, "Read a staged buffer one
+      // phase AFTER the wait that retires it"
       if (kt == WP_KT - 2) asm volatile("s_barrier" ::: "memory");
       if (kt + 2 < WP_KT) {
         xf[(kt + 2) & 3][0] = xrd(xb, kt + 2, 0);

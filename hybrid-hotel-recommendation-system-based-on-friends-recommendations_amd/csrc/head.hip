@@ -129,24 +129,28 @@ struct AdamBatch {
 };
 static_assert(sizeof(AdamBatch) <= 4096, "kernel argument size");
 
-// torch.optim._functional single-tensor Adam/AdamW algorithm, fp32:
-//   AdamW: p *= 1 - lr*wd ; Adam: g += wd*p
-//   m = lerp(m, g, 1-b1) ; v = b2*v + (1-b2)*g*g
-//   p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps)
+// torch.optim AdamW / Adam (the foreach form torch uses on a GPU), fp32, in
+// torch's order of operations and roundings:
+//   AdamW: p *= 1 - lr*wd ; Adam: g += wd*p          (_foreach_mul_ / add)
+//   m = lerp(m, g, 1-b1) = m + (1-b1)*(g - m)        (_foreach_lerp_: one fma)
+//   v = v*b2 ; v += ((1-b2)*g)*g                      (_foreach_mul_, _foreach_addcmul_)
+//   p += ((-lr/bc1)*m) / (sqrt(v)/sqrt(bc2) + eps)    (_foreach_addcdiv_)
 __device__ __forceinline__ void adam_elem(float& pp, float gg, float& mm, float& vv, float lr, float b1,
                                           float b2, float eps, float wd, float step_size,
                                           float bc2_sqrt, int decoupled) {
   // every fused multiply-add spelled out, no other contraction: the 16-B
   // path and the element path (a tensor's unaligned tail, a mapped table's
   // last partial group) then round alike -- left to the compiler they
-  // differed by an ulp of v
+  // differed by an ulp of v (v*b2 is rounded before the add, as
+  // torch's mul_ then addcmul_ do)
 #pragma clang fp contract(off)
   if (decoupled) pp = pp * (1.f - lr * wd);
   else if (wd != 0.f) gg = fmaf(wd, pp, gg);
   mm = fmaf(1.f - b1, gg - mm, mm);
-  vv = fmaf(vv, b2, (1.f - b2) * gg * gg);
+  vv = vv * b2;
+  vv = vv + ((1.f - b2) * gg) * gg;
   const float denom = sqrtf(vv) / bc2_sqrt + eps;
-  pp = fmaf(-step_size, mm / denom, pp);
+  pp = pp + (-step_size * mm) / denom;
 }
 
 // One thread per 4 consecutive elements (16-B loads and stores where the
@@ -166,10 +170,13 @@ __global__ __launch_bounds__(NT) void adam_kernel(AdamBatch ab, float lr, float 
   const uint8_t* map = ab.map[t];
   const uint32_t rw = (uint32_t)ab.rw[t];
   // an unmarked row's gradient is exactly 0 and is not read (the same
-  // arithmetic as a stored +0: m, v decay, weight decay, the update)
+  // arithmetic as a stored +0: m, v decay, weight decay, the update); the
+  // row index in 32 bits below 2^32 elements, in 64 above (a uniform branch)
+  const bool wide = n > (int64_t)0xFFFFFFFFll;
   bool gr[4];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) gr[e] = !map || (i0 + e < n && map[(uint32_t)(i0 + e) / rw]);
+  for (int e = 0; e < 4; ++e)
+    gr[e] = !map || (i0 + e < n && map[wide ? (i0 + e) / (int64_t)rw : (int64_t)((uint32_t)(i0 + e) / rw)]);
   const bool vec = i0 + 4 <= n && ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0);
   if (vec) {
     float4 pp = *reinterpret_cast<const float4*>(p + i0);

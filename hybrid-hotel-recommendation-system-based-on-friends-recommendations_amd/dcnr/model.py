@@ -202,10 +202,25 @@ class IndexErrorWatch:
         return True
 
     def _reclaim(self):
-        """Orphaned slots return to the ring once their word has landed."""
+        """Orphaned slots return to the ring once their word has landed, or
+        once the stream of the call that owned them has drained without
+        storing it (the call never ran to completion: no late store can come;
+        ADVICE r05 -- else the 64-slot ring would shrink for good)."""
         if self.orphans:
-            left = [s for s in self.orphans if int(self.view[s]) == self.PENDING]
-            self.free.extend(s for s in self.orphans if s not in left)
+            left = []
+            for s in self.orphans:
+                if int(self.view[s]) != self.PENDING:
+                    self.free.append(s)
+                    continue
+                try:
+                    idle = self._stream_idle(s)
+                except RuntimeError:   # a failed stream stores nothing more either
+                    idle = True
+                if idle and int(self.view[s]) == self.PENDING:
+                    self.view[s] = 0
+                    self.free.append(s)
+                else:
+                    left.append(s)
             self.orphans = left
 
     def _poll(self, oldest=False, all_=False):

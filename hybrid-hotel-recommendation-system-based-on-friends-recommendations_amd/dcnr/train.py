@@ -37,7 +37,9 @@ tables' gradients (142 MB at the bench shape) but marks the rows it writes in a
 byte map (DCNR_FLAG_ROW_MAP), and the optimizer launch reads unmarked rows'
 gradients as exactly 0 (dcnr_adam_step_rows): the same parameters bit for bit,
 without the zero fill and without reading the untouched rows' gradients.  The
-tables' ``.grad`` rows a step did not touch then hold stale values.
+tables' ``.grad`` rows a step did not touch then hold stale values: call
+``FusedTrainer.materialize_table_grads()`` before reading them (gradient-norm
+logging, ``clip_grad_norm_``), or pass ``dense_table_grads=True``.
 world > 1 with exchange="sparse" (same opt-out): the same backward, since the
 exchange reads only the touched rows of the user and item tables; the small
 categorical tables, all-reduced densely, are zeroed before it.
@@ -57,6 +59,11 @@ from .ops import bce_with_logits
 
 
 class FusedTrainer:
+    """The reference's training step (train.py:219-226) as native calls; see
+    the module docstring.  ``dense_table_grads=False`` (default) at world 1
+    leaves the tables' untouched ``.grad`` rows stale after ``step()`` --
+    ``materialize_table_grads()`` zeroes them when a caller reads them."""
+
     def __init__(self, model: DCN_RecSys, lr=1e-3, weight_decay=1e-2, optimizer_name='AdamW',
                  betas=(0.9, 0.999), eps=1e-8, process_group=None, sync_bn=False,
                  shard_optimizer=None, exchange="dense", sparse_ops=None, dense_table_grads=False):
@@ -192,6 +199,30 @@ class FusedTrainer:
             marks.append((e0, e1))
         return (loss, logits) if return_logits else loss
 
+    def materialize_table_grads(self):
+        """Zero the table-gradient rows the last row-map step did not write.
+
+        With the row map (world 1 by default, and the sparse exchange) the
+        backward leaves an untouched row's ``.grad`` as it was, where the
+        reference's ``zero_grad()`` + ``backward()`` (train.py:222-225) leaves
+        it 0: code that reads the tables' ``p.grad`` after ``step()``
+        (gradient-norm logging, ``clip_grad_norm_``) calls this first.  The
+        parameters and moments do not depend on it (dcnr_adam_step_rows reads
+        an unmarked row as 0).  No-op without the row map."""
+        if self._ws is None or not (self.row_map or self._sparse_rows()):
+            return
+        model = self.model
+        map_off = model.workspace_offset(self._B, _lib.TRAIN, "row_map", extra_flags=_lib.FLAG_ROW_MAP)
+        if map_off < 0:
+            raise RuntimeError("train workspace has no row map")
+        d = model._dims
+        rows = [d['n_users'], d['n_items']] + list(d['cat_dims'])
+        kb = 0
+        for t, r in enumerate(rows):
+            untouched = self._ws[map_off + kb:map_off + kb + r] == 0
+            self._grads[t][untouched] = 0.0
+            kb += r
+
     def exchange_window_ms(self):
         """Mean time between the end of the backward and the end of the step
         (exchange + optimizer: what the step adds after its last backward
@@ -309,16 +340,23 @@ class FusedTrainer:
                     self._sparse.begin(touched if touched is not None else self.touched_rows())
                 self.last_exchange = self._sparse.finish(self.gflat, self.gshard)
             else:
-                dist.reduce_scatter_tensor(self.gshard, self.gflat[:E], op=dist.ReduceOp.SUM,
-                                           group=self.pg)
+                rs = dist.reduce_scatter_tensor(self.gshard, self.gflat[:E], op=dist.ReduceOp.SUM,
+                                                group=self.pg, async_op=True)
+                # the dense segment's AdamW (its all-reduce ran under the
+                # embedding backward) goes under the tables' reduce-scatter
+                dense.wait()
+                adam(self.flat[E:], self.gflat[E:], self.m[Es:], self.v[Es:], self.step_count)
+                dense = None
+                rs.wait()
             pshard = self.flat[self.rank * Es:(self.rank + 1) * Es]
             adam(pshard, self.gshard, self.m[:Es], self.v[:Es], self.step_count)
             dist.all_gather_into_tensor(self.flat[:E], pshard, group=self.pg)
         else:
             dist.all_reduce(self.gflat[:E], op=dist.ReduceOp.SUM, group=self.pg)
             adam(self.flat[:E], self.gflat[:E], self.m[:E], self.v[:E], self.step_count)
-        dense.wait()
-        adam(self.flat[E:], self.gflat[E:], self.m[Es:], self.v[Es:], self.step_count)
+        if dense is not None:
+            dense.wait()
+            adam(self.flat[E:], self.gflat[E:], self.m[Es:], self.v[Es:], self.step_count)
 
     def optimizer_step(self):
         """Adam/AdamW over the local flat gradient (no exchange)."""

@@ -84,6 +84,33 @@ def test_eval_tower_matches_layer_by_layer(dev, cfg, B):
     _oracle_check(m, cfg, inp, zf, B)
 
 
+@pytest.mark.parametrize("bad", ["nan_weight", "inf_bias"])
+def test_eval_relu_nan_rule_same_in_both_paths(dev, bad):
+    """One ReLU rule for NaN in the fused tower and the layer-by-layer
+    epilogues: max over the value's sign-magnitude bits, the
+    tower's packed-int16 rule -- a positive NaN (what NaN arithmetic yields
+    here) and +inf pass, as torch.relu passes NaN (train.py:117); -inf and a
+    negative-signed NaN give 0.  A NaN row of the first block's layer1 weight
+    (t1[:, j] NaN for every sample) or an infinite bias: both paths give
+    the same NaN pattern and the same finite logits."""
+    cfg, B = gc.CFG3R, 4099
+    m = _model(cfg, dev)
+    with torch.no_grad():
+        if bad == "nan_weight":
+            m.res_blocks[0].layer1.weight[5].fill_(float("nan"))
+        else:
+            m.res_blocks[0].layer1.bias[5] = float("-inf")
+    inp = gc.make_inputs(cfg, B, 5)
+    zf = _eval_logits(m, inp, dev, keep=False)
+    zk = _eval_logits(m, inp, dev, keep=True)
+    print(f"{bad}: NaN logits tower {np.isnan(zf).mean():.3f} layer-by-layer {np.isnan(zk).mean():.3f}")
+    assert np.array_equal(np.isnan(zf), np.isnan(zk))
+    ok = np.isfinite(zk)
+    if ok.any():
+        scale = max(1.0, float(np.abs(zk[ok]).max()))
+        assert np.abs(zf[ok] - zk[ok]).max() / scale < 2e-3
+
+
 def test_eval_tower_chunked_launch(dev):
     """2.4M samples: x0 is 2.2 GB of bf16, past the 32-bit buffer offsets of
     one launch; every chunk's logits must equal scoring the same rows alone."""

@@ -105,6 +105,42 @@ def test_f2_cfg1_optimizer_step(dev, opt):
     np.testing.assert_allclose(sums, fx[f"{opt}_sum"], rtol=1e-5, atol=1e-3)
 
 
+@pytest.mark.parametrize("opt", ["adamw", "adam"])
+def test_adam_kernel_matches_torch_optim_on_device(dev, opt):
+    """dcnr_adam_step follows torch.optim.AdamW / Adam's foreach form (the
+    one torch runs on a GPU, train.py:201-204) operation by operation: v*b2
+    rounded before the addcmul, the addcdiv as (alpha*m)/denom.
+    Not bit for bit: the C ABI carries the betas as fp32, so 1 - b1 and
+    1 - b2 are fp32 differences of fp32 betas (1 - 0.999f = 9.9998713e-4),
+    where torch rounds its double 1 - 0.999 to fp32 (1.0e-3): about 1 % of
+    the parameters differ by an ulp or two after five steps.  Five steps on
+    1M random parameters (odd length: the element path for the tail)."""
+    import dcnr
+    g0 = torch.Generator(device=dev).manual_seed(5)
+    n = 1_000_003
+    p1 = torch.randn(n, device=dev, generator=g0)
+    p2 = torch.nn.Parameter(p1.clone())
+    p1 = torch.nn.Parameter(p1)
+    cls = dcnr.AdamW if opt == "adamw" else dcnr.Adam
+    tcls = torch.optim.AdamW if opt == "adamw" else torch.optim.Adam
+    o1 = cls([p1], lr=1e-3, weight_decay=1e-2)
+    o2 = tcls([p2], lr=1e-3, weight_decay=1e-2, foreach=True)
+    for _ in range(5):
+        g = torch.randn(n, device=dev, generator=g0)
+        g[::7] = 0.0
+        p1.grad, p2.grad = g.clone(), g.clone()
+        o1.step()
+        o2.step()
+    torch.cuda.synchronize()
+    a, b = p1.detach(), p2.detach()
+    same = (a == b).float().mean().item()
+    d = (a - b).abs()
+    # ~2 ulp of b, or 1e-4 of one update (lr = 1e-3) for parameters near 0
+    worst = (d / (b.abs() * 2.4e-7 + 1e-7)).max().item()
+    print(f"bit-equal {same:.4f}, max |diff| {d.max().item():.3e}, worst / (2 ulp + 1e-7) {worst:.3f}")
+    assert same >= 0.97 and worst <= 1.0, (same, worst)
+
+
 @pytest.mark.parametrize("fname,cfg", [("f3_cfg3r_train.npz", gc.CFG3R),
                                        ("f3b_odd_train.npz", gc.CFG_ODD)])
 def test_f3_train_golden(dev, fname, cfg):

@@ -108,6 +108,13 @@ def test_fused_trainer_row_map_bit_identical(dev, precision, skew):
     for (k, a), (_, b2) in zip(m1.state_dict().items(), m2.state_dict().items()):
         assert torch.equal(a, b2), k
     assert torch.equal(t1.m, t2.m) and torch.equal(t1.v, t2.v)
+    # the tables' .grad rows the last step did not touch hold stale values
+    # until materialize_table_grads() zeroes them: then every
+    # gradient equals the dense path's (zero_grad + backward, train.py:222-225)
+    t1.materialize_table_grads()
+    torch.cuda.synchronize()
+    for (k, p1), (_, p2) in zip(m1.named_parameters(), m2.named_parameters()):
+        assert torch.equal(p1.grad, p2.grad), k
 
 
 def test_fused_trainer_row_map_bench_model(dev):
