@@ -503,6 +503,201 @@ __global__ __launch_bounds__(NT) void gather_cross_v4_kernel(GatherDesc g, Cross
   }
 }
 
+// ------------------------------------------- low-rank front (train / eval)
+// The deep forward never needs the cross output x_L itself, only zc = w_f[H:]
+// . x_L (and in train mode the backward's scalars).  CrossLayer keeps every
+// x_l in span{x_0, b_0 .. b_{l-1}} (x_{l+1} = (1 + s_l) x_l + b_l,
+// train.py:96-99), so with x_l = a_l x_0 + sum_j e_lj b_j
+//   s_l = x_l . w_l = a_l u_l + sum_{j<l} e_lj (b_j . w_l),     u_l = x_0 . w_l
+//   a_{l+1} = (1 + s_l) a_l,  e_{l+1,j} = (1 + s_l) e_lj,  e_{l+1,l} = 1
+//   zc = a_L u_f + sum_j e_Lj (b_j . w_f[H:]),                   u_f = x_0 . w_f[H:]
+// -- the same algebra the low-rank backward (cross_bwd.hip) runs on.  Per
+// sample: L + 1 dot products of the gathered x0 row (4 samples per wave
+// reduction) and scalar arithmetic; no D-wide cross stack, no per-layer
+// reduction of x_l.  The Gram terms b_j . w_m are computed per block, in a
+// fixed order, from the parameters.  (fp32 throughout; it differs from the
+// elementwise stack by rounding only: zc and the scalars are checked against
+// fp64 in tests/test_stages_gpu.py and test_gather_cross_gpu.py.)
+template <int R4, int SPW, int IDR, int X0BF16, int L>
+__global__ __launch_bounds__(NT) void gather_lowrank_kernel(GatherDesc g, CrossParams cp,
+                                                            const int64_t* user, const int64_t* item,
+                                                            const int64_t* cat, const float* num,
+                                                            int64_t B, GcOut out, int* err, int check) {
+  static_assert(SPW % 4 == 0 && L >= 1 && L <= 4, "4 samples per reduction, 1..4 layers");
+  constexpr int C = R4 * WAVE;       // float4 chunks per image
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  __shared__ TabLds tl;
+  __shared__ float gram[L][L + 1];   // b_j . w_m (m < L), b_j . w_f[H:] (m = L)
+  const int D = g.D, nt = g.n_tab;
+  v4f* sw = reinterpret_cast<v4f*>(smem);   // [L + 1][C]: w_0 .. w_{L-1}, w_f[H:] (0 past D)
+  for (int i = threadIdx.x; i < (L + 1) * C * 4; i += NT) {
+    const int l = i / (C * 4), e = i % (C * 4);
+    smem[i] = e < D ? (l < L ? cp.w[l][e] : cp.wf_cross[e]) : 0.f;
+  }
+  fill_tab_lds(g, tl);
+  // the Gram terms: one wave per term, lanes over D in order, a fixed tree
+  for (int t = threadIdx.x >> 6; t < L * (L + 1); t += WPB) {
+    const int j = t / (L + 1), m = t % (L + 1);
+    const float* wm = m < L ? cp.w[m] : cp.wf_cross;
+    float acc = 0.f;
+    for (int e = threadIdx.x & 63; e < D; e += WAVE) acc = fmaf(cp.b[j][e], wm[e], acc);
+    acc = wave_sum_dpp(acc);
+    if ((threadIdx.x & 63) == 0) gram[j][m] = acc;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const float* base[R4];
+  int stride[R4], tab[R4];
+#pragma unroll
+  for (int r = 0; r < R4; ++r) {
+    const int e = 4 * (lane + WAVE * r);
+    int t = NO_ELEM, col = 0;
+    if (e < D) {
+      t = NUM_TAB;
+      col = e - (D - g.n_num);
+      for (int q = 0; q < nt; ++q)
+        if (e >= tl.off[q] && e < tl.off[q] + tl.width[q]) { t = q; col = e - tl.off[q]; }
+    }
+    tab[r] = t;
+    base[r] = t >= 0 ? tl.tab[t] + col : (t == NUM_TAB ? num + col : tl.tab[0]);
+    stride[r] = t >= 0 ? tl.width[t] : (t == NUM_TAB ? g.n_num : 0);
+  }
+  float G[L][L + 1];
+#pragma unroll
+  for (int j = 0; j < L; ++j)
+#pragma unroll
+    for (int m = 0; m <= L; ++m) G[j][m] = gram[j][m];
+  int ju[IDR], jt[IDR];
+  int64_t jrows[IDR];
+#pragma unroll
+  for (int q = 0; q < IDR; ++q) {
+    const int j = lane + WAVE * q;
+    ju[q] = j / nt;
+    jt[q] = j % nt;
+    jrows[q] = tl.rows[jt[q]];
+  }
+  auto load_ids = [&](int64_t b0, int (&idr)[IDR]) {
+#pragma unroll
+    for (int q = 0; q < IDR; ++q) {
+      const int64_t b = b0 + ju[q];
+      const bool ok = ju[q] < SPW && b < B;
+      const int t = jt[q];
+      const int64_t bc = ok ? b : 0;
+      const int64_t* src = t == 0 ? user + bc : t == 1 ? item + bc : cat + bc * (nt - 2) + (t - 2);
+      int64_t raw = ok ? *src : 0;
+      if (raw < 0 || raw >= jrows[q]) {
+        if (check && err) atomicOr(err, 1);
+        raw = raw < 0 ? 0 : jrows[q] - 1;
+      }
+      idr[q] = (int)raw;
+    }
+  };
+
+  constexpr int NSC = 2 * L + 1;
+  const int64_t ntiles = (B + SPW - 1) / SPW;
+  const int64_t wave_id = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
+  const int64_t n_waves = (int64_t)gridDim.x * WPB;
+  int idc[IDR];
+  if (wave_id < ntiles) load_ids(wave_id * SPW, idc);
+  for (int64_t tile = wave_id; tile < ntiles; tile += n_waves) {
+    const int64_t b0 = tile * SPW;
+    v4f x[SPW][R4];
+#pragma unroll
+    for (int u = 0; u < SPW; ++u) {
+      const int64_t bc = b0 + u < B ? b0 + u : B - 1;
+#pragma unroll
+      for (int r = 0; r < R4; ++r) {
+        const int t = tab[r];
+        const int id = lane_id_of<IDR>(idc, u * nt + (t >= 0 ? t : 0));
+        const int64_t row = t >= 0 ? (int64_t)id : (t == NUM_TAB ? bc : 0);
+        x[u][r] = *reinterpret_cast<const v4f*>(base[r] + row * stride[r]);
+      }
+    }
+    if (tile + n_waves < ntiles) load_ids((tile + n_waves) * SPW, idc);
+#pragma unroll
+    for (int u = 0; u < SPW; ++u)
+#pragma unroll
+      for (int r = 0; r < R4; ++r)
+        if (tab[r] == NO_ELEM) x[u][r] = v4f{0.f, 0.f, 0.f, 0.f};
+    // x0 (A operand of the initial Linear), pad columns 0
+#pragma unroll
+    for (int u = 0; u < SPW; ++u) {
+      const int64_t b = b0 + u;
+#pragma unroll
+      for (int r = 0; r < R4; ++r) {
+        const int e = 4 * (lane + WAVE * r);
+        if (b < B && e < out.ld_x0) {
+          if constexpr (X0BF16) {
+            bf16x4 h = {(bf16)x[u][r][0], (bf16)x[u][r][1], (bf16)x[u][r][2], (bf16)x[u][r][3]};
+            *reinterpret_cast<bf16x4*>(static_cast<bf16*>(out.x0) + b * out.ld_x0 + e) = h;
+          } else {
+            *reinterpret_cast<v4f*>(static_cast<float*>(out.x0) + b * out.ld_x0 + e) = x[u][r];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u0 = 0; u0 < SPW; u0 += 4) {
+      // us[m][k]: x_0 . w_m (m < L), x_0 . w_f[H:] (m = L) of sample u0 + k
+      float us[L + 1][4];
+#pragma unroll
+      for (int m = 0; m <= L; ++m) {
+        v4f wv[R4];
+#pragma unroll
+        for (int r = 0; r < R4; ++r) wv[r] = sw[m * C + lane + WAVE * r];
+        float d[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          d[k] = 0.f;
+#pragma unroll
+          for (int r = 0; r < R4; ++r) d[k] += dot4(x[u0 + k][r], wv[r]);
+        }
+        wave_sum4(d[0], d[1], d[2], d[3], us[m][0], us[m][1], us[m][2], us[m][3]);
+      }
+      // the recurrence (wave-uniform scalars)
+      float vals[4][NSC], zcv[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float a = 1.f, e[L];
+#pragma unroll
+        for (int l = 0; l < L; ++l) {
+          float s = a * us[l][k];
+#pragma unroll
+          for (int j = 0; j < l; ++j) s = fmaf(e[j], G[j][l], s);
+          vals[k][l] = s;
+          vals[k][L + l] = us[l][k];
+          const float f = 1.f + s;
+          a *= f;
+#pragma unroll
+          for (int j = 0; j < l; ++j) e[j] *= f;
+          e[l] = 1.f;
+        }
+        vals[k][2 * L] = us[L][k];
+        float z = a * us[L][k];
+#pragma unroll
+        for (int j = 0; j < L; ++j) z = fmaf(e[j], G[j][L], z);
+        zcv[k] = z;
+      }
+      if (out.zc) {
+        float zl = zcv[0];
+#pragma unroll
+        for (int k = 1; k < 4; ++k) zl = lane == k ? zcv[k] : zl;
+        if (lane < 4 && b0 + u0 + lane < B) out.zc[b0 + u0 + lane] = zl;
+      }
+      if (out.sc && lane < 4 && b0 + u0 + lane < B) {   // lane k: sample u0 + k's NSC scalars
+#pragma unroll
+        for (int i = 0; i < NSC; ++i) {
+          float v = vals[0][i];
+#pragma unroll
+          for (int k = 1; k < 4; ++k) v = lane == k ? vals[k][i] : v;
+          out.sc[(b0 + u0 + lane) * NSC + i] = v;
+        }
+      }
+    }
+  }
+}
+
 // -------------------------------------------------------------- launchers
 constexpr int FWD_SPW = 4;   // samples per wave per tile (forward)
 
@@ -543,6 +738,23 @@ dcnr_status launch_v4(const GatherDesc& g, const CrossParams& cp, const int64_t*
   const int64_t target = o.x0 ? GC_V4_WAVES : GC_V4_WAVES_NOX0;
   const int64_t waves = cdiv(ntiles, cdiv(ntiles, target));
   const unsigned blocks = (unsigned)cdiv(waves, WPB);
+  if (o.x0 && !o.cross && cp.L >= 1 && cp.L <= 4) {   // the deep forward: the low-rank front
+    const size_t lr_lds = (size_t)(cp.L + 1) * R4 * WAVE * 16;
+    const bool i1 = SPW * g.n_tab <= 64;
+#define DCNR_LR(LL)                                                                                    \
+  if (cp.L == LL) {                                                                                    \
+    if (i1)                                                                                            \
+      hipLaunchKernelGGL((gather_lowrank_kernel<R4, SPW, 1, X0BF16, LL>), dim3(blocks), dim3(NT), lr_lds, \
+                         s, g, cp, user, item, cat, num, B, o, err, check);                           \
+    else                                                                                               \
+      hipLaunchKernelGGL((gather_lowrank_kernel<R4, SPW, 2, X0BF16, LL>), dim3(blocks), dim3(NT), lr_lds, \
+                         s, g, cp, user, item, cat, num, B, o, err, check);                           \
+  }
+    DCNR_LR(1) DCNR_LR(2) DCNR_LR(3) DCNR_LR(4)
+#undef DCNR_LR
+    DCNR_LAUNCH_CHECK();
+    return DCNR_OK;
+  }
   if (SPW * g.n_tab <= 64)
     hipLaunchKernelGGL((gather_cross_v4_kernel<R4, SPW, 1, X0BF16>), dim3(blocks), dim3(NT), lds, s,
                        g, cp, user, item, cat, num, B, o, err, check);
