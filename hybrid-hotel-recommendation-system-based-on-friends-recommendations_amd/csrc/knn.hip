@@ -789,7 +789,10 @@ __global__ __launch_bounds__(256) void bound5_kernel(const float* __restrict__ t
         qb[(q0 + qq) * D + lane] = (bf16)(v * in);
       }
     }
-    if (g == 0 && qq < nq && lane == 0) qcnt[q0 + qq] = 0;
+    if (g == 0 && qq < nq && lane == 0) {
+      qcnt[q0 + qq] = 0;
+      qcnt[Q + 1 + q0 + qq] = 0;   // the split fallback's arrival counter (rescore_kernel)
+    }
   }
   __syncthreads();
   // the row tiles' A fragments (bf16, as scan4 rounds them)
@@ -1128,8 +1131,8 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
 // scan, so a query that lands here returns what scan v2 returns.  Needs
 // k <= 32 (two k-lists per 64-lane merge step) and 16 * 64 * 8 B of LDS.
 template <int DV>
-__device__ void exact_query_topk(const float* __restrict__ tab, const float* __restrict__ inv, int64_t N,
-                                 const float* __restrict__ qrow, int k, float* lds, int64_t* idx,
+__device__ void exact_query_topk(const float* __restrict__ tab, const float* __restrict__ inv, int64_t lo,
+                                 int64_t N, const float* __restrict__ qrow, int k, float* lds, int64_t* idx,
                                  float* dist) {
   constexpr int NW = B4_T / 64;
   __shared__ int cntl[NW];
@@ -1140,7 +1143,7 @@ __device__ void exact_query_topk(const float* __restrict__ tab, const float* __r
   const float4* qv = reinterpret_cast<const float4*>(qrow);
   int c = 0;
   float th = FLT_MAX;
-  for (int64_t base = 64 * w; base < N; base += 64 * NW) {
+  for (int64_t base = lo + 64 * w; base < N; base += 64 * NW) {   // rows [lo, N)
     const int64_t r = base + lane;
     const bool ok = r < N;
     const int64_t rc = ok ? r : 0;
@@ -1203,23 +1206,72 @@ __device__ void exact_query_topk(const float* __restrict__ tab, const float* __r
 // One block per query: the exact distances of its admitted rows (computed
 // by scan4's epilogue), the k-th smallest by block_select_kth, then a bitonic
 // sort of the rows at or under the selected bin by (distance, row).  A query
-// whose list overflowed takes exact_query_topk (DV = d / 4).
+// whose list overflowed takes exact_query_topk (DV = d / 4) -- with few
+// queries (F > 1: blocks q + Q f, f = 1 .. F-1, that return at once unless
+// q's list overflowed) split over F blocks, each scanning 1/F of the table
+// into a k-list, the last-arriving one merging them: the all-overflow call
+// (a table with thousands of duplicates per query) no longer puts the whole
+// table through one CU (the merge keeps the (distance,
+// row) order, so the answer is the single block's bit for bit).
+constexpr int V4_FMAX = 64;        // fallback blocks per query
+constexpr int V4_FQ = 16;          // queries up to which the fallback is split
+inline int v4_fallback_split(int64_t Q) {
+  return Q <= V4_FQ ? (int)std::min<int64_t>(V4_FMAX, 256 / Q) : 1;
+}
 template <int DV>
 __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__ dists, const int* qcnt,
                                                        const int* rows, int k, int64_t* idx,
                                                        float* dist, const float* __restrict__ tab,
                                                        const float* __restrict__ inv, int64_t N,
-                                                       const float* __restrict__ qn) {
+                                                       const float* __restrict__ qn, int64_t Q, int F,
+                                                       float* pd, int64_t* pi, int* pcnt) {
   __shared__ float dl[V4_CAP];
   __shared__ float cd[V4_SCAP];
   __shared__ int ci[V4_SCAP];
   __shared__ int cnt;
+  __shared__ int last;
   static_assert(V4_CAP >= 2 * B4_T, "exact fallback lists live in dl");
-  const int64_t qq = blockIdx.x;
+  const int64_t qq = blockIdx.x % Q;
+  const int f = (int)(blockIdx.x / Q);
   auto fail = [&]() {
     __syncthreads();   // (dl is reused)
-    exact_query_topk<DV>(tab, inv, N, qn + qq * DV * 4, k, dl, idx + qq * k, dist + qq * k);
+    exact_query_topk<DV>(tab, inv, 0, N, qn + qq * DV * 4, k, dl, idx + qq * k, dist + qq * k);
   };
+  // the split fallback: rows [N f / F, N (f+1) / F) -> k-list f of the query,
+  // then the last of its F blocks merges the F lists (wave 0)
+  auto split = [&]() {
+    __syncthreads();
+    const int64_t lo = N * f / F, hi = N * (f + 1) / F;
+    float* pdq = pd + (qq * F + f) * k;
+    int64_t* piq = pi + (qq * F + f) * k;
+    exact_query_topk<DV>(tab, inv, lo, hi, qn + qq * DV * 4, k, dl, piq, pdq);
+    if (!last_arriver(pcnt + qq, F, &last)) return;
+    if (threadIdx.x < 64) {
+      const int lane = threadIdx.x;
+      float d = FLT_MAX;
+      int i = INT_MAX;
+      for (int ff = 0; ff < F; ++ff) {
+        const int sl = ff == 0 ? lane : lane - k;
+        if (ff == 0 || lane >= k) {
+          const bool has = sl >= 0 && sl < k;
+          const float dv = has ? pd[(qq * F + ff) * k + sl] : FLT_MAX;
+          const int64_t iv = has ? pi[(qq * F + ff) * k + sl] : (int64_t)INT_MAX;
+          d = dv;
+          i = dv == FLT_MAX ? INT_MAX : (int)iv;   // (a range shorter than k: FLT_MAX / INT_MAX pads)
+        }
+        if (ff > 0) wave_sort64(d, i, lane);
+      }
+      if (lane < k) {
+        idx[qq * k + lane] = (int64_t)i;
+        dist[qq * k + lane] = d;
+      }
+    }
+  };
+  if (f > 0) {   // a split-fallback block: only for an overflowed list
+    const int n = qcnt[qq];
+    if (n > V4_CAP || n < k) split();
+    return;
+  }
   const int* rl = rows + qq * V4_CAP;
   const float* dq = dists + qq * V4_CAP;
   // the list's first B4_T entries are read beside its count (the slots
@@ -1228,7 +1280,8 @@ __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__
   const int i0 = rl[threadIdx.x];
   const int n = qcnt[qq];
   if (n > V4_CAP || n < k) {   // overflow (fewer than k admitted rows only when N < k)
-    fail();
+    if (F > 1) split();
+    else fail();
     return;
   }
   if (threadIdx.x == 0) cnt = 0;
@@ -1581,9 +1634,14 @@ bool use_v4(int64_t N, int64_t Q, int d, int k) {
 // queries [Q][d] | per-query counts [Q] | admitted rows [Q][V4_CAP]
 // | their exact distances [Q][V4_CAP] | the bound's block minima
 // [Q][B5_G]
+// the split fallback's k-lists (k <= 32: scan v4's range), for Q <= V4_FQ
+size_t v4_split_bytes(int64_t Q) {
+  const int F = v4_fallback_split(Q);
+  return F > 1 ? rup((size_t)Q * F * 32 * (4 + 8), 256) : 0;
+}
 size_t v4_extra(int64_t Q, int d) {
-  return rup((size_t)Q * d * 2, 256) + rup((size_t)Q * 4 + 4, 256) + 2 * (size_t)Q * V4_CAP * 4 +
-         rup((size_t)Q * B5_G * 4, 256) + 256;
+  return rup((size_t)Q * d * 2, 256) + rup((size_t)Q * 8 + 8, 256) + 2 * (size_t)Q * V4_CAP * 4 +
+         rup((size_t)Q * B5_G * 4, 256) + v4_split_bytes(Q) + 256;
 }
 
 size_t topk_ws_d(int64_t N, int64_t Q, int k, int d) {
@@ -1643,16 +1701,21 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
     int *qcnt = nullptr, *rows = nullptr;   // v4 scratch
     float* dists = nullptr;
     float* bmins = nullptr;             // v4 bound: block minima
+    float* split_d = nullptr;           // v4 split fallback: k-lists
+    int64_t* split_i = nullptr;
     if (v4) {
       char* x = (char*)ws + rup(rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4, 256);
       qb = (bf16*)x;
       x += rup((size_t)Q * d * 2, 256);
-      qcnt = (int*)x;
-      x += rup((size_t)Q * 4 + 4, 256);
+      qcnt = (int*)x;   // [Q] list counts, a word, [Q] split-fallback arrival counters
+      x += rup((size_t)Q * 8 + 8, 256);
       rows = (int*)x;
       dists = (float*)(rows + Q * V4_CAP);
       x += 2 * (size_t)Q * V4_CAP * 4;
       bmins = (float*)x;
+      x += rup((size_t)Q * B5_G * 4, 256);
+      split_d = (float*)x;
+      split_i = (int64_t*)(x + rup((size_t)Q * v4_fallback_split(Q) * 32 * 4, 256));
     }
     if (!v4) {
       switch (d / 4) {
@@ -1719,12 +1782,13 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       CASES4(NQ, g4, N, rpb)
       DCNR_LAUNCH_CHECK();
       // (a query whose list overflowed scans the table exactly in its block)
+      const int F = v4_fallback_split(Q);
       if (d == 32)
-        hipLaunchKernelGGL(rescore_kernel<8>, dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k, idx,
-                           dist, t, inv, N, qn);
+        hipLaunchKernelGGL(rescore_kernel<8>, dim3((unsigned)(Q * F)), dim3(B4_T), 0, s, dists, qcnt, rows, k,
+                           idx, dist, t, inv, N, qn, Q, F, split_d, split_i, qcnt + Q + 1);
       else
-        hipLaunchKernelGGL(rescore_kernel<16>, dim3((unsigned)Q), dim3(B4_T), 0, s, dists, qcnt, rows, k, idx,
-                           dist, t, inv, N, qn);
+        hipLaunchKernelGGL(rescore_kernel<16>, dim3((unsigned)(Q * F)), dim3(B4_T), 0, s, dists, qcnt, rows, k,
+                           idx, dist, t, inv, N, qn, Q, F, split_d, split_i, qcnt + Q + 1);
       DCNR_LAUNCH_CHECK();
 #undef CASES4
 #undef CASE4

@@ -665,7 +665,7 @@ def test_cosine_knn_small_and_ragged_tables(dev, N, Q, d):
             nn_.kneighbors_device(q, N + 1)
 
 
-@pytest.mark.parametrize("Q,dim", [(32, 64), (256, 64), (40, 32)])
+@pytest.mark.parametrize("Q,dim", [(32, 64), (256, 64), (40, 32), (2, 64), (16, 32)])
 def test_cosine_knn_v4_overflow_falls_back_exact(dev, Q, dim):
     """More than V4_CAP rows inside one query's admission bound (12000 rows
     on the query's own direction, every one at distance 0): scan v4's list
@@ -694,6 +694,33 @@ def test_cosine_knn_v4_overflow_falls_back_exact(dev, Q, dim):
         isolated[1:] &= ~near
         isolated[:-1] &= ~near
         np.testing.assert_array_equal(i[r][isolated], ref_i[r][isolated])
+
+
+@pytest.mark.parametrize("Q,dim", [(3, 64), (16, 64), (5, 32)])
+def test_cosine_knn_v4_all_overflow_split_fallback(dev, Q, dim):
+    """Every query overflows (6000 duplicates of each query's direction):
+    with few queries (Q <= 16) the exact fallback is split over up to 64
+    blocks per query, each scanning a slice of the table, the last one
+    merging the k-lists (knn.hip rescore_kernel).  Each query's answer is
+    its exact top-k -- the 11 lowest duplicate rows at distance 0 -- and the
+    answers equal the unsplit single-block fallback's (the same query
+    answered inside a batch of 32, where the fallback is not split)."""
+    import dcnr
+    g = torch.Generator(device=dev).manual_seed(17 + Q + dim)
+    n = 120_000 + 6000 * Q
+    table = torch.randn(n, dim, device=dev, generator=g)
+    q = torch.randn(32, dim, device=dev, generator=g)
+    perm = torch.randperm(n, device=dev, generator=g)
+    dups = [perm[6000 * j:6000 * (j + 1)] for j in range(Q)]
+    for j in range(Q):
+        table[dups[j]] = q[j] * (1.0 + j)
+    nn_ = dcnr.NearestNeighbors(metric="cosine", algorithm="brute").fit(table)
+    d, i = nn_.kneighbors(q[:Q], n_neighbors=11)
+    d32, i32 = nn_.kneighbors(q, n_neighbors=11)   # 32 queries: one fallback block per query
+    for j in range(Q):
+        assert np.all(d[j] <= 2e-6)
+        assert i[j].tolist() == sorted(dups[j].cpu().tolist())[:11]
+    assert np.array_equal(i, i32[:Q]) and np.array_equal(d, d32[:Q])
 
 
 @pytest.mark.parametrize("M,K,N,out_f32", [(4096, 512, 512, 0), (1000, 456, 512, 1),
