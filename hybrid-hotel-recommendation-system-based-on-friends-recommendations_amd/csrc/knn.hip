@@ -568,18 +568,17 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 // merged by the last-arriving block).  The admitted rows (~N k / V4_S per
 // query) are appended to a per-query list with their exact fp32 distances
 // (scan v2's arithmetic, computed in scan4's epilogue); rescore_kernel
-// selects the k best by (distance, row).  A query whose list overflows
-// V4_CAP (the count word carries V4_OVF when a block's wave list ran out of
-// room), or whose k-th distance is shared by more than V4_SCAP rows, is
-// answered by an exact scan of the whole table inside its own rescore block
-// (scan v2's per-wave lists and arithmetic): no batch-wide flag, no gated
-// launches behind the chain.  Three launches per call: bound5, scan4,
-// rescore.
+// selects the k best by (distance, row) -- however many rows share the
+// k-th's bin, the whole list at most.  A query whose list overflows V4_CAP
+// (the count word carries V4_OVF when a block's wave list ran out of room)
+// is answered by an exact scan of the whole table in rescore blocks (scan
+// v2's per-wave lists and arithmetic; split over up to V4_FMAX blocks per
+// query for Q <= V4_FQ): no batch-wide flag, no gated launches behind the
+// chain.  Three launches per call: bound5, scan4, rescore.
 constexpr float V4_EPS = 0.004f;
 constexpr int V4_S = 65536;     // sample rows for the admission bound
 constexpr int V4_WPS = 3;       // min waves per SIMD of scan4 for NQB > 4
 constexpr int V4_CAP = 4096;     // admitted rows per query
-constexpr int V4_SCAP = 256;     // rows at or under the selected k-th bin
 constexpr int V4_OVF = 1 << 30;  // count-word mark: a block dropped some of this query's rows
 constexpr int V4_QC = 256;       // queries per block (LDS: V4_QC x d bf16)
 // table rows per block: few query blocks -> long blocks (the per-block
@@ -1226,8 +1225,8 @@ __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__
                                                        const float* __restrict__ qn, int64_t Q, int F,
                                                        float* pd, int64_t* pi, int* pcnt) {
   __shared__ float dl[V4_CAP];
-  __shared__ float cd[V4_SCAP];
-  __shared__ int ci[V4_SCAP];
+  __shared__ float cd[V4_CAP];   // the rows at or under the k-th's bin: all of the list at most
+  __shared__ int ci[V4_CAP];
   __shared__ int cnt;
   __shared__ int last;
   static_assert(V4_CAP >= 2 * B4_T, "exact fallback lists live in dl");
@@ -1292,14 +1291,14 @@ __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__
   for (int e = threadIdx.x; e < n; e += B4_T)
     if (__float_as_uint(dl[e]) <= tk) {
       const int pos = atomicAdd(&cnt, 1);
-      if (pos < V4_SCAP) { cd[pos] = dl[e]; ci[pos] = e < B4_T ? i0 : rl[e]; }
+      cd[pos] = dl[e];
+      ci[pos] = e < B4_T ? i0 : rl[e];
     }
   __syncthreads();
+  // (many rows sharing the k-th's bin -- duplicates -- are sorted here too,
+  // up to the whole list: round 5 sent a bin of more than 256 rows to the
+  // exact table scan, 9.9 ms for 256 such queries over 1M rows)
   const int nv = cnt;
-  if (nv > V4_SCAP) {   // too many rows share the k-th bin
-    fail();
-    return;
-  }
   if (nv <= 64) {   // (the usual case) one wave's register sort, no more barriers
     if (threadIdx.x < 64) {
       const int lane = threadIdx.x;

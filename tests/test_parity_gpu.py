@@ -723,6 +723,28 @@ def test_cosine_knn_v4_all_overflow_split_fallback(dev, Q, dim):
     assert np.array_equal(i, i32[:Q]) and np.array_equal(d, d32[:Q])
 
 
+@pytest.mark.parametrize("Q,ndup", [(32, 300), (256, 3000), (2, 4000)])
+def test_cosine_knn_v4_crowded_bin_sorted(dev, Q, ndup):
+    """Hundreds to thousands of rows tied at the k-th distance (duplicates
+    of each query's direction, fewer than the list's 4096 slots): the
+    rescore block sorts all of them by (distance, row) -- round 5 sent a bin
+    of more than 256 rows to the exact whole-table scan -- and returns the
+    exact top-k: each query's 11 lowest duplicate rows."""
+    import dcnr
+    g = torch.Generator(device=dev).manual_seed(23 + Q)
+    n = 900_000
+    table = torch.randn(n, 64, device=dev, generator=g)
+    q = torch.randn(Q, 64, device=dev, generator=g)
+    rows = torch.randperm(n, device=dev, generator=g)[:Q * ndup].view(Q, ndup)
+    for j in range(Q):
+        table[rows[j]] = q[j]
+    nn_ = dcnr.NearestNeighbors(metric="cosine", algorithm="brute").fit(table)
+    d, i = nn_.kneighbors(q, n_neighbors=11)
+    want = torch.sort(rows, dim=1).values[:, :11].cpu().numpy()
+    assert np.array_equal(i, want)
+    assert np.all(d <= 2e-6)
+
+
 @pytest.mark.parametrize("M,K,N,out_f32", [(4096, 512, 512, 0), (1000, 456, 512, 1),
                                            (333, 64, 96, 0), (70000, 128, 256, 1)])
 def test_linear_bf16_vs_torch(dev, M, K, N, out_f32):
