@@ -780,7 +780,9 @@ def main():
                            "sharded AdamW + all-gather; categorical tables: all-reduce"
                            if args.exchange == "sparse"
                            else "dense params: all-reduce started in the backward (overlapped); "
-                                "tables: reduce-scatter + sharded AdamW + all-gather")},
+                                "tables: reduce-scatter + sharded AdamW + all-gather, "
+                                f"pipelined in {trainer.chunks} chunks"),
+                       "exchange_chunks": trainer.chunks if world > 1 else None},
             "distributed": None if world == 1 else {
                 "backend": dist.get_backend(), "world_size": world, "ranks": ranks_info,
                 "distinct_devices": len({(r["pci_bus_id"], r["uuid"], r["local_rank"]) for r in ranks_info})},

@@ -16,7 +16,14 @@ optimizer.step) as native calls over flat parameter/gradient/moment buffers:
              rank's 1/world shard with its 1/world of the moments,
              all-gather of the updated parameters -- the all-reduce's bytes,
              1/world of the optimizer's HBM traffic and moment memory
-             (ZeRO-1 style); the dense segment is updated whole on every rank
+             (ZeRO-1 style); the dense segment is updated whole on every rank,
+             under the first reduce-scatter.  The segment is exchanged in
+             ``exchange_chunks`` pieces (default 4), each split over the ranks,
+             so a rank owns one piece of every chunk and each chunk's
+             reduce-scatter input and all-gather output are contiguous; the
+             chunks run as a pipeline on the communicator's stream:
+             reduce-scatter(c+1) under AdamW(c) under all-gather(c-1), the
+             segment's tail (the item and categorical tables) first
            shard_optimizer=False: all-reduce, every rank updates everything
            exchange="sparse" (ZeRO-1 like the default): the user and item
              tables' gradient rows the rank's batch touched -- read from the
@@ -66,7 +73,8 @@ class FusedTrainer:
 
     def __init__(self, model: DCN_RecSys, lr=1e-3, weight_decay=1e-2, optimizer_name='AdamW',
                  betas=(0.9, 0.999), eps=1e-8, process_group=None, sync_bn=False,
-                 shard_optimizer=None, exchange="dense", sparse_ops=None, dense_table_grads=False):
+                 shard_optimizer=None, exchange="dense", sparse_ops=None, dense_table_grads=False,
+                 exchange_chunks=4):
         if optimizer_name not in ('AdamW', 'Adam'):
             raise ValueError("optimizer_name must be 'AdamW' or 'Adam' (train.py:201-204)")
         self.model = model
@@ -86,13 +94,20 @@ class FusedTrainer:
                                  f"ranks (world {self.world})")
             shard_optimizer = True
         self.shard = (self.world > 1) if shard_optimizer is None else bool(shard_optimizer)
+        if int(exchange_chunks) < 1:
+            raise ValueError("exchange_chunks must be >= 1")
+        # the dense exchange's pipeline depth (module docstring); the sparse
+        # exchange keeps one contiguous shard per rank (its owners are offset // Es)
+        self.chunks = int(exchange_chunks) if (self.shard and exchange == "dense"
+                                               and self.world > 1) else 1
         # the sparse exchange's layout: the user and item tables at flat
         # offsets 0 and nu (rows of emb_dim elements), the categorical tables
         # after them (dense all-reduce); rows must not straddle a shard, so
         # both tables and the shards are padded to multiples of lcm(64, emb_dim)
         d = model._dims['emb_dim']
         unit = 64 * d // math.gcd(64, d) if exchange == "sparse" else 64
-        self.flat, self.gflat = model.flatten_(pad_to=unit * self.world, table_align=unit)
+        self.flat, self.gflat = model.flatten_(pad_to=unit * self.world * self.chunks,
+                                               table_align=unit)
         self.E = model.flat_emb_end                      # embedding segment [0, E)
         N = self.flat.numel()
         self.Es = self.E // self.world if self.shard else self.E   # this rank's embedding moments
@@ -339,24 +354,76 @@ class FusedTrainer:
                 if touched is not None or self._sparse._pending is None:
                     self._sparse.begin(touched if touched is not None else self.touched_rows())
                 self.last_exchange = self._sparse.finish(self.gflat, self.gshard)
+                pshard = self.flat[self.rank * Es:(self.rank + 1) * Es]
+                adam(pshard, self.gshard, self.m[:Es], self.v[:Es], self.step_count)
+                dist.all_gather_into_tensor(self.flat[:E], pshard, group=self.pg)
             else:
-                rs = dist.reduce_scatter_tensor(self.gshard, self.gflat[:E], op=dist.ReduceOp.SUM,
-                                                group=self.pg, async_op=True)
-                # the dense segment's AdamW (its all-reduce ran under the
-                # embedding backward) goes under the tables' reduce-scatter
-                dense.wait()
-                adam(self.flat[E:], self.gflat[E:], self.m[Es:], self.v[Es:], self.step_count)
-                dense = None
-                rs.wait()
-            pshard = self.flat[self.rank * Es:(self.rank + 1) * Es]
-            adam(pshard, self.gshard, self.m[:Es], self.v[:Es], self.step_count)
-            dist.all_gather_into_tensor(self.flat[:E], pshard, group=self.pg)
+                dense = self._chunked_exchange(adam, dense)
         else:
             dist.all_reduce(self.gflat[:E], op=dist.ReduceOp.SUM, group=self.pg)
             adam(self.flat[:E], self.gflat[:E], self.m[:E], self.v[:E], self.step_count)
         if dense is not None:
             dense.wait()
             adam(self.flat[E:], self.gflat[E:], self.m[Es:], self.v[Es:], self.step_count)
+
+    def shard_ranges(self):
+        """The flat ranges [lo, hi) of the embedding segment this rank owns,
+        in the order its ``gshard`` and embedding moments hold them (one range
+        unless the dense exchange runs in chunks; empty without sharding).
+        The sparse exchange owns one contiguous range per rank, so switching
+        ``exchange`` on a live trainer with chunks > 1 re-assigns the
+        embedding moments (bench.py does it only to time the other exchange)."""
+        if not self.shard:
+            return []
+        W, r, C = self.world, self.rank, self.chunks
+        if self.exchange == "sparse":
+            return [(r * self.Es, (r + 1) * self.Es)]
+        cs = self.Es // C
+        return [(c * W * cs + r * cs, c * W * cs + (r + 1) * cs) for c in range(C)]
+
+    def _chunked_exchange(self, adam, dense):
+        """The dense embedding exchange as a pipeline of ``self.chunks``
+        chunks (module docstring).  Chunk c is the flat range
+        [c W cs, (c+1) W cs) (cs = Es / chunks, W = world); rank r owns its
+        piece [c W cs + r cs, c W cs + (r+1) cs), whose gradient and moments
+        are gshard / m / v [c cs, (c+1) cs).  The communicator runs its
+        collectives in issue order, so issuing RS(0), RS(1), then per chunk
+        AG(c) followed by RS(c+2) lets RS(c+1) run under AdamW(c) and AG(c)
+        under AdamW(c+1).  Each element is still the SUM of the ranks'
+        gradients (at world 2 the same bits as one reduce-scatter).  Returns
+        None once the dense segment's AdamW is enqueued."""
+        E, Es, W, r, C = self.E, self.Es, self.world, self.rank, self.chunks
+        cs = Es // C
+        order = list(range(C))[::-1]   # the segment's tail (item, categorical tables) first
+        rs = {}
+
+        def start(i):
+            if i < C:
+                c = order[i]
+                rs[c] = dist.reduce_scatter_tensor(self.gshard[c * cs:(c + 1) * cs],
+                                                   self.gflat[c * W * cs:(c + 1) * W * cs],
+                                                   op=dist.ReduceOp.SUM, group=self.pg,
+                                                   async_op=True)
+
+        start(0)
+        start(1)
+        # the dense segment's AdamW (its all-reduce ran under the embedding
+        # backward) goes under the first reduce-scatters
+        dense.wait()
+        adam(self.flat[E:], self.gflat[E:], self.m[Es:], self.v[Es:], self.step_count)
+        gathers = []
+        for i, c in enumerate(order):
+            rs.pop(c).wait()
+            lo = c * W * cs + r * cs
+            pc = self.flat[lo:lo + cs]
+            adam(pc, self.gshard[c * cs:(c + 1) * cs], self.m[c * cs:(c + 1) * cs],
+                 self.v[c * cs:(c + 1) * cs], self.step_count)
+            gathers.append(dist.all_gather_into_tensor(self.flat[c * W * cs:(c + 1) * W * cs], pc,
+                                                       group=self.pg, async_op=True))
+            start(i + 2)
+        for g in gathers:
+            g.wait()
+        return None
 
     def optimizer_step(self):
         """Adam/AdamW over the local flat gradient (no exchange)."""

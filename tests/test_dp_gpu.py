@@ -224,7 +224,8 @@ def _worker_hook(rank, world, port, shard, cfg_name="toy", sync_bn=True):
         dist.all_reduce(g, op=dist.ReduceOp.SUM)
         assert torch.equal(dense_hook, g[E:]), "dense segment: hook exchange != explicit all-reduce"
         Es = tr.Es
-        emb_ref = g[rank * Es:(rank + 1) * Es] if shard else g[:E]
+        emb_ref = torch.cat([g[lo:hi] for lo, hi in tr.shard_ranges()]) if shard else g[:E]
+        assert not shard or sum(hi - lo for lo, hi in tr.shard_ranges()) == Es
         assert torch.equal(emb_hook, emb_ref), "embedding segment differs"
         assert dense_hook.abs().sum().item() > 0
         if cfg_name == "bench":   # the shard boundary of the 142 MB table segment
@@ -290,7 +291,9 @@ def _worker_sparse(rank, world, port, cfg_name="toy", sync_bn=True):
                     assert torch.equal(own.cpu(), torch.bincount((allw // tr.Es).cpu(),
                                                                  minlength=world))
             torch.cuda.synchronize()
-            flats.append(tr.flat.clone())
+            # per parameter: the dense exchange's chunked layout pads the
+            # table segment differently from the sparse exchange's
+            flats.append(torch.cat([p.detach().reshape(-1) for p in m.param_tensors()]))
             assert tr.exchange != "sparse" or tr.last_exchange["rows_sent"] > 0
             del tr, m
             torch.cuda.empty_cache()

@@ -202,21 +202,36 @@ def _exchange_worker(rank, world, port):
     _init(rank, world, port)
     try:
         import dcnr
-        for shard in (True, False):
+        finals = {}
+        for shard, chunks in ((True, 4), (True, 1), (True, 3), (False, 4)):
             torch.manual_seed(0)
             m = dcnr.DCN_RecSys(50, 40, {"a": 10, "b": 3}, 3,
                                 dict(emb_dim=8, hidden_dim=16, n_cross_layers=1, n_res_blocks=1,
                                      dropout=0.0))
-            tr = dcnr.FusedTrainer(m, lr=1e-2, weight_decay=1e-2, shard_optimizer=shard)
+            tr = dcnr.FusedTrainer(m, lr=1e-2, weight_decay=1e-2, shard_optimizer=shard,
+                                   exchange_chunks=chunks)
             assert tr.flat.numel() % (64 * world) == 0 and tr.E % (64 * world) == 0
+            assert tr.chunks == (chunks if shard else 1)
+            # the owned pieces: one per chunk, together 1/world of the segment
+            rng = tr.shard_ranges()
+            assert len(rng) == (chunks if shard else 0)
+            assert sum(hi - lo for lo, hi in rng) == (tr.E // world if shard else 0)
             # the embedding segment's moments are sharded, the dense segment's whole
             assert tr.m.numel() == tr.E // (world if shard else 1) + tr.flat.numel() - tr.E
             ref_p = tr.flat.clone()
             ref_m = torch.zeros_like(ref_p)
             ref_v = torch.zeros_like(ref_p)
             for step in range(1, 4):
-                gs = [torch.Generator().manual_seed(100 * step + r) for r in range(world)]
-                grads = [torch.randn(tr.flat.numel(), generator=gg) for gg in gs]
+                # per parameter (not per flat position: the padding depends on
+                # the chunk count), zeros in the padding
+                grads = []
+                for r in range(world):
+                    gg = torch.zeros(tr.flat.numel())
+                    for k, p in enumerate(m.param_tensors()):
+                        o = (p.data_ptr() - tr.flat.data_ptr()) // 4
+                        gen = torch.Generator().manual_seed(1000 * step + 10 * k + r)
+                        gg[o:o + p.numel()] = torch.randn(p.numel(), generator=gen)
+                    grads.append(gg)
                 tr.gflat.copy_(grads[rank])
                 tr.exchange_and_update(adam=_host_adam)
                 _host_adam(ref_p, sum(grads), ref_m, ref_v, step)
@@ -227,6 +242,10 @@ def _exchange_worker(rank, world, port):
                 assert all(torch.equal(allp[0], a) for a in allp[1:])
             # the module's parameters are views of the exchanged flat buffer
             assert m.final_linear.weight.data_ptr() >= tr.flat.data_ptr()
+            finals[(shard, chunks)] = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+        if world == 2:   # a sum of two is order-free: chunking changes no bit
+            assert torch.equal(finals[(True, 4)], finals[(True, 1)])
+            assert torch.equal(finals[(True, 3)], finals[(True, 1)])
     finally:
         dist.destroy_process_group()
 
