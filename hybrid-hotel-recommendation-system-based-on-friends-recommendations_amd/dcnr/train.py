@@ -21,9 +21,10 @@ optimizer.step) as native calls over flat parameter/gradient/moment buffers:
              ``exchange_chunks`` pieces (default 4), each split over the ranks,
              so a rank owns one piece of every chunk and each chunk's
              reduce-scatter input and all-gather output are contiguous; the
-             chunks run as a pipeline on the communicator's stream:
-             reduce-scatter(c+1) under AdamW(c) under all-gather(c-1), the
-             segment's tail (the item and categorical tables) first
+             chunks run as a pipeline over two communicators (two RCCL
+             streams): reduce-scatter(c+1) under AdamW(c) under
+             all-gather(c-1), the segment's tail (the item and categorical
+             tables) first
            shard_optimizer=False: all-reduce, every rank updates everything
            exchange="sparse" (ZeRO-1 like the default): the user and item
              tables' gradient rows the rank's batch touched -- read from the
@@ -100,6 +101,13 @@ class FusedTrainer:
         # exchange keeps one contiguous shard per rank (its owners are offset // Es)
         self.chunks = int(exchange_chunks) if (self.shard and exchange == "dense"
                                                and self.world > 1) else 1
+        # the pipeline's all-gathers run on a second communicator (its own
+        # stream), beside the reduce-scatters on the first
+        self._ag_pg = None
+        if self.chunks > 1:
+            ranks = (dist.get_process_group_ranks(process_group) if process_group is not None
+                     else list(range(self.world)))
+            self._ag_pg = dist.new_group(ranks=ranks, use_local_synchronization=True)
         # the sparse exchange's layout: the user and item tables at flat
         # offsets 0 and nu (rows of emb_dim elements), the categorical tables
         # after them (dense all-reduce); rows must not straddle a shard, so
@@ -387,40 +395,32 @@ class FusedTrainer:
         [c W cs, (c+1) W cs) (cs = Es / chunks, W = world); rank r owns its
         piece [c W cs + r cs, c W cs + (r+1) cs), whose gradient and moments
         are gshard / m / v [c cs, (c+1) cs).  The communicator runs its
-        collectives in issue order, so issuing RS(0), RS(1), then per chunk
-        AG(c) followed by RS(c+2) lets RS(c+1) run under AdamW(c) and AG(c)
-        under AdamW(c+1).  Each element is still the SUM of the ranks'
+        collectives in issue order: every reduce-scatter is issued up front on
+        the trainer's group, each all-gather on a second group (its own
+        stream) once its chunk's AdamW is enqueued, so RS(c+1) runs under
+        AdamW(c) and beside AG(c-1).  Each element is still the SUM of the ranks'
         gradients (at world 2 the same bits as one reduce-scatter).  Returns
         None once the dense segment's AdamW is enqueued."""
         E, Es, W, r, C = self.E, self.Es, self.world, self.rank, self.chunks
         cs = Es // C
         order = list(range(C))[::-1]   # the segment's tail (item, categorical tables) first
-        rs = {}
-
-        def start(i):
-            if i < C:
-                c = order[i]
-                rs[c] = dist.reduce_scatter_tensor(self.gshard[c * cs:(c + 1) * cs],
-                                                   self.gflat[c * W * cs:(c + 1) * W * cs],
-                                                   op=dist.ReduceOp.SUM, group=self.pg,
-                                                   async_op=True)
-
-        start(0)
-        start(1)
+        rs = {c: dist.reduce_scatter_tensor(self.gshard[c * cs:(c + 1) * cs],
+                                            self.gflat[c * W * cs:(c + 1) * W * cs],
+                                            op=dist.ReduceOp.SUM, group=self.pg, async_op=True)
+              for c in order}
         # the dense segment's AdamW (its all-reduce ran under the embedding
         # backward) goes under the first reduce-scatters
         dense.wait()
         adam(self.flat[E:], self.gflat[E:], self.m[Es:], self.v[Es:], self.step_count)
         gathers = []
-        for i, c in enumerate(order):
+        for c in order:
             rs.pop(c).wait()
             lo = c * W * cs + r * cs
             pc = self.flat[lo:lo + cs]
             adam(pc, self.gshard[c * cs:(c + 1) * cs], self.m[c * cs:(c + 1) * cs],
                  self.v[c * cs:(c + 1) * cs], self.step_count)
             gathers.append(dist.all_gather_into_tensor(self.flat[c * W * cs:(c + 1) * W * cs], pc,
-                                                       group=self.pg, async_op=True))
-            start(i + 2)
+                                                       group=self._ag_pg, async_op=True))
         for g in gathers:
             g.wait()
         return None
