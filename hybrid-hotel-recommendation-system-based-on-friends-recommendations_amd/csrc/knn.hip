@@ -79,6 +79,34 @@ __device__ void compact(float* cd, int* ci, int* cnt, float* thr, int k) {
   __syncthreads();
 }
 
+
+// The exact cosine distance's arithmetic, spelled out: x . q per float4
+// chunk with the contraction fixed (fma(w, fma(z, fma(x, y-product)))), then
+// 1 - s / |x| as one fma, clamped to [0, 2].  Written as plain expressions,
+// the compiler picked which product to fuse -- and packed some chunks into
+// v_pk_mul / v_pk_add, unfused -- differently at different call sites, so
+// two scans could give one row distances an ulp apart.  Every exact-distance
+// site (scan v1 / v2, the k-th bound, scan v4's epilogue, the exact
+// fallbacks) sums dot4 over the chunks in order and ends with cos_dist.
+__device__ __forceinline__ float dot4(const float4 x, const float4 q) {
+  return fmaf(x.w, q.w, fmaf(x.z, q.z, fmaf(x.x, q.x, x.y * q.y)));
+}
+// dot4 of one row chunk x against two queries at once on packed fp32 math:
+// qa = {q0.x, q1.x, q0.y, q1.y}, qb = {q0.z, q1.z, q0.w, q1.w} (the
+// batched fallback's interleaved query layout); each lane of the result is
+// dot4(x, q) bit for bit (v_pk_mul / v_pk_fma are pairs of the same ops)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 dot4_q2(const float4 x, const float4 qa, const float4 qb) {
+  f32x2 p = f32x2{x.y, x.y} * f32x2{qa.z, qa.w};
+  p = __builtin_elementwise_fma(f32x2{x.x, x.x}, f32x2{qa.x, qa.y}, p);
+  p = __builtin_elementwise_fma(f32x2{x.z, x.z}, f32x2{qb.x, qb.y}, p);
+  p = __builtin_elementwise_fma(f32x2{x.w, x.w}, f32x2{qb.z, qb.w}, p);
+  return p;
+}
+__device__ __forceinline__ float cos_dist(float s, float ir) {
+  return fminf(fmaxf(fmaf(-s, ir, 1.f), 0.f), 2.f);
+}
+
 template <int MAXV>
 __global__ __launch_bounds__(NT) void scan_kernel(const float* __restrict__ tab,
                                                   const float* __restrict__ inv, int64_t N, int d,
@@ -127,9 +155,9 @@ __global__ __launch_bounds__(NT) void scan_kernel(const float* __restrict__ tab,
         for (int v = 0; v < MAXV; ++v)
           if (v < dv) {
             float4 w = qp[v];
-            s += x[v].x * w.x + x[v].y * w.y + x[v].z * w.z + x[v].w * w.w;
+            s += dot4(x[v], w);
           }
-        float dist = fminf(fmaxf(1.f - s * ir, 0.f), 2.f);
+        float dist = cos_dist(s, ir);
         if (dist <= thr[qq]) {
           int pos = atomicAdd(&cnt[qq], 1);
           cd[qq][pos] = dist;
@@ -246,9 +274,9 @@ __global__ __launch_bounds__(K2_NT) void scan2_kernel(const float* __restrict__ 
 #pragma unroll
       for (int v = 0; v < DV; ++v) {
         const float4 q = qv[qq * DV + v];
-        s += x[v].x * q.x + x[v].y * q.y + x[v].z * q.z + x[v].w * q.w;
+        s += dot4(x[v], q);
       }
-      const float dist = fminf(fmaxf(1.f - s * ir, 0.f), 2.f);
+      const float dist = cos_dist(s, ir);
       float th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thrv), qq));
       const float b0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bound0), qq));
       bool pass = ok && dist < th && dist <= b0;
@@ -500,9 +528,9 @@ __global__ __launch_bounds__(NTB) void kth_bound_kernel(const float* __restrict_
 #pragma unroll
       for (int v = 0; v < DV; ++v) {
         const float4 q = qv[v];
-        s += x[v].x * q.x + x[v].y * q.y + x[v].z * q.z + x[v].w * q.w;
+        s += dot4(x[v], q);
       }
-      dist = fminf(fmaxf(1.f - s * inv[t], 0.f), 2.f);
+      dist = cos_dist(s, inv[t]);
     }
     key[j] = __float_as_uint(dist) & 0x7fffffffu;   // >= 0: bits order like values
   }
@@ -790,7 +818,11 @@ __global__ __launch_bounds__(256) void bound5_kernel(const float* __restrict__ t
     }
     if (g == 0 && qq < nq && lane == 0) {
       qcnt[q0 + qq] = 0;
-      qcnt[Q + 1 + q0 + qq] = 0;   // the split fallback's arrival counter (rescore_kernel)
+      qcnt[Q + 1 + q0 + qq] = 0;   // the fallbacks' arrival counters (rescore_kernel)
+      if (q0 + qq == 0) {          // the overflow word and the batched fallback's 8 queues
+        qcnt[Q] = 0;
+        for (int j = 0; j < 8; ++j) qcnt[2 * Q + 2 + j] = 0;
+      }
     }
   }
   __syncthreads();
@@ -1072,6 +1104,7 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
   if (max(max(c0, c1), max(c2, c3)) > V4_WL) {   // a wave's list overflowed: every query
     for (int q = threadIdx.x; q < nq; q += 256)     // of the block takes the exact path
       atomicOr(&qcnt[qc0 + q], V4_OVF);
+    if (threadIdx.x == 0) qcnt[Q] = 1;              // the call's overflow word
     return;
   }
   // entry j of the block (waves' lists back to back) -> its LDS slot
@@ -1084,6 +1117,7 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
   for (int q = threadIdx.x; q < nq; q += 256) {
     const int c = qn_[q];
     qn_[q] = c ? atomicAdd(&qcnt[qc0 + q], c) : 0;   // this block's range of query q's list
+    if (c && qn_[q] + c > V4_CAP) qcnt[Q] = 1;       // the list overflowed: the call's overflow word
   }
   __syncthreads();
   // exact fp32 distance of every admitted pair, here rather than in the
@@ -1109,9 +1143,9 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
 #pragma unroll
     for (int v = 0; v < DV; ++v) {
       const float4 q = qp[v];
-      s += x[v].x * q.x + x[v].y * q.y + x[v].z * q.z + x[v].w * q.w;
+      s += dot4(x[v], q);
     }
-    const float dist = fminf(fmaxf(1.f - s * ir, 0.f), 2.f);
+    const float dist = cos_dist(s, ir);
     const int pos = atomicAdd(&qn_[qe], 1);
     if (pos < V4_CAP) {   // (past it the query's count exceeds V4_CAP: exact path)
       const int64_t o = (qc0 + qe) * V4_CAP + pos;
@@ -1129,6 +1163,65 @@ __global__ __launch_bounds__(256, NQB > 4 ? V4_WPS : 1) void scan4_kernel(const 
 // the waves' sorted k-lists.  The same (distance, row) order as every other
 // scan, so a query that lands here returns what scan v2 returns.  Needs
 // k <= 32 (two k-lists per 64-lane merge step) and 16 * 64 * 8 B of LDS.
+// scan v2's exact distance of one row (x, its inverse norm ir) to one
+// normalised query (wave-uniform qv): the one expression every exact path
+// uses, so they agree bit for bit
+template <int DV>
+__device__ __forceinline__ float exact_dist(const float4 (&x)[DV], const float4* qv, float ir) {
+  float s = 0.f;
+#pragma unroll
+  for (int v = 0; v < DV; ++v) {
+    const float4 q = qv[v];
+    s += dot4(x[v], q);
+  }
+  return cos_dist(s, ir);
+}
+
+// admit (dd, r) into one wave's k-list (64 LDS slots, compacted when full)
+// while strictly under its k-th best: scan v2's per-wave list protocol
+__device__ __forceinline__ void wave_admit(float* lcd, int* lci, int& c, float& th, int k, int lane,
+                                           bool ok, float dd, int64_t r) {
+  bool pass = ok && dd < th;
+  uint64_t m = __ballot(pass);
+  while (m) {
+    const int room = 64 - c;
+    if (room == 0) {
+      c = wave_compact(lcd, lci, c, k, lane, &th);
+      pass = pass && dd < th;
+      m = __ballot(pass);
+      continue;
+    }
+    const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+    if (pass && rank < room) {
+      lcd[c + rank] = dd;
+      lci[c + rank] = (int)r;
+    }
+    const int n = __popcll(m);
+    c += n < room ? n : room;
+    pass = pass && rank >= room;
+    m = __ballot(pass);
+  }
+}
+
+// merge NW sorted wave k-lists (wave ww's at cd[ww * 64], ci[ww * 64], counts
+// cnt[ww]) in one wave: the k best by (distance, row) in lanes [0, k)
+template <int NW>
+__device__ __forceinline__ void wave_merge_lists(const float* cd, const int* ci, const int* cnt, int k,
+                                                 int lane, float& d, int& i) {
+  d = FLT_MAX;
+  i = INT_MAX;
+  for (int ww = 0; ww < NW; ++ww) {
+    const int cw = cnt[ww];
+    const int sl = ww == 0 ? lane : lane - k;
+    if (ww == 0 || lane >= k) {
+      const bool has = sl >= 0 && sl < k && sl < cw;
+      d = has ? cd[ww * 64 + sl] : FLT_MAX;
+      i = has ? ci[ww * 64 + sl] : INT_MAX;
+    }
+    if (ww > 0) wave_sort64(d, i, lane);
+  }
+}
+
 template <int DV>
 __device__ void exact_query_topk(const float* __restrict__ tab, const float* __restrict__ inv, int64_t lo,
                                  int64_t N, const float* __restrict__ qrow, int k, float* lds, int64_t* idx,
@@ -1150,54 +1243,184 @@ __device__ void exact_query_topk(const float* __restrict__ tab, const float* __r
     const float4* rp = reinterpret_cast<const float4*>(tab + rc * DV * 4);
 #pragma unroll
     for (int v = 0; v < DV; ++v) x[v] = rp[v];
-    const float ir = inv[rc];
-    float s = 0.f;
-#pragma unroll
-    for (int v = 0; v < DV; ++v) {
-      const float4 q = qv[v];
-      s += x[v].x * q.x + x[v].y * q.y + x[v].z * q.z + x[v].w * q.w;
-    }
-    const float dd = fminf(fmaxf(1.f - s * ir, 0.f), 2.f);
-    bool pass = ok && dd < th;
-    uint64_t m = __ballot(pass);
-    while (m) {
-      const int room = 64 - c;
-      if (room == 0) {
-        c = wave_compact(lcd, lci, c, k, lane, &th);
-        pass = pass && dd < th;
-        m = __ballot(pass);
-        continue;
-      }
-      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
-      if (pass && rank < room) {
-        lcd[c + rank] = dd;
-        lci[c + rank] = (int)r;
-      }
-      const int n = __popcll(m);
-      c += n < room ? n : room;
-      pass = pass && rank >= room;
-      m = __ballot(pass);
-    }
+    const float dd = exact_dist<DV>(x, qv, inv[rc]);
+    wave_admit(lcd, lci, c, th, k, lane, ok, dd, r);
   }
   c = wave_compact(lcd, lci, c, k, lane, &th);
   if (lane == 0) cntl[w] = c;
   __syncthreads();
   if (w == 0) {
-    float d = FLT_MAX;
-    int i = INT_MAX;
-    for (int ww = 0; ww < NW; ++ww) {
-      const int cw = cntl[ww];
-      const int sl = ww == 0 ? lane : lane - k;
-      if (ww == 0 || lane >= k) {
-        const bool has = sl >= 0 && sl < k && sl < cw;
-        d = has ? lds[ww * 64 + sl] : FLT_MAX;
-        i = has ? reinterpret_cast<const int*>(lds + NW * 64)[ww * 64 + sl] : INT_MAX;
-      }
-      if (ww > 0) wave_sort64(d, i, lane);
-    }
+    float d;
+    int i;
+    wave_merge_lists<NW>(lds, reinterpret_cast<const int*>(lds + NW * 64), cntl, k, lane, d, i);
     if (lane < k) {
       idx[lane] = (int64_t)i;
       dist[lane] = d;
+    }
+  }
+}
+
+// The batched exact fallback (Q > V4_FQ): work item (group h of V4_BQ
+// queries, row chunk f) scans rows [lo, hi) once for every overflowed query
+// of the group -- each wave holds a row in registers and scores it against
+// each of them (exact_dist: the single-query scan's bits), one k-list per
+// (query, wave) -- then the block's waves merge query qi's wave lists into
+// the item's k-list for that query.  The table is read once per group
+// of V4_BQ queries instead of once per query.
+constexpr int V4_BQ = 8;      // queries per batch work item
+template <int DV, int BT>
+__device__ void exact_batch_item(const float* __restrict__ tab, const float* __restrict__ inv, int64_t lo,
+                                 int64_t hi, const float* __restrict__ qg, unsigned act, int k,
+                                 float* bcd, int* bci, int* bcnt, float* bq, float* pd, int64_t* pi,
+                                 int64_t lstride) {
+  constexpr int NW = BT / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  // the group's queries, interleaved by pairs: chunk v of pair pr at
+  // bq[(pr DV + v) 8 ..] = q0.x q1.x q0.y q1.y q0.z q1.z q0.w q1.w
+  for (int e = threadIdx.x; e < V4_BQ * DV * 4; e += BT) {
+    const int pr = e / (DV * 8), r = e % (DV * 8), v = r / 8, c = (r % 8) / 2, o = r % 2;
+    bq[e] = qg[(2 * pr + o) * DV * 4 + v * 4 + c];
+  }
+  __syncthreads();
+  // query qi's list count and k-th best live in lane qi (two VGPRs, not
+  // 2 x V4_BQ scalars: the kernel's SGPRs are already full)
+  int cv = 0;
+  float thv = FLT_MAX;
+  for (int64_t base = lo + 64 * w; base < hi; base += 64 * NW) {
+    const int64_t r = base + lane;
+    const bool ok = r < hi;
+    const int64_t rc = ok ? r : lo;
+    const float4* rp = reinterpret_cast<const float4*>(tab + rc * DV * 4);
+    const float ir = ((const __attribute__((address_space(1))) float*)inv)[rc];
+    // the V4_BQ distances, float4 chunk by chunk (each query's sum in
+    // exact_dist's order: dot4 per chunk, in order; two queries per packed
+    // op); the queries come from the LDS copy (uniform-address reads into
+    // VGPRs: as scalar loads the compiler hoists them into 4 DV V4_BQ SGPRs
+    // and spills)
+    float sq[V4_BQ];
+#pragma unroll
+    for (int qi = 0; qi < V4_BQ; ++qi) sq[qi] = 0.f;
+    // the whole row first: its DV loads in flight together (global address
+    // space: a flat load would also count against the LDS reads' waits)
+    typedef float f32x4v __attribute__((ext_vector_type(4)));
+    typedef const __attribute__((address_space(1))) f32x4v gf32x4;
+    float4 x[DV];
+#pragma unroll
+    for (int v = 0; v < DV; ++v) {
+      const f32x4v t = ((gf32x4*)rp)[v];
+      x[v] = make_float4(t.x, t.y, t.z, t.w);
+    }
+    const float4* bq4 = reinterpret_cast<const float4*>(bq);
+#pragma unroll
+    for (int v = 0; v < DV; ++v) {
+      const float4 xv = x[v];
+#pragma unroll
+      for (int pr = 0; pr < V4_BQ / 2; ++pr) {
+        const f32x2 p = dot4_q2(xv, bq4[(pr * DV + v) * 2], bq4[(pr * DV + v) * 2 + 1]);
+        sq[2 * pr] += p.x;
+        sq[2 * pr + 1] += p.y;
+      }
+    }
+#pragma unroll
+    for (int qi = 0; qi < V4_BQ; ++qi) sq[qi] = cos_dist(sq[qi], ir);
+#pragma unroll 1
+    for (int qi = 0; qi < V4_BQ; ++qi) {
+      if (!((act >> qi) & 1u)) continue;   // (uniform)
+      float dd = sq[0];
+#pragma unroll
+      for (int j = 1; j < V4_BQ; ++j) dd = qi == j ? sq[j] : dd;
+      int c = __builtin_amdgcn_readlane(cv, qi);
+      float th = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(thv), qi));
+      wave_admit(bcd + (qi * NW + w) * 64, bci + (qi * NW + w) * 64, c, th, k, lane, ok, dd, r);
+      cv = lane == qi ? c : cv;
+      thv = lane == qi ? th : thv;
+    }
+  }
+#pragma unroll
+  for (int qi = 0; qi < V4_BQ; ++qi) {
+    if (!((act >> qi) & 1u)) continue;
+    float th = 0.f;
+    const int cc = wave_compact(bcd + (qi * NW + w) * 64, bci + (qi * NW + w) * 64,
+                                __builtin_amdgcn_readlane(cv, qi), k, lane, &th);
+    if (lane == 0) bcnt[qi * NW + w] = cc;
+  }
+  __syncthreads();
+  for (int qi = w; qi < V4_BQ; qi += NW) {
+    if (!((act >> qi) & 1u)) continue;
+    float d;
+    int i;
+    wave_merge_lists<NW>(bcd + qi * NW * 64, bci + qi * NW * 64, bcnt + qi * NW, k, lane, d, i);
+    if (lane < k) {
+      pd[qi * lstride + lane] = d;
+      pi[qi * lstride + lane] = (int64_t)i;
+    }
+  }
+}
+
+// The batched fallback's work pool (Q > V4_FQ).  scan4 raises the call's
+// overflow word (qcnt[Q]) when any query's list overflows; then every
+// rescore block, its own query done, pulls work items from a queue word
+// (qcnt[2Q + 1]) until they run out.  Item it = (row chunk it / H, group
+// it % H): consecutive items share a chunk, so blocks pulling together read
+// the same rows.  An item scans its chunk for the group's overflowed queries
+// (exact_batch_item); the last of a group's FB items merges each overflowed
+// query's FB k-lists.  Not inlined, so the per-query path keeps its
+// registers (inlined, the kernel spilled SGPRs).  A call with nothing
+// overflowed never enters it: no extra blocks, one extra word read per block.
+template <int DV>
+__device__ __attribute__((noinline)) void batch_fallback_pool(
+    const int* qcnt, int* heads, int k, int64_t* idx, float* dist, const float* __restrict__ tab,
+    const float* __restrict__ inv, int64_t N, const float* __restrict__ qn, int64_t Q, int FB, float* pd,
+    int64_t* pi, int* pcnt, float* bcd, int* bci, int* bcnt, float* bq, int* slot) {
+  constexpr int NW = B4_T / 64;
+  const int64_t H = (Q + V4_BQ - 1) / V4_BQ;
+  // queue g = blockIdx % 8 holds the chunks f = g (mod 8): blocks sharing an
+  // XCD share its queue, so a chunk (<= ~2 MB) is read from HBM once and its
+  // groups' items hit that XCD's L2 (speed only: every queue has blocks
+  // -- Q > 16 -- and every block joins when the overflow word is up)
+  const int g = (int)(blockIdx.x % 8);
+  const int64_t items = H * (FB / 8);
+  for (;;) {
+    __syncthreads();   // (the LDS lists and the slot word are reused)
+    if (threadIdx.x == 0) *slot = atomicAdd(heads + g, 1);
+    __syncthreads();
+    const int64_t it = *slot;
+    if (it >= items) return;
+    const int fb = g + 8 * (int)(it / H);
+    const int64_t h = it % H, q0 = h * V4_BQ;
+    unsigned act = 0;
+    for (int qi = 0; qi < V4_BQ && q0 + qi < Q; ++qi) {
+      const int n = qcnt[q0 + qi];
+      if (n > V4_CAP || n < k) act |= 1u << qi;
+    }
+    if (!act) continue;
+    const int64_t lo = N * fb / FB, hi = N * (fb + 1) / FB;
+    exact_batch_item<DV, B4_T>(tab, inv, lo, hi, qn + q0 * DV * 4, act, k, bcd, bci, bcnt, bq,
+                               pd + (q0 * FB + fb) * k, pi + (q0 * FB + fb) * k, (int64_t)FB * k);
+    if (last_arriver(pcnt + h, FB, slot)) {
+      // the group's last item: its waves merge the overflowed queries' FB k-lists
+      const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+      for (int qi = w; qi < V4_BQ; qi += NW) {
+        if (!((act >> qi) & 1u)) continue;
+        const int64_t qq = q0 + qi;
+        float d = FLT_MAX;
+        int i = INT_MAX;
+        for (int ff = 0; ff < FB; ++ff) {
+          const int sl = ff == 0 ? lane : lane - k;
+          if (ff == 0 || lane >= k) {
+            const bool has = sl >= 0 && sl < k;
+            const float dv = has ? pd[(qq * FB + ff) * k + sl] : FLT_MAX;
+            const int64_t iv = has ? pi[(qq * FB + ff) * k + sl] : (int64_t)INT_MAX;
+            d = dv;
+            i = dv == FLT_MAX ? INT_MAX : (int)iv;
+          }
+          if (ff > 0) wave_sort64(d, i, lane);
+        }
+        if (lane < k) {
+          idx[qq * k + lane] = (int64_t)i;
+          dist[qq * k + lane] = d;
+        }
+      }
     }
   }
 }
@@ -1217,19 +1440,51 @@ constexpr int V4_FQ = 16;          // queries up to which the fallback is split
 inline int v4_fallback_split(int64_t Q) {
   return Q <= V4_FQ ? (int)std::min<int64_t>(V4_FMAX, 256 / Q) : 1;
 }
+// Q > V4_FQ: row chunks of the batched fallback (about V4_BI work items,
+// 8..128 chunks, a multiple of 8); 0: none.  Few large items: all-overflow
+// Q = 256 over 1M x 64 took 1.27 / 1.34 / 1.57 / 1.93 / 2.67 ms at 256 / 512 /
+// 1024 / 2048 / 4096 items (profiles/lab/r06_knn_batch_lab.txt).  The
+// k-lists: Q x chunks x 32 x 12 B, ~12 MB at most.
+constexpr int V4_BI = 256;
+inline int v4_batch_chunks(int64_t Q) {
+  if (Q <= V4_FQ) return 0;
+  const int64_t H = (Q + V4_BQ - 1) / V4_BQ;
+  return (int)std::max<int64_t>(8, std::min<int64_t>(128, (V4_BI / H) / 8 * 8));
+}
+// k-lists per query of either fallback form
+inline int v4_lists(int64_t Q) {
+  const int F = v4_fallback_split(Q);
+  return F > 1 ? F : v4_batch_chunks(Q);
+}
 template <int DV>
 __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__ dists, const int* qcnt,
                                                        const int* rows, int k, int64_t* idx,
                                                        float* dist, const float* __restrict__ tab,
                                                        const float* __restrict__ inv, int64_t N,
                                                        const float* __restrict__ qn, int64_t Q, int F,
-                                                       float* pd, int64_t* pi, int* pcnt) {
-  __shared__ float dl[V4_CAP];
-  __shared__ float cd[V4_CAP];   // the rows at or under the k-th's bin: all of the list at most
-  __shared__ int ci[V4_CAP];
+                                                       int FB, float* pd, int64_t* pi, int* pcnt) {
+  // one LDS image: dl / cd / ci of the per-query path, or the batched
+  // fallback's (query, wave) lists (FB > 0: blocks from Q on, which answer
+  // the overflowed queries)
+  constexpr int NW = B4_T / 64;
+  constexpr int BL = V4_BQ * NW * 64;
+  constexpr int SMW = 3 * V4_CAP > 2 * BL ? 3 * V4_CAP : 2 * BL;
+  __shared__ float smem[SMW];
+  __shared__ int bcnt[V4_BQ * NW];
+  __shared__ float bq[V4_BQ * 64];   // the batched fallback's queries (d <= 64)
+  float* dl = smem;
+  float* cd = smem + V4_CAP;   // the rows at or under the k-th's bin: all of the list at most
+  int* ci = reinterpret_cast<int*>(smem + 2 * V4_CAP);
   __shared__ int cnt;
   __shared__ int last;
   static_assert(V4_CAP >= 2 * B4_T, "exact fallback lists live in dl");
+  // FB > 0: the batched fallback's pool, entered after this block's own
+  // query when scan4 raised the overflow word (or this query overflowed)
+  const bool pool = FB > 0 && qcnt[Q] != 0;
+  auto join_pool = [&]() {
+    batch_fallback_pool<DV>(qcnt, const_cast<int*>(qcnt) + 2 * Q + 2, k, idx, dist, tab, inv, N, qn, Q, FB, pd,
+                            pi, pcnt, smem, reinterpret_cast<int*>(smem + BL), bcnt, bq, &last);
+  };
   const int64_t qq = blockIdx.x % Q;
   const int f = (int)(blockIdx.x / Q);
   auto fail = [&]() {
@@ -1280,7 +1535,8 @@ __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__
   const int n = qcnt[qq];
   if (n > V4_CAP || n < k) {   // overflow (fewer than k admitted rows only when N < k)
     if (F > 1) split();
-    else fail();
+    else if (FB == 0) fail();
+    else join_pool();   // (the pool answers it)
     return;
   }
   if (threadIdx.x == 0) cnt = 0;
@@ -1310,6 +1566,7 @@ __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__
         dist[qq * k + lane] = d;
       }
     }
+    if (pool) join_pool();
     return;
   }
   int n2 = 2;
@@ -1321,6 +1578,7 @@ __global__ __launch_bounds__(B4_T) void rescore_kernel(const float* __restrict__
     idx[qq * k + t] = (int64_t)ci[t];
     dist[qq * k + t] = cd[t];
   }
+  if (pool) join_pool();
 }
 
 // Per query: the k best of nslices k-lists.  All of a chunk's candidates are
@@ -1635,11 +1893,11 @@ bool use_v4(int64_t N, int64_t Q, int d, int k) {
 // [Q][B5_G]
 // the split fallback's k-lists (k <= 32: scan v4's range), for Q <= V4_FQ
 size_t v4_split_bytes(int64_t Q) {
-  const int F = v4_fallback_split(Q);
-  return F > 1 ? rup((size_t)Q * F * 32 * (4 + 8), 256) : 0;
+  const int L = v4_lists(Q);
+  return L > 1 ? rup((size_t)Q * L * 32 * 4, 256) + (size_t)Q * L * 32 * 8 : 0;
 }
 size_t v4_extra(int64_t Q, int d) {
-  return rup((size_t)Q * d * 2, 256) + rup((size_t)Q * 8 + 8, 256) + 2 * (size_t)Q * V4_CAP * 4 +
+  return rup((size_t)Q * d * 2, 256) + rup((size_t)Q * 8 + 48, 256) + 2 * (size_t)Q * V4_CAP * 4 +
          rup((size_t)Q * B5_G * 4, 256) + v4_split_bytes(Q) + 256;
 }
 
@@ -1706,15 +1964,16 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
       char* x = (char*)ws + rup(rup((size_t)Q * ns * k * sizeof(Cand), 256) + (size_t)Q * (d + 1) * 4, 256);
       qb = (bf16*)x;
       x += rup((size_t)Q * d * 2, 256);
-      qcnt = (int*)x;   // [Q] list counts, a word, [Q] split-fallback arrival counters
-      x += rup((size_t)Q * 8 + 8, 256);
+      qcnt = (int*)x;   // [Q] list counts, the overflow word, [Q] fallback arrival counters,
+                        // a spare word, the batched fallback's 8 queue heads
+      x += rup((size_t)Q * 8 + 48, 256);
       rows = (int*)x;
       dists = (float*)(rows + Q * V4_CAP);
       x += 2 * (size_t)Q * V4_CAP * 4;
       bmins = (float*)x;
       x += rup((size_t)Q * B5_G * 4, 256);
       split_d = (float*)x;
-      split_i = (int64_t*)(x + rup((size_t)Q * v4_fallback_split(Q) * 32 * 4, 256));
+      split_i = (int64_t*)(x + rup((size_t)Q * v4_lists(Q) * 32 * 4, 256));
     }
     if (!v4) {
       switch (d / 4) {
@@ -1780,14 +2039,17 @@ dcnr_status cosine_topk(const float* t, const float* inv, const bf16* tb, int64_
   CASE4(2, 8, sel, g, n, rp) CASE4(2, 16, sel, g, n, rp)
       CASES4(NQ, g4, N, rpb)
       DCNR_LAUNCH_CHECK();
-      // (a query whose list overflowed scans the table exactly in its block)
+      // (a query whose list overflowed: the split fallback for Q <= V4_FQ,
+      // else the batched fallback's pool, inside these blocks)
       const int F = v4_fallback_split(Q);
+      const int FB = v4_batch_chunks(Q);
+      const unsigned nb = (unsigned)(Q * F);
       if (d == 32)
-        hipLaunchKernelGGL(rescore_kernel<8>, dim3((unsigned)(Q * F)), dim3(B4_T), 0, s, dists, qcnt, rows, k,
-                           idx, dist, t, inv, N, qn, Q, F, split_d, split_i, qcnt + Q + 1);
+        hipLaunchKernelGGL(rescore_kernel<8>, dim3(nb), dim3(B4_T), 0, s, dists, qcnt, rows, k,
+                           idx, dist, t, inv, N, qn, Q, F, FB, split_d, split_i, qcnt + Q + 1);
       else
-        hipLaunchKernelGGL(rescore_kernel<16>, dim3((unsigned)(Q * F)), dim3(B4_T), 0, s, dists, qcnt, rows, k,
-                           idx, dist, t, inv, N, qn, Q, F, split_d, split_i, qcnt + Q + 1);
+        hipLaunchKernelGGL(rescore_kernel<16>, dim3(nb), dim3(B4_T), 0, s, dists, qcnt, rows, k,
+                           idx, dist, t, inv, N, qn, Q, F, FB, split_d, split_i, qcnt + Q + 1);
       DCNR_LAUNCH_CHECK();
 #undef CASES4
 #undef CASE4

@@ -723,6 +723,35 @@ def test_cosine_knn_v4_all_overflow_split_fallback(dev, Q, dim):
     assert np.array_equal(i, i32[:Q]) and np.array_equal(d, d32[:Q])
 
 
+@pytest.mark.parametrize("Q,dim,every", [(40, 64, 3), (256, 64, 4), (256, 32, 1), (17, 64, 1)])
+def test_cosine_knn_v4_batched_fallback(dev, Q, dim, every):
+    """Q > 16 with some (every-th) or all queries overflowing (5000
+    duplicates of their direction): the batched exact fallback -- groups of 8
+    queries x row chunks, each chunk read once per group, per-group
+    last-arriver merge (knn.hip exact_batch_item) -- returns each overflowed
+    query's 11 lowest duplicate rows, and the whole answer equals the same
+    queries asked 16 at a time (the split fallback and the unchanged
+    per-query path), bit for bit."""
+    import dcnr
+    g = torch.Generator(device=dev).manual_seed(31 + Q + dim + every)
+    over = list(range(0, Q, every))
+    n = 150_000 + 5000 * len(over)
+    table = torch.randn(n, dim, device=dev, generator=g)
+    q = torch.randn(Q, dim, device=dev, generator=g)
+    perm = torch.randperm(n, device=dev, generator=g)
+    dups = {j: perm[5000 * t:5000 * (t + 1)] for t, j in enumerate(over)}
+    for j, rr in dups.items():
+        table[rr] = q[j] * (0.5 + j % 3)
+    nn_ = dcnr.NearestNeighbors(metric="cosine", algorithm="brute").fit(table)
+    d, i = nn_.kneighbors(q, n_neighbors=11)
+    for j, rr in dups.items():
+        assert np.all(d[j] <= 2e-6), j
+        assert i[j].tolist() == sorted(rr.cpu().tolist())[:11], j
+    parts = [nn_.kneighbors(q[a:a + 16], n_neighbors=11) for a in range(0, Q, 16)]
+    assert np.array_equal(i, np.concatenate([p[1] for p in parts]))
+    assert np.array_equal(d, np.concatenate([p[0] for p in parts]))
+
+
 @pytest.mark.parametrize("Q,ndup", [(32, 300), (256, 3000), (2, 4000)])
 def test_cosine_knn_v4_crowded_bin_sorted(dev, Q, ndup):
     """Hundreds to thousands of rows tied at the k-th distance (duplicates
