@@ -662,11 +662,21 @@ dcnr_status linear_fwd_stats(const Dims& d, const Layout& L, const void* A, int 
 }
 
 // C = mask(H) * (X W^T [+ R]) and part = [sum C, sum C*xhat(T)] (BN backward)
+// xbn (optional): X is a BatchNorm backward's du; the GEMM's operand is its
+// dt = bn_bwd_dt(du, xt, xbn mean / invstd, L.coef), also written to dt_out
+// (the row pass folded into this GEMM, gemm_ws.hip XBN)
+struct XbnOperand { const void* xt; const BnBufs* bn; void* dt_out; };
 dcnr_status linear_dx_bn(const Dims& d, const Layout& L, int epi, const void* X, const void* Wt,
                          const void* R, void* C, const uint8_t* Hbits, float hscale,
-                         const void* T, const BnBufs& bn, int64_t B, int* nc, hipStream_t s) {
+                         const void* T, const BnBufs& bn, int64_t B, int* nc, hipStream_t s,
+                         const XbnOperand* xbn = nullptr) {
   NtArgs a;
   memset(&a, 0, sizeof(a));
+  if (xbn) {
+    a.Tx = (const bf16*)xbn->xt;
+    a.xmean = xbn->bn->mean; a.xinvstd = xbn->bn->invstd; a.xcoef = L.coef;
+    a.dt = (bf16*)xbn->dt_out;
+  }
   a.X = (const bf16*)X; a.ldx = d.Hp; a.M = B; a.K = d.Hp;
   a.W = (const bf16*)Wt; a.ldw = d.Hp; a.N = d.Hp;
   a.C = C; a.ldc = d.Hp;
@@ -1281,6 +1291,8 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
 
   const void* Gin = nullptr;  // gradient wrt the current block output (null: rank-1 dz*wf)
   const bool fuse = epi_stats_ok(d);   // BN partials from the dX GEMM epilogues
+  // the BN backward's row passes folded into those GEMMs (bf16, K = Hp in (256, 512])
+  const bool xbn_ok = fuse && d.prec == DCNR_PREC_BF16 && gemm_ws_xbn_supported(NT_EPI_DROP_BN, d.Hp, d.Hp);
   int nc_du = 0;   // > 0: L.du and its BN2 partials were made by the previous dX GEMM
   for (int j = d.R - 1; j >= 0; --j) {
     const auto& Bk = P.blk[j];
@@ -1306,21 +1318,28 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       TRY(bn_bwd_reduce(desc, d, L, nc, 3, B, Bk.g2, bn2.invstd, Gk.g2, Gk.be2,
                         Gin ? nullptr : Gr.wf, Gk.b2, accumulate, s));
     }
-    if (!Gin && j == d.R - 1 && L.mask_h[d.R] && d.prec == DCNR_PREC_BF16)
+    const bool rank1 = !Gin && j == d.R - 1 && L.mask_h[d.R] && d.prec == DCNR_PREC_BF16;
+    // the BN2 backward's row pass folded into the DROP_BN dX GEMM (du and t2
+    // in, dt2 out for dW2) where that GEMM runs the fused epilogue
+    const bool xbn2 = fuse && !rank1 && xbn_ok;
+    if (rank1)
       TRYB(DCNR_K_ROWWISE, 2 * act_b(d, B) + mask_b(d, B) + 4.0 * B,
            bwd_bn2_apply_rank1(L.mask_h[d.R], dz, P.wf, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
                                dt2, s));
-    else
+    else if (!xbn2)
       TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn2_apply2(d.prec, du, L.t2[j], bn2.mean, bn2.invstd, L.coef, B, Hp, Hp,
                          dt2, L.part, &nc, s));
-    // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2
-    TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe));
+    // ---- layer2: dW2 = dt2^T a1 ; da = dt2 W2 (the weight gradient after
+    // the GEMM that makes dt2 when the row pass is folded in)
+    if (!xbn2) TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe));
     if (fuse) {
       // dy1 = (dt2 W2) * [a1 != 0] / (1-p): relu and dropout masks from the
       // saved activation, BN1 partials in the same pass
-      TRYB(DCNR_K_GEMM_DX, 3 * act_b(d, B) + mask_b(d, B) + w_b(d, d.Hp), linear_dx_bn(d, L, NT_EPI_DROP_BN, dt2, L.W2t[j], nullptr, da,
-                                        L.mask_a1[j], p > 0.f ? 1.f / (1.f - p) : 1.f, L.t1[j],
-                                        bn1, B, &nc, s));
+      const XbnOperand xo{L.t2[j], &bn2, dt2};
+      TRYB(DCNR_K_GEMM_DX, (xbn2 ? 5 : 3) * act_b(d, B) + mask_b(d, B) + w_b(d, d.Hp),
+           linear_dx_bn(d, L, NT_EPI_DROP_BN, xbn2 ? du : dt2, L.W2t[j], nullptr, da, L.mask_a1[j],
+                        p > 0.f ? 1.f / (1.f - p) : 1.f, L.t1[j], bn1, B, &nc, s, xbn2 ? &xo : nullptr));
+      if (xbn2) TRY(linear_dw(d, L, dt2, Hp, Hp, L.a1s[j], Hp, Hp, B, Gk.w2, H, H, accumulate, s, pipe));
     } else {
       GemmArgs g;
       memset(&g, 0, sizeof(g));
@@ -1333,17 +1352,24 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     }
     TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
                         accumulate, s));
-    TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_apply2(d.prec, da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, dt1,
-                       L.part, &nc, s));
-    // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
-    TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe));
+    // the BN1 backward's row pass folded into the RESID_BN dX GEMM likewise
+    const bool xbn1 = fuse && j > 0 && xbn_ok;
+    if (!xbn1) {
+      TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_apply2(d.prec, da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, dt1,
+                         L.part, &nc, s));
+      // ---- layer1: dW1 = dt1^T h_j ; G = dt1 W1 + du
+      TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe));
+    }
     if (fuse && j > 0) {
       // G is only consumed by block j-1's BN2 backward: emit its du = G * [h_j > 0]
       // (in place over this block's du, the residual operand, unless
       // KEEP_INTERMEDIATES) and the partials
       const BnBufs& bp = L.bn[2 * (j - 1) + 1];
-      TRYB(DCNR_K_GEMM_DX, 4 * act_b(d, B) + mask_b(d, B) + w_b(d, d.Hp), linear_dx_bn(d, L, NT_EPI_RESID_BN, dt1, L.W1t[j], du, L.duk[j - 1],
-                                        L.mask_h[j], 1.f, L.t2[j - 1], bp, B, &nc_du, s));
+      const XbnOperand xo{L.t1[j], &bn1, dt1};
+      TRYB(DCNR_K_GEMM_DX, (xbn1 ? 6 : 4) * act_b(d, B) + mask_b(d, B) + w_b(d, d.Hp),
+           linear_dx_bn(d, L, NT_EPI_RESID_BN, xbn1 ? da : dt1, L.W1t[j], du, L.duk[j - 1], L.mask_h[j], 1.f,
+                        L.t2[j - 1], bp, B, &nc_du, s, xbn1 ? &xo : nullptr));
+      if (xbn1) TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe));
       Gin = L.duk[j - 1];
     } else {
       GemmArgs g;

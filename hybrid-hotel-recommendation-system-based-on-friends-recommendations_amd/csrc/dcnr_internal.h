@@ -145,6 +145,17 @@ __device__ __forceinline__ bool last_arriver(int* counter, int n_arrivals, int* 
 // and a negative-signed NaN give +0.  (fmaxf would map every NaN to 0.)
 __device__ __forceinline__ float relu_f(float x) { return __int_as_float(max(__float_as_int(x), 0)); }
 
+// BatchNorm backward apply (train.py:225 through nn.BatchNorm1d, train
+// mode): dt = k0 du - k1 xhat - k2, xhat = (t - mean) invstd, with the
+// per-column k0 = gamma invstd, k1, k2 from the batch sums.  One fixed
+// operation order for the row passes (Bwd*ApplyOp) and the dX GEMM's fused
+// operand transform (gemm_ws.hip), so the two give the same bits.
+__device__ __forceinline__ float bn_bwd_dt(float u, float t, float mu, float is, float k0, float k1,
+                                           float k2) {
+  const float xh = (t - mu) * is;
+  return fmaf(-k1, xh, k0 * u) - k2;
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -373,9 +384,16 @@ struct NtArgs {
                                                     // headp rows ldh apart, ldh >= M)
   float* part;                                      // column partials (stats epilogues)
   int Nr;                                           // real columns (eval BN / head: N pads to 8)
+  // operand transform (RESID_BN / DROP_BN, Tx != null): X holds a BatchNorm
+  // backward's du, and the GEMM's operand is dt = bn_bwd_dt(du, Tx, xmean,
+  // xinvstd, xcoef[0 / K / 2K]) per column of K, written to dt (row stride
+  // ldx) for the weight gradient -- the row pass folded into the dX GEMM
+  const bf16* Tx; const float* xmean; const float* xinvstd; const float* xcoef; bf16* dt;
   int nslices, groups; int64_t mtiles;   // filled by gemm_ws
 };
 bool gemm_ws_supported(int64_t K, int64_t N);
+// the dX GEMMs' fused BatchNorm-backward operand transform (NtArgs.Tx)
+bool gemm_ws_xbn_supported(int epi, int64_t K, int64_t N);
 // the train forward's BIAS / BIAS_STATS epilogues at 256 < K <= 512: the
 // pipelined one-wave-per-SIMD variant (gemm_wsp.hip), taken by gemm_ws
 bool gemm_wsp_supported(int epi, int64_t K, int64_t N);

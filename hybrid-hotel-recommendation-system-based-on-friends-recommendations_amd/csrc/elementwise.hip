@@ -331,10 +331,7 @@ template <typename T> struct Bwd2ApplyOp {
   }
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[1][VE<T>]) const {
 #pragma unroll
-    for (int v = 0; v < VE<T>; ++v) {
-      float xh = (q.t[v] - k.mu[v]) * k.is[v];
-      q.u[v] = k.k0[v] * q.u[v] - k.k1[v] * xh - k.k2[v];
-    }
+    for (int v = 0; v < VE<T>; ++v) q.u[v] = bn_bwd_dt(q.u[v], q.t[v], k.mu[v], k.is[v], k.k0[v], k.k1[v], k.k2[v]);
     stv<T>(dt + r * ld + c, q.u);
   }
 };
@@ -360,8 +357,7 @@ template <typename T> struct Bwd2ApplyRank1Op {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
       const float du = (q.b >> v) & 1u ? (float)(T)(q.d * k.wf[v]) : 0.f;
-      const float xh = (q.t[v] - k.mu[v]) * k.is[v];
-      o[v] = k.k0[v] * du - k.k1[v] * xh - k.k2[v];
+      o[v] = bn_bwd_dt(du, q.t[v], k.mu[v], k.is[v], k.k0[v], k.k1[v], k.k2[v]);
     }
     stv<T>(dt + r * ld + c, o);
   }
@@ -411,10 +407,7 @@ template <typename T> struct Bwd1ApplyOp {
   }
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[1][VE<T>]) const {
 #pragma unroll
-    for (int v = 0; v < VE<T>; ++v) {
-      float xh = (q.t[v] - k.mu[v]) * k.is[v];
-      q.a[v] = k.k0[v] * q.a[v] - k.k1[v] * xh - k.k2[v];
-    }
+    for (int v = 0; v < VE<T>; ++v) q.a[v] = bn_bwd_dt(q.a[v], q.t[v], k.mu[v], k.is[v], k.k0[v], k.k1[v], k.k2[v]);
     stv<T>(dt + r * ld + c, q.a);
   }
 };

@@ -52,10 +52,13 @@ struct DwCfg {
   static_assert(IPW * RPI * NW == BKW && ROWB / 32 >= 8, "dw tile geometry");
 };
 
-// the shipped tile (see gemm_dw_splits for the workgroup count).  T = 128
-// (16 splits: a 16 MB slab instead of 64 MB, -0.92 GB of HBM traffic per
-// train step) measured 102 us alone against 79 and +8 % per step; with 8
-// splits (128 workgroups) 181 us and +22 % (profiles/lab/r06_dw_slab_lab.txt)
+// the shipped tile and workgroup target (gemm_dw_splits): 256 x 256 tiles,
+// 256 workgroups = 64 splits per 512 x 512 call.  Round 6, with the BN row
+// passes folded into the dX GEMMs: 48 splits (a 48 MB slab, -0.29 GB per
+// step) ran level with 64 in the step but 92 instead of 79 us alone; 32
+// splits +0.8 %.  T = 128 (16 splits: a 16 MB slab, -0.92 GB per step)
+// measured 102 us alone against 79 and +8 % per step; with 8 splits (128
+// workgroups) 181 us and +22 % (profiles/lab/r06_dw_slab_lab.txt)
 constexpr int DW_T = 256, DW_WGS = 256;
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -185,8 +188,8 @@ bool gemm_dw_supported(int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t B
          Btot * lda * 2 < (int64_t(1) << 31) && Btot * ldb * 2 < (int64_t(1) << 31);
 }
 
-// splits: 256 workgroups per launch, one per CU (32 / 40 / 48 splits per
-// 512 x 512 call measured slower, profiles/lab/r03z_dw_splits_ab.txt)
+// splits: DW_WGS workgroups per launch, one per CU (32 / 40 / 48 splits
+// measured slower or level, profiles/lab/r03z_dw_splits_ab.txt and DW_WGS)
 int gemm_dw_splits(int64_t N, int64_t K, int64_t Btot) {
   const int64_t tiles = cdiv(N, DW_T) * cdiv(K, DW_T);
   int64_t s = std::max<int64_t>(8, (DW_WGS / tiles) / 8 * 8);

@@ -111,7 +111,13 @@ __device__ __forceinline__ void issue_tile(u32x4 xr, int64_t ldx, int K, uint32_
   }
 }
 
-template <int KTP, int EPI>
+// XBN (RESID_BN / DROP_BN at K = 512): the operand transform of NtArgs.Tx --
+// each X tile's du and t are DMA'd side by side, the workgroup turns du into
+// dt in LDS (bn_bwd_dt, per-column constants in LDS) before the MFMAs read
+// it, and slice 0's workgroups store dt for the weight gradient.  This takes
+// the BatchNorm backward's row pass (read du and t, write dt) and the GEMM's
+// re-read of dt off the backward: one kernel reads du and t once.
+template <int KTP, int EPI, bool XBN = false>
 __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   constexpr int WS_TM = ws_tm<KTP, EPI>();
   constexpr int NB = WS_NB;
@@ -123,6 +129,7 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   constexpr bool HAS_HT = EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN;
   constexpr bool HAS_BIAS = EPI <= NT_EPI_BIAS_STATS || EPI >= NT_EPI_BN_RELU;
   constexpr bool HAS_SS = EPI >= NT_EPI_BN_RELU;   // eval BN affine + ReLU
+  static_assert(!XBN || (WS_NT % C::CPR == 0 && HAS_HT), "operand transform: dX epilogues, whole rows");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, l15 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -140,11 +147,22 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
     return rsrc_words(a.X + m0 * a.ldx, rows > 0 ? rows * a.ldx * 2 : 0);
   };
   const uint32_t lbase = lds_addr(lds);
+  // XBN: the t tiles after the X tiles and the slice constants
+  constexpr int XOFF = NB * C::TILE + 4 * WS_TN * 4;
+  auto ttile_rsrc = [&](int64_t mt) {
+    const int64_t m0 = mt * WS_TM;
+    const int64_t rows = a.M - m0;
+    return rsrc_words(a.Tx + m0 * a.ldx, rows > 0 ? rows * a.ldx * 2 : 0);
+  };
 #pragma unroll
   for (int j = 0; j < NB - 1; ++j)
-    if (group + (int64_t)j * groups < a.mtiles)
+    if (group + (int64_t)j * groups < a.mtiles) {
       issue_tile<KTP, WS_TM>(tile_rsrc(group + (int64_t)j * groups), a.ldx, a.K, lbase + j * C::TILE,
                              wave, lane);
+      if constexpr (XBN)
+        issue_tile<KTP, WS_TM>(ttile_rsrc(group + (int64_t)j * groups), a.ldx, a.K,
+                               lbase + XOFF + j * C::TILE, wave, lane);
+    }
 
   // resident W: fragments (column block cb, k-step kt) of columns nw + 16cb + l15
   bf16x8 wf[2][KTP];
@@ -193,6 +211,18 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
       }
     }
     if constexpr (HEAD) wf_s[c] = n < a.Nr ? a.wf[n] : 0.f;
+  }
+  // XBN: the transform's per-column constants [mean, invstd, k0, k1, k2][K]
+  float* xc_s = reinterpret_cast<float*>(lds + XOFF + NB * C::TILE);
+  if constexpr (XBN) {
+    for (int c = tid; c < KTP * 32; c += WS_NT) {
+      const bool ok = c < a.K;
+      xc_s[c] = ok ? a.xmean[c] : 0.f;
+      xc_s[KTP * 32 + c] = ok ? a.xinvstd[c] : 0.f;
+      xc_s[2 * KTP * 32 + c] = ok ? a.xcoef[c] : 0.f;
+      xc_s[3 * KTP * 32 + c] = ok ? a.xcoef[a.K + c] : 0.f;
+      xc_s[4 * KTP * 32 + c] = ok ? a.xcoef[2 * a.K + c] : 0.f;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -372,8 +402,49 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   for (int64_t mt = group; mt < a.mtiles; mt += groups, buf = buf + 1 == NB ? 0 : buf + 1) {
     const int64_t mn = mt + (int64_t)(NB - 1) * groups;
     const int nbuf = buf + NB - 1 >= NB ? buf - 1 : buf + NB - 1;   // (buf + NB - 1) % NB
-    if (mn < a.mtiles) issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + nbuf * C::TILE, wave, lane);
+    if (mn < a.mtiles) {
+      issue_tile<KTP, WS_TM>(tile_rsrc(mn), a.ldx, a.K, lbase + nbuf * C::TILE, wave, lane);
+      if constexpr (XBN)
+        issue_tile<KTP, WS_TM>(ttile_rsrc(mn), a.ldx, a.K, lbase + XOFF + nbuf * C::TILE, wave, lane);
+    }
     const int64_t m0 = mt * WS_TM;
+    if constexpr (XBN) {
+      // du -> dt in place in this tile's LDS image (16-B chunk c of row r at
+      // position c ^ (r & 15)); a thread keeps one column group (WS_NT is a
+      // multiple of the chunks per row), so its constants are read once
+      char* xt = lds + buf * C::TILE;
+      const char* tt = lds + XOFF + buf * C::TILE;
+      const int cg = tid % C::CPR;
+      float mu[8], is[8], k0[8], k1[8], k2[8];
+#pragma unroll
+      for (int v = 0; v < 8; ++v) {
+        mu[v] = xc_s[cg * 8 + v];
+        is[v] = xc_s[KTP * 32 + cg * 8 + v];
+        k0[v] = xc_s[2 * KTP * 32 + cg * 8 + v];
+        k1[v] = xc_s[3 * KTP * 32 + cg * 8 + v];
+        k2[v] = xc_s[4 * KTP * 32 + cg * 8 + v];
+      }
+      const __amdgpu_buffer_rsrc_t dr = buf_rsrc(a.dt + m0 * a.ldx, slice == 0 ? (a.M - m0) * a.ldx * 2 : 0);
+#pragma unroll
+      for (int e = tid; e < WS_TM * C::CPR; e += WS_NT) {
+        const int r = e / C::CPR;
+        const int pos = r * C::P + ((cg ^ (r & 15)) << 4);
+        const u32x4 u = *reinterpret_cast<const u32x4*>(xt + pos);
+        const u32x4 t = *reinterpret_cast<const u32x4*>(tt + pos);
+        u32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const f2v uu = unpack2(u[j]), tv2 = unpack2(t[j]);
+          o[j] = pack2(bn_bwd_dt(uu[0], tv2[0], mu[2 * j], is[2 * j], k0[2 * j], k1[2 * j], k2[2 * j]),
+                       bn_bwd_dt(uu[1], tv2[1], mu[2 * j + 1], is[2 * j + 1], k0[2 * j + 1], k1[2 * j + 1],
+                                 k2[2 * j + 1]));
+        }
+        *reinterpret_cast<u32x4*>(xt + pos) = o;
+        // (rows past M: 0 bytes of descriptor, the store is dropped)
+        __builtin_amdgcn_raw_buffer_store_b128(o, dr, (int)((r * a.ldx + cg * 8) * 2), 0, 0);
+      }
+      __syncthreads();
+    }
     if constexpr (WS_OPS_EARLY) {
 #pragma unroll
       for (int rb = 0; rb < WS_RB; ++rb) load_ops(m0, rb, rb);
@@ -454,11 +525,14 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   }
 }
 
-template <int KTP, int EPI>
+template <int KTP, int EPI, bool XBN = false>
 dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   constexpr int WS_TM = ws_tm<KTP, EPI>();
   using C = WsCfg<KTP, WS_TM>;
-  TRY_ST(set_max_dyn_lds((const void*)gemm_ws_kernel<KTP, EPI>, C::LDS_BYTES));
+  // XBN: + the t tiles and the transform's 5 x K constants
+  constexpr size_t LDSB = C::LDS_BYTES + (XBN ? WS_NB * (size_t)C::TILE + 5 * KTP * 32 * 4 : 0);
+  static_assert(LDSB <= 160 * 1024, "LDS budget");
+  TRY_ST(set_max_dyn_lds((const void*)gemm_ws_kernel<KTP, EPI, XBN>, LDSB));
   a.nslices = (int)cdiv(a.N, WS_TN);
   // 32-bit buffer offsets: launch in M-chunks of < 2^29 bytes per operand
   const int64_t maxld = std::max<int64_t>({a.ldx, a.ldc * 2, a.R ? a.ldr : 0, a.Hb ? a.ldhb * 2 : 0,
@@ -475,9 +549,11 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
       if (a.Hb) b.Hb = a.Hb + m0 * a.ldhb;
       if (a.headp) b.headp = a.headp + m0;   // same row stride ldh
       if (a.T) b.T = a.T + m0 * a.ldt;
+      if (a.Tx) b.Tx = a.Tx + m0 * a.ldx;
+      if (a.dt) b.dt = a.dt + m0 * a.ldx;
       if (a.part) b.part = a.part + (int64_t)total * 2 * a.N;
       int np = 0;
-      dcnr_status st = launch_ws<KTP, EPI>(b, s, &np);
+      dcnr_status st = launch_ws<KTP, EPI, XBN>(b, s, &np);
       if (st != DCNR_OK) return st;
       total += np;
     }
@@ -486,12 +562,17 @@ dcnr_status launch_ws(NtArgs a, hipStream_t s, int* nparts) {
   }
   a.mtiles = cdiv(a.M, WS_TM);
   const int unit = 8 * a.nslices;
-  int grid = std::max(unit, (256 / unit) * unit);
+  // (XBN: the workgroups could leave XBN_FREE CUs to the side stream's
+  // weight gradients, which cannot share a CU with this kernel's registers
+  // and LDS: 32 / 64 / 96 / 128 measured level / level / level / +5 % per
+  // step, profiles/lab/r06_xbn_lab.txt)
+  constexpr int XBN_FREE = 0;
+  int grid = std::max(unit, ((256 - (XBN ? XBN_FREE : 0)) / unit) * unit);
   const int64_t need = a.mtiles * a.nslices;
   if (need < grid) grid = (int)(cdiv(need, unit) * unit);
   a.groups = grid / a.nslices;
   if (nparts) *nparts = a.groups;
-  hipLaunchKernelGGL((gemm_ws_kernel<KTP, EPI>), dim3(grid), dim3(WS_NT), C::LDS_BYTES, s, a);
+  hipLaunchKernelGGL((gemm_ws_kernel<KTP, EPI, XBN>), dim3(grid), dim3(WS_NT), LDSB, s, a);
   DCNR_LAUNCH_CHECK();
   return DCNR_OK;
 }
@@ -506,6 +587,9 @@ dcnr_status dispatch_ws(const NtArgs& a, hipStream_t s, int* nparts) {
 }  // namespace
 
 bool gemm_ws_supported(int64_t K, int64_t N) { return K <= 512 && K % 8 == 0 && N % 8 == 0; }
+bool gemm_ws_xbn_supported(int epi, int64_t K, int64_t N) {
+  return (epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN) && K > 256 && K <= 512 && K % 8 == 0 && N % 8 == 0;
+}
 int gemm_ws_head_parts(int64_t N) { return N % 8 == 0 && N <= 4096 ? (int)cdiv(N, WS_TN) * WS_WAVES : 0; }
 
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
@@ -523,6 +607,14 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
       (nt_epi_stats(epi) && !a.part)) {
     set_error("gemm_ws: unsupported K=%d N=%d / missing epilogue operand", a.K, a.N);
     return DCNR_UNSUPPORTED_SHAPE;
+  }
+  if (a.Tx) {   // the dX GEMMs with the BatchNorm backward's row pass folded in
+    if (!gemm_ws_xbn_supported(epi, a.K, a.N) || !a.dt || !a.xmean || !a.xinvstd || !a.xcoef) {
+      set_error("gemm_ws: unsupported operand transform (epi %d K=%d N=%d)", epi, a.K, a.N);
+      return DCNR_UNSUPPORTED_SHAPE;
+    }
+    return epi == NT_EPI_RESID_BN ? launch_ws<16, NT_EPI_RESID_BN, true>(a, s, nparts)
+                                  : launch_ws<16, NT_EPI_DROP_BN, true>(a, s, nparts);
   }
   if (gemm_wsp_supported(epi, a.K, a.N)) return gemm_wsp(epi, a, s, nparts);
   switch (epi) {

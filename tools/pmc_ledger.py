@@ -21,8 +21,8 @@ from collections import OrderedDict
 # kernel-name pattern -> the library's kernel classes (bench.py roofline_by_class)
 CLASSES = [
     ("gather_cross", r"gather_lowrank_kernel|gather_cross_v4_kernel|gather_cross_fwd"),
-    ("gemm_fwd", r"gemm_wsp_kernel|gemm_ws_kernel<16, [03](, \d)?>"),
-    ("gemm_dx", r"gemm_ws_kernel<16, [1245](, \d)?>"),
+    ("gemm_fwd", r"gemm_wsp_kernel|gemm_ws_kernel<16, [03](, (\d|true|false))?>"),
+    ("gemm_dx", r"gemm_ws_kernel<16, [1245](, (\d|true|false))?>"),
     ("gemm_dw", r"gemm_dw_kernel"),
     ("rowwise", r"rowcol_kernel"),
     ("reduce", r"reduce_small_kernel|reduce_fused_kernel|splitk_reduce_t_kernel|bce_final"),

@@ -18,11 +18,11 @@ from collections import defaultdict
 CLASSES = [
     # deep-tower forward Linears: initial layer (EPI 0) + 8 BN-input layers (EPI 3)
     # (template args <KTP, EPI, HB>: HB = 1-bit keep masks)
-    ("gemm_fwd", r"gemm_wsp_kernel|gemm_ws_kernel<16, [03](, \d)?>"),
-    ("gemm_dx_bn", r"gemm_ws_kernel<16, [45](, \d)?>"),
-    ("gemm_resid", r"gemm_ws_kernel<16, 2(, \d)?>"),
-    ("gemm_f32", r"gemm_ws_kernel<16, 1(, \d)?>"),
-    ("gemm_eval_bn", r"gemm_ws_kernel<16, [67](, \d)?>"),
+    ("gemm_fwd", r"gemm_wsp_kernel|gemm_ws_kernel<16, [03](, (\d|true|false))?>"),
+    ("gemm_dx_bn", r"gemm_ws_kernel<16, [45](, (\d|true|false))?>"),
+    ("gemm_resid", r"gemm_ws_kernel<16, 2(, (\d|true|false))?>"),
+    ("gemm_f32", r"gemm_ws_kernel<16, 1(, (\d|true|false))?>"),
+    ("gemm_eval_bn", r"gemm_ws_kernel<16, [67](, (\d|true|false))?>"),
     ("gemm_dw", r"gemm_dw_kernel"),
     ("gather_cross", r"gather_lowrank_kernel|gather_cross_fwd_kernel|gather_cross_v4_kernel<\d, \d, \d, 1>"),
     ("gather_cross_cfg2", r"gather_cross_v4_kernel<\d, \d, \d, 0>"),
