@@ -309,6 +309,7 @@ struct Layout {
   void* duk[MAX_RES]; void* dt2k[MAX_RES]; void* dak[MAX_RES]; void* dt1k[MAX_RES];
   float* dx0;                 // deep part of dL/dx0, [B][Dq] (Dq = Dp rounded up to 32)
   float* slab; int64_t slab_elems;
+  float* slab2;   // the side stream's weight gradients alternate slabs (DwPipe)
   float* sc;                 // forward -> backward cross scalars [B][2L+1]
   float* xcoef; float* xalpha;  // [B][L+1] each (cross_bwd.hip)
   void* cscratch; size_t cscratch_bytes;
@@ -429,6 +430,7 @@ Layout make_layout(const Dims& d, int64_t B, int mode, void* ws, uint32_t flags 
                                       (int64_t)gemm_dw_splits(d.Hp, d.Hp, B) * d.Hp * d.Hp,
                                       (int64_t)gemm_dw_splits(d.Hp, d.Dp, B) * d.Hp * d.Dp});
     L.slab = (float*)b.take((size_t)L.slab_elems * 4);
+    L.slab2 = (float*)b.take((size_t)L.slab_elems * 4);
     L.sc = (float*)b.take((size_t)B * (2 * d.L + 1) * 4);
     L.xcoef = (float*)b.take((size_t)B * (d.L + 1) * 4);
     L.xalpha = (float*)b.take((size_t)B * (d.L + 1) * 4);
@@ -721,6 +723,12 @@ dcnr_status wgrad_bf16(const void* dY, int64_t ldy, int N, const void* X, int64_
 // call n-1's GEMM. The reduces share one slab because they are serialised
 // on the side stream. join() orders the main stream after all of it. Same kernels, same order per
 // output: the gradients are unchanged.
+// Round 6: each call's split-K combine runs in the NEXT call's gemm_dw
+// launch (its tail, over the workgroups already resident) instead of as a
+// launch of its own, which beside the dX GEMMs waited for CUs (150-240 us
+// for a 12 us kernel): the calls alternate slabs (L.slab, L.slab2), and the
+// last call's combine is launched by join().  Same tiles, same order: the
+// gradients are unchanged.
 struct DwPipe {
   static constexpr int RING = 4;
   hipStream_t side = nullptr, main = nullptr;
@@ -728,6 +736,17 @@ struct DwPipe {
   hipEvent_t dw_ev[RING] = {};
   int calls = 0, lag = 1;
   bool pending = false;   // side work enqueued since the last join
+  struct Combine { const float* slab; int S; int64_t stride; int ld, Nr, Kr; float* out; int acc; };
+  Combine pend{};          // the last call's combine, not yet enqueued (slab != null)
+  dcnr_status flush() {
+    if (!pend.slab) return DCNR_OK;
+    const Combine c = pend;
+    pend = Combine{};
+    hipStream_t s = side;   // TRYB launches and times on the side stream
+    TRYB(DCNR_K_REDUCE, 4.0 * c.S * c.stride + 4.0 * c.Nr * c.Kr * (c.acc ? 2 : 1),
+         splitk_reduce_t(c.slab, c.S, c.stride, c.ld, c.Nr, c.Kr, c.out, c.acc, s));
+    return DCNR_OK;
+  }
   dcnr_status init(hipStream_t side_stream, int lag_calls) {
     side = side_stream;
     lag = lag_calls;
@@ -758,26 +777,40 @@ struct DwPipe {
       set_error("wgrad: slab too small");
       return DCNR_WORKSPACE_TOO_SMALL;
     }
+    float* slab = (call & 1) ? L.slab2 : L.slab;
     DwArgs a;
     memset(&a, 0, sizeof(a));
     a.A = (const bf16*)dY; a.lda = ldy; a.B = (const bf16*)X; a.ldb = ldx;
-    a.C = L.slab; a.ldc = N; a.slab_stride = (int64_t)N * Kc;   // transposed slab [Kc][N]
+    a.C = slab; a.ldc = N; a.slab_stride = (int64_t)N * Kc;   // transposed slab [Kc][N]
     a.Btot = B; a.k_per_split = rup(cdiv(B, S), 64);
     a.N = N; a.K = Kc; a.splits = S;
-    TRYB(DCNR_K_GEMM_DW, 2.0 * B * (N + Kc) + 4.0 * Nr * Kr * (accumulate ? 2 : 1), gemm_dw(a, s));
+    double rbytes = 0;
+    if (pend.slab) {   // the previous call's combine, in this launch's tail
+      a.rslab = pend.slab; a.rsplits = pend.S; a.rstride = pend.stride; a.rld = pend.ld;
+      a.rN = pend.Nr; a.rK = pend.Kr; a.rout = pend.out;
+      const int vec = pend.Kr % 4 == 0 && (uintptr_t)pend.out % 16 == 0;
+      a.racc = (pend.acc ? 1 : 0) | (vec << 1);
+      rbytes = 4.0 * pend.S * pend.stride + 4.0 * pend.Nr * pend.Kr * (pend.acc ? 2 : 1);
+      if (pend.ld % 4 || pend.stride % 4 || (uintptr_t)pend.slab % 16) {
+        set_error("wgrad: slab not 16-B aligned");
+        return DCNR_UNSUPPORTED_SHAPE;
+      }
+    }
+    TRYB(DCNR_K_GEMM_DW, 2.0 * B * (N + Kc) + 4.0 * Nr * Kr * (accumulate ? 2 : 1) + rbytes, gemm_dw(a, s));
     DCNR_HIP(hipEventRecord(dw_ev[call % RING], s));
-    TRYB(DCNR_K_REDUCE, 4.0 * S * N * Kc + 4.0 * Nr * Kr * (accumulate ? 2 : 1),
-         splitk_reduce_t(L.slab, S, (int64_t)N * Kc, N, Nr, Kr, out, accumulate, s));
+    pend = Combine{slab, S, (int64_t)N * Kc, N, Nr, Kr, out, accumulate};
     return DCNR_OK;
   }
   dcnr_status join(hipStream_t main_s) {
     if (!pending) return DCNR_OK;
+    TRY(flush());
     DCNR_HIP(hipEventRecord(done_ev, side));
     DCNR_HIP(hipStreamWaitEvent(main_s, done_ev, 0));
     pending = false;
     return DCNR_OK;
   }
   ~DwPipe() {
+    if (pend.slab && side) (void)flush();   // error path: the last combine too
     if (pending && main) {   // error path: order the side work before the caller's stream
       (void)hipEventRecord(done_ev, side);
       (void)hipStreamWaitEvent(main, done_ev, 0);

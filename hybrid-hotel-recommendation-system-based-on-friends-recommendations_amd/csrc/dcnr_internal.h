@@ -156,6 +156,58 @@ __device__ __forceinline__ float bn_bwd_dt(float u, float t, float mu, float is,
   return fmaf(-k1, xh, k0 * u) - k2;
 }
 
+// The weight gradient's split-K combine, one 64 k x 16 n tile of
+// out[n][k] (+)= sum_z slab[z][k][n] by 256 threads (splitk_reduce_t's
+// kernel, and gemm_dw's tail when it combines the previous call's slab):
+// sum in fixed z order into LDS t, barrier, transposed store of rows of out.
+constexpr int RT_K = 64, RT_N = 16;
+__device__ __forceinline__ void splitk_t_sum(const float* slab, int splits, int64_t stride, int ld, int N,
+                                             int K, int bx, int by, int idx, float (*t)[RT_N + 1]) {
+  const int k0 = bx * RT_K, n0 = by * RT_N;
+  const int kk = idx >> 2, nq = idx & 3;
+  const int k = k0 + kk, n = n0 + 4 * nq;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (k < K && n < N) {
+    const float* base = slab + (int64_t)k * ld + n;
+    int z = 0;
+    for (; z + 16 <= splits; z += 16) {
+      float4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const float4*>(base + (int64_t)(z + u) * stride);
+#pragma unroll
+      for (int u = 0; u < 16; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
+    }
+    for (; z < splits; ++z) {
+      const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)z * stride);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  t[kk][4 * nq] = s.x; t[kk][4 * nq + 1] = s.y; t[kk][4 * nq + 2] = s.z; t[kk][4 * nq + 3] = s.w;
+}
+__device__ __forceinline__ void splitk_t_store(int N, int K, float* out, int accumulate, int vec_out, int bx,
+                                               int by, int idx, const float (*t)[RT_N + 1]) {
+  const int k0 = bx * RT_K, n0 = by * RT_N;
+  const int nn = idx >> 4, kq = idx & 15;
+  const int n = n0 + nn, k = k0 + 4 * kq;
+  if (n >= N) return;
+  float v[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) v[j] = t[4 * kq + j][nn];
+  float* o = out + (int64_t)n * K + k;
+  if (vec_out && k + 3 < K) {
+    float4 r = make_float4(v[0], v[1], v[2], v[3]);
+    if (accumulate) {
+      const float4 a = *reinterpret_cast<const float4*>(o);
+      r.x += a.x; r.y += a.y; r.z += a.z; r.w += a.w;
+    }
+    *reinterpret_cast<float4*>(o) = r;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (k + j < K) o[j] = accumulate ? o[j] + v[j] : v[j];
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -413,6 +465,10 @@ struct DwArgs {
   int64_t Btot, k_per_split;
   int N, K, splits;
   int tiles_n, tiles_k;            // filled by gemm_dw
+  // the PREVIOUS call's split-K combine, in this launch's tail (rslab !=
+  // null): out[rN][rK] (+)= sum of rsplits slabs of another buffer, the
+  // splitk_reduce_t tiles dealt over the workgroups
+  const float* rslab; int rsplits; int64_t rstride; int rld, rN, rK; float* rout; int racc;
 };
 bool gemm_dw_supported(int64_t N, int64_t K, int64_t lda, int64_t ldb, int64_t Btot);
 // split count for ~wg_target workgroups (0: the default, one per CU)

@@ -991,7 +991,6 @@ namespace {
 // segment, 16 slab loads in flight per lane), sums in fixed z order (the same
 // bits as summing the untransposed slabs), transposes through LDS, writes
 // rows of out along k (16-B stores when out's rows allow).
-constexpr int RT_K = 64, RT_N = 16;
 // (Several thread groups per output tile, each summing a contiguous share of
 // the splits, measured 12-13 us alone either way per 512 x 512 call and
 // 40-54 us under the concurrent dX chain; one group kept -- the summation
@@ -1000,50 +999,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_t_kernel(const float* slab,
                                                               int64_t stride, int ld, int N, int K,
                                                               float* out, int accumulate, int vec_out) {
   __shared__ float t[RT_K][RT_N + 1];
-  const int k0 = blockIdx.x * RT_K, n0 = blockIdx.y * RT_N;
-  const int idx = threadIdx.x;
-  {
-    const int kk = idx >> 2, nq = idx & 3;
-    const int k = k0 + kk, n = n0 + 4 * nq;
-    const int z0 = 0, z1 = splits;
-    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (k < K && n < N) {
-      const float* base = slab + (int64_t)k * ld + n;
-      int z = z0;
-      for (; z + 16 <= z1; z += 16) {
-        float4 v[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const float4*>(base + (int64_t)(z + u) * stride);
-#pragma unroll
-        for (int u = 0; u < 16; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
-      }
-      for (; z < z1; ++z) {
-        const float4 v = *reinterpret_cast<const float4*>(base + (int64_t)z * stride);
-        s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
-      }
-    }
-    t[kk][4 * nq] = s.x; t[kk][4 * nq + 1] = s.y; t[kk][4 * nq + 2] = s.z; t[kk][4 * nq + 3] = s.w;
-  }
+  splitk_t_sum(slab, splits, stride, ld, N, K, blockIdx.x, blockIdx.y, threadIdx.x, t);
   __syncthreads();
-  const int nn = idx >> 4, kq = idx & 15;
-  const int n = n0 + nn, k = k0 + 4 * kq;
-  if (n >= N) return;
-  float v[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) v[j] = t[4 * kq + j][nn];
-  float* o = out + (int64_t)n * K + k;
-  if (vec_out && k + 3 < K) {
-    float4 r = make_float4(v[0], v[1], v[2], v[3]);
-    if (accumulate) {
-      const float4 a = *reinterpret_cast<const float4*>(o);
-      r.x += a.x; r.y += a.y; r.z += a.z; r.w += a.w;
-    }
-    *reinterpret_cast<float4*>(o) = r;
-  } else {
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-      if (k + j < K) o[j] = accumulate ? o[j] + v[j] : v[j];
-  }
+  splitk_t_store(N, K, out, accumulate, vec_out, blockIdx.x, blockIdx.y, threadIdx.x, t);
 }
 }  // namespace
 

@@ -179,6 +179,26 @@ __global__ __launch_bounds__(DwCfg<T>::NW * 64, 1) void gemm_dw_kernel(DwArgs g)
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), cr,
                                                ok ? (k * g.ldc + n) * 4 : OOR, 0, 0);
     }
+
+  // the previous call's split-K combine (its slab is complete: that launch
+  // ended before this one began on the stream), splitk_reduce_t's tiles
+  // dealt over the workgroups, two at a time (256 threads each): a separate
+  // launch of it on the side stream waited for CUs beside the dX GEMMs
+  if (g.rslab) {
+    constexpr int NT = C::NW * 64, PER = NT / 256;
+    static_assert(NT % 256 == 0, "tail: whole 256-thread tile groups");
+    __syncthreads();   // every wave is past its last read of the LDS ring
+    float(*tt)[RT_N + 1] = reinterpret_cast<float(*)[RT_N + 1]>(lds) + (threadIdx.x / 256) * RT_K;
+    const int nbx = (g.rK + RT_K - 1) / RT_K, nby = (g.rN + RT_N - 1) / RT_N;
+    const int tiles_r = nbx * nby, h = threadIdx.x / 256, idx = threadIdx.x % 256;
+    for (int b0 = blockIdx.x * PER; b0 < tiles_r; b0 += gridDim.x * PER) {
+      const int b = b0 + h;
+      if (b < tiles_r) splitk_t_sum(g.rslab, g.rsplits, g.rstride, g.rld, g.rN, g.rK, b % nbx, b / nbx, idx, tt);
+      __syncthreads();
+      if (b < tiles_r) splitk_t_store(g.rN, g.rK, g.rout, g.racc & 1, g.racc >> 1, b % nbx, b / nbx, idx, tt);
+      __syncthreads();
+    }
+  }
 }
 
 }  // namespace
