@@ -185,17 +185,20 @@ __global__ __launch_bounds__(DwCfg<T>::NW * 64, 1) void gemm_dw_kernel(DwArgs g)
   // dealt over the workgroups, two at a time (256 threads each): a separate
   // launch of it on the side stream waited for CUs beside the dX GEMMs
   if (g.rslab) {
-    constexpr int NT = C::NW * 64, PER = NT / 256;
-    static_assert(NT % 256 == 0, "tail: whole 256-thread tile groups");
+    constexpr int NT = C::NW * 64;
+    static_assert(NT == 512, "tail: two 256-thread tile groups");
     __syncthreads();   // every wave is past its last read of the LDS ring
     float(*tt)[RT_N + 1] = reinterpret_cast<float(*)[RT_N + 1]>(lds) + (threadIdx.x / 256) * RT_K;
+    // the two halves take tiles (bx, 2j) and (bx, 2j+1): the two 64-B halves
+    // of each 128-B slab line, read together (dealt singly, each line came
+    // from HBM twice: 134 instead of 67 MB per call by PMC)
     const int nbx = (g.rK + RT_K - 1) / RT_K, nby = (g.rN + RT_N - 1) / RT_N;
-    const int tiles_r = nbx * nby, h = threadIdx.x / 256, idx = threadIdx.x % 256;
-    for (int b0 = blockIdx.x * PER; b0 < tiles_r; b0 += gridDim.x * PER) {
-      const int b = b0 + h;
-      if (b < tiles_r) splitk_t_sum(g.rslab, g.rsplits, g.rstride, g.rld, g.rN, g.rK, b % nbx, b / nbx, idx, tt);
+    const int npairs = nbx * ((nby + 1) / 2), h = threadIdx.x / 256, idx = threadIdx.x % 256;
+    for (int pr = blockIdx.x; pr < npairs; pr += gridDim.x) {
+      const int bx = pr % nbx, by = 2 * (pr / nbx) + h;
+      if (by < nby) splitk_t_sum(g.rslab, g.rsplits, g.rstride, g.rld, g.rN, g.rK, bx, by, idx, tt);
       __syncthreads();
-      if (b < tiles_r) splitk_t_store(g.rN, g.rK, g.rout, g.racc & 1, g.racc >> 1, b % nbx, b / nbx, idx, tt);
+      if (by < nby) splitk_t_store(g.rN, g.rK, g.rout, g.racc & 1, g.racc >> 1, bx, by, idx, tt);
       __syncthreads();
     }
   }
