@@ -161,6 +161,7 @@ __device__ __forceinline__ float bn_bwd_dt(float u, float t, float mu, float is,
 // kernel, and gemm_dw's tail when it combines the previous call's slab):
 // sum in fixed z order into LDS t, barrier, transposed store of rows of out.
 constexpr int RT_K = 64, RT_N = 16;
+template <bool NT = false>
 __device__ __forceinline__ void splitk_t_sum(const float* slab, int splits, int64_t stride, int ld, int N,
                                              int K, int bx, int by, int idx, float (*t)[RT_N + 1]) {
   const int k0 = bx * RT_K, n0 = by * RT_N;
@@ -173,7 +174,16 @@ __device__ __forceinline__ void splitk_t_sum(const float* slab, int splits, int6
     for (; z + 16 <= splits; z += 16) {
       float4 v[16];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = *reinterpret_cast<const float4*>(base + (int64_t)(z + u) * stride);
+      for (int u = 0; u < 16; ++u) {
+        const float4* pp = reinterpret_cast<const float4*>(base + (int64_t)(z + u) * stride);
+        if constexpr (NT) {
+          typedef float f4v __attribute__((ext_vector_type(4)));
+          const f4v w = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(pp));
+          v[u] = make_float4(w.x, w.y, w.z, w.w);
+        } else {
+          v[u] = *pp;
+        }
+      }
 #pragma unroll
       for (int u = 0; u < 16; ++u) { s.x += v[u].x; s.y += v[u].y; s.z += v[u].z; s.w += v[u].w; }
     }

@@ -60,6 +60,9 @@ struct DwCfg {
 // measured 102 us alone against 79 and +8 % per step; with 8 splits (128
 // workgroups) 181 us and +22 % (profiles/lab/r06_dw_slab_lab.txt)
 constexpr int DW_T = 256, DW_WGS = 256;
+// the tail combine's slab loads: default policy (nontemporal measured in
+// profiles/lab/r06_xbn_lab.txt)
+constexpr bool DW_TAIL_NT = false;
 
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -196,7 +199,7 @@ __global__ __launch_bounds__(DwCfg<T>::NW * 64, 1) void gemm_dw_kernel(DwArgs g)
     const int npairs = nbx * ((nby + 1) / 2), h = threadIdx.x / 256, idx = threadIdx.x % 256;
     for (int pr = blockIdx.x; pr < npairs; pr += gridDim.x) {
       const int bx = pr % nbx, by = 2 * (pr / nbx) + h;
-      if (by < nby) splitk_t_sum(g.rslab, g.rsplits, g.rstride, g.rld, g.rN, g.rK, bx, by, idx, tt);
+      if (by < nby) splitk_t_sum<DW_TAIL_NT>(g.rslab, g.rsplits, g.rstride, g.rld, g.rN, g.rK, bx, by, idx, tt);
       __syncthreads();
       if (by < nby) splitk_t_store(g.rN, g.rK, g.rout, g.racc & 1, g.racc >> 1, bx, by, idx, tt);
       __syncthreads();
