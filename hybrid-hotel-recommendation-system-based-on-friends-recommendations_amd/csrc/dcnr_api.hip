@@ -1386,7 +1386,8 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     TRY(bn_bwd_reduce(desc, d, L, nc, 2, B, Bk.g1, bn1.invstd, Gk.g1, Gk.be1, nullptr, Gk.b1,
                         accumulate, s));
     // the BN1 backward's row pass folded into the RESID_BN dX GEMM likewise
-    const bool xbn1 = fuse && j > 0 && xbn_ok;
+    // (block 0: into the RESID GEMM that makes G)
+    const bool xbn1 = fuse && xbn_ok;
     if (!xbn1) {
       TRYB(DCNR_K_ROWWISE, 3 * act_b(d, B), bwd_bn1_apply2(d.prec, da, L.t1[j], bn1.mean, bn1.invstd, L.coef, B, Hp, Hp, dt1,
                          L.part, &nc, s));
@@ -1404,6 +1405,20 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
                         L.t2[j - 1], bp, B, &nc_du, s, xbn1 ? &xo : nullptr));
       if (xbn1) TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe));
       Gin = L.duk[j - 1];
+    } else if (xbn1) {   // G = dt1 W1 + du, dt1 made from da and t1 in the GEMM
+      NtArgs a;
+      memset(&a, 0, sizeof(a));
+      a.Tx = (const bf16*)L.t1[j];
+      a.xmean = bn1.mean; a.xinvstd = bn1.invstd; a.xcoef = L.coef;
+      a.dt = (bf16*)dt1;
+      a.X = (const bf16*)da; a.ldx = Hp; a.M = B; a.K = Hp;
+      a.W = (const bf16*)L.W1t[j]; a.ldw = Hp; a.N = Hp;
+      a.C = L.G; a.ldc = Hp;
+      a.R = du; a.ldr = Hp;
+      TRYB(DCNR_K_GEMM_DX, 5 * act_b(d, B) + w_b(d, d.Hp), gemm_ws(NT_EPI_RESID, a, s));
+      TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe));
+      Gin = L.G;
+      nc_du = 0;
     } else {
       GemmArgs g;
       memset(&g, 0, sizeof(g));

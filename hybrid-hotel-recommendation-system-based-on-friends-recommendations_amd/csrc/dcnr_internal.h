@@ -6,6 +6,9 @@
 #include <stdint.h>
 #include <stddef.h>
 
+#include <algorithm>
+#include <cmath>
+
 #include "../../include/dcnr.h"
 
 namespace dcnr {
@@ -289,6 +292,33 @@ __device__ __forceinline__ uint32_t dropout_bits(uint64_t seed, int layer, int64
                                                  int colpair) {
   uint32_t x = fmix32((uint32_t)row * 0x9E3779B1u ^ (uint32_t)seed ^ ((uint32_t)layer * 0x7FEB352Du));
   return fmix32((x + (uint32_t)colpair * 0x846CA68Bu) ^ (uint32_t)(seed >> 32));
+}
+
+// y[v] *= keep(r, c+v) ? inv_keep : 0 for V consecutive columns (c even)
+template <int V>
+__device__ __forceinline__ void apply_dropout(uint64_t seed, int layer, int64_t r, int c,
+                                              uint32_t thresh16, float inv_keep, float (&y)[V]) {
+#pragma unroll
+  for (int v = 0; v < V; v += 2) {
+    const uint32_t bits = dropout_bits(seed, layer, r, (c + v) >> 1);
+    y[v] = (bits & 0xFFFFu) >= thresh16 ? y[v] * inv_keep : 0.f;
+    y[v + 1] = (bits >> 16) >= thresh16 ? y[v + 1] * inv_keep : 0.f;
+  }
+}
+
+// the 16-bit keep threshold of dropout probability p (see dropout_bits)
+inline uint32_t drop_thresh16(float p) {
+  return (uint32_t)std::min(65536.0, std::floor((double)p * 65536.0 + 0.5));
+}
+
+// train-mode BatchNorm apply + ReLU (train.py:117-122) from the batch affine
+// sc = gamma invstd, sh = beta - mean sc: relu(t sc + sh) and, for the
+// residual block's output, relu(t sc + sh + x) -- one explicit fma order for
+// every pass that makes or rebuilds them (BnReluDropOp, BnAddRelu(Head)Op,
+// the backward's rebuild of h_R)
+__device__ __forceinline__ float bn_fwd_relu(float t, float sc, float sh) { return relu_f(fmaf(t, sc, sh)); }
+__device__ __forceinline__ float bn_fwd_add_relu(float t, float sc, float sh, float x) {
+  return relu_f(fmaf(t, sc, sh) + x);
 }
 
 // ------------------------------------------------------------------ GEMM

@@ -149,18 +149,6 @@ dcnr_status run_rowcol(const Op& op, int64_t B, int N, float* part, int* nchunks
 
 struct NoCst {};
 
-// y[v] *= keep(r, c+v) ? inv_keep : 0 for V consecutive columns (c even)
-template <int V>
-__device__ __forceinline__ void apply_dropout(uint64_t seed, int layer, int64_t r, int c,
-                                              uint32_t thresh16, float inv_keep, float (&y)[V]) {
-#pragma unroll
-  for (int v = 0; v < V; v += 2) {
-    const uint32_t bits = dropout_bits(seed, layer, r, (c + v) >> 1);
-    y[v] = (bits & 0xFFFFu) >= thresh16 ? y[v] * inv_keep : 0.f;
-    y[v + 1] = (bits >> 16) >= thresh16 ? y[v + 1] * inv_keep : 0.f;
-  }
-}
-
 // ---------------------------------------------------------------- ops
 // sums of (t-K) and (t-K)^2 with K = t[0] (the batch's first row)
 template <typename T> struct StatsOp {
@@ -217,7 +205,7 @@ template <typename T> struct BnReluDropOp {  // a = dropout(relu(t*sc+sh))
   __device__ void load(int64_t r, int c, Reg& q) const { ldv<T>(t + r * ld + c, q.x); }
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&)[1][VE<T>]) const {
 #pragma unroll
-    for (int v = 0; v < VE<T>; ++v) q.x[v] = relu_f(q.x[v] * k.sc[v] + k.sh[v]);
+    for (int v = 0; v < VE<T>; ++v) q.x[v] = bn_fwd_relu(q.x[v], k.sc[v], k.sh[v]);
     if (drop) apply_dropout<VE<T>>(seed, layer, r, c, thresh, inv_keep, q.x);
     stv<T, true>(a + r * ld + c, q.x);
     if (bits) store_pos_bits<T>(bits, r, ld >> 3, c, q.x);
@@ -236,7 +224,7 @@ template <typename T> struct BnAddReluOp {   // out = relu(t*sc+sh + x)
   }
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&)[1][VE<T>]) const {
 #pragma unroll
-    for (int v = 0; v < VE<T>; ++v) q.a[v] = relu_f(q.a[v] * k.sc[v] + k.sh[v] + q.b[v]);
+    for (int v = 0; v < VE<T>; ++v) q.a[v] = bn_fwd_add_relu(q.a[v], k.sc[v], k.sh[v], q.b[v]);
     stv<T, true>(out + r * ld + c, q.a);
     if (bits) store_pos_bits<T>(bits, r, ld >> 3, c, q.a);
   }
@@ -264,7 +252,7 @@ template <typename T> struct BnAddReluHeadOp {
     float d = 0.f;
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      q.a[v] = relu_f(q.a[v] * k.sc[v] + k.sh[v] + q.b[v]);
+      q.a[v] = bn_fwd_add_relu(q.a[v], k.sc[v], k.sh[v], q.b[v]);
       d += (float)(T)q.a[v] * k.wf[v];   // the stored (rounded) activation, as row_dot reads it
     }
     if (out) stv<T, true>(out + r * ld + c, q.a);   // (train: null, the backward rebuilds it)
@@ -300,7 +288,7 @@ template <typename T, bool HAS_G, bool REBUILD = false> struct Bwd2StatsOp {
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[3][VE<T>]) const {
     if constexpr (REBUILD) {
 #pragma unroll
-      for (int v = 0; v < VE<T>; ++v) q.o[v] = (float)(T)relu_f(q.t[v] * k.sc[v] + k.sh[v] + q.o[v]);
+      for (int v = 0; v < VE<T>; ++v) q.o[v] = (float)(T)bn_fwd_add_relu(q.t[v], k.sc[v], k.sh[v], q.o[v]);
     }
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
@@ -378,7 +366,7 @@ template <typename T> struct Bwd1StatsOp {
   __device__ void apply(int64_t r, int c, const Cst& k, Reg& q, float (&acc)[2][VE<T>]) const {
 #pragma unroll
     for (int v = 0; v < VE<T>; ++v) {
-      float pre = q.t[v] * k.sc[v] + k.sh[v];
+      float pre = fmaf(q.t[v], k.sc[v], k.sh[v]);
       q.a[v] = pre > 0.f ? q.a[v] : 0.f;
     }
     if (drop) apply_dropout<VE<T>>(seed, layer, r, c, thresh, inv_keep, q.a);
@@ -821,16 +809,13 @@ dcnr_status bn_bwd_coef(const double* sums, int N, int Nr, const float* gamma, c
   return DCNR_OK;
 }
 
-static uint32_t drop_thresh(float p) {   // 16-bit threshold (see dropout_bits)
-  return (uint32_t)std::min(65536.0, std::floor((double)p * 65536.0 + 0.5));
-}
 
 template <typename T>
 static dcnr_status bn_relu_drop_impl(const void* t, void* a, int64_t B, int N, int ld,
                                      const float* sc, const float* sh, float p, uint64_t seed,
                                      int layer, hipStream_t s, uint8_t* bits) {
   BnReluDropOp<T> op{(const T*)t, (T*)a, ld, sc, sh, p > 0.f ? 1.f / (1.f - p) : 1.f,
-                     drop_thresh(p), seed, layer, p > 0.f, bits};
+                     drop_thresh16(p), seed, layer, p > 0.f, bits};
   return run_rowcol<T, 0>(op, B, N, nullptr, nullptr, s);
 }
 dcnr_status bn_relu_drop(int precision, const void* t, void* a, int64_t B, int N, int ld,
@@ -935,7 +920,7 @@ static dcnr_status bwd1_stats_impl(void* da, const void* t, const float* sc, con
                                    int ld, float p, uint64_t seed, int layer, float* part, int* nc,
                                    hipStream_t s) {
   Bwd1StatsOp<T> op{(T*)da, (const T*)t, sc, sh, mean, invstd, ld,
-                    p > 0.f ? 1.f / (1.f - p) : 1.f, drop_thresh(p), seed, layer, p > 0.f};
+                    p > 0.f ? 1.f / (1.f - p) : 1.f, drop_thresh16(p), seed, layer, p > 0.f};
   return run_rowcol<T, 2>(op, B, N, part, nc, s);
 }
 dcnr_status bwd_bn1_stats(int precision, void* da_dr, const void* t, const float* scale,

@@ -129,7 +129,8 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   constexpr bool HAS_HT = EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN;
   constexpr bool HAS_BIAS = EPI <= NT_EPI_BIAS_STATS || EPI >= NT_EPI_BN_RELU;
   constexpr bool HAS_SS = EPI >= NT_EPI_BN_RELU;   // eval BN affine + ReLU
-  static_assert(!XBN || (WS_NT % C::CPR == 0 && HAS_HT), "operand transform: dX epilogues, whole rows");
+  static_assert(!XBN || (WS_NT % C::CPR == 0 && (HAS_HT || EPI == NT_EPI_RESID)),
+                "operand transform: dX epilogues, whole rows");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, l15 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -440,8 +441,11 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
                                  k2[2 * j + 1]));
         }
         *reinterpret_cast<u32x4*>(xt + pos) = o;
-        // (rows past M: 0 bytes of descriptor, the store is dropped)
-        __builtin_amdgcn_raw_buffer_store_b128(o, dr, (int)((r * a.ldx + cg * 8) * 2), 0, 0);
+        // (rows past M: 0 bytes of descriptor, the store is dropped; chunks
+        // past K are not columns of the row: K < 512 would write them into
+        // the next row)
+        __builtin_amdgcn_raw_buffer_store_b128(o, dr, cg * 8 < a.K ? (int)((r * a.ldx + cg * 8) * 2) : OOR, 0,
+                                               0);
       }
       __syncthreads();
     }
@@ -588,7 +592,8 @@ dcnr_status dispatch_ws(const NtArgs& a, hipStream_t s, int* nparts) {
 
 bool gemm_ws_supported(int64_t K, int64_t N) { return K <= 512 && K % 8 == 0 && N % 8 == 0; }
 bool gemm_ws_xbn_supported(int epi, int64_t K, int64_t N) {
-  return (epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN) && K > 256 && K <= 512 && K % 8 == 0 && N % 8 == 0;
+  return (epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN || epi == NT_EPI_RESID) && K > 256 && K <= 512 &&
+         K % 8 == 0 && N % 8 == 0;
 }
 int gemm_ws_head_parts(int64_t N) { return N % 8 == 0 && N <= 4096 ? (int)cdiv(N, WS_TN) * WS_WAVES : 0; }
 
@@ -613,6 +618,7 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
       set_error("gemm_ws: unsupported operand transform (epi %d K=%d N=%d)", epi, a.K, a.N);
       return DCNR_UNSUPPORTED_SHAPE;
     }
+    if (epi == NT_EPI_RESID) return launch_ws<16, NT_EPI_RESID, true>(a, s, nparts);
     return epi == NT_EPI_RESID_BN ? launch_ws<16, NT_EPI_RESID_BN, true>(a, s, nparts)
                                   : launch_ws<16, NT_EPI_DROP_BN, true>(a, s, nparts);
   }

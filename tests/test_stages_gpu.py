@@ -48,6 +48,10 @@ REL = 2e-4
 
 
 def _cfg(full):
+    if full == "h384":   # K = 384 < 512: the fused BN-backward operand's partial last chunks
+        return dict(n_users=50_000, n_items=5_000, cat_dims={f"c{k}": 100 for k in range(4)},
+                    n_num=8, params=dict(emb_dim=32, hidden_dim=384, n_cross_layers=2,
+                                         n_res_blocks=3, dropout=0.6)), 8192
     if full:
         return dict(n_users=1_000_000, n_items=100_000, cat_dims={f"c{k}": 1000 for k in range(12)},
                     n_num=8, params=dict(emb_dim=32, hidden_dim=512, n_cross_layers=3,
@@ -96,7 +100,7 @@ def unpack_bits(b, B, Hp):
     return ((b.view(B, Hp // 8)[:, :, None] >> sh) & 1).reshape(B, Hp).bool()
 
 
-@pytest.mark.parametrize("full", [False, True], ids=["cfg3r_B1024", "cfg2_B131072"])
+@pytest.mark.parametrize("full", [False, True, "h384"], ids=["cfg3r_B1024", "cfg2_B131072", "h384_B8192"])
 def test_bf16_step_stage_by_stage(dev, full):
     import dcnr
     from dcnr import _lib
