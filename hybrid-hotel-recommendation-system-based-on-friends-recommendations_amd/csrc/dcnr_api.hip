@@ -1430,19 +1430,17 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       nc_du = 0;
     }
   }
-  // ---- initial layer
-  // its bias gradient (column sums of G) also goes under the dx0 GEMM and
-  // the embedding sums when the pipe runs (L.part and the reduction counters
-  // are not used by the main stream after the blocks)
+  // ---- initial layer: the weight gradient on the side stream (after block
+  // 0's), the bias gradient (column sums of G) here on the main stream, ahead
+  // of the dx0 GEMM.  The side stream's queue sets the backward's tail: with
+  // the column sums on it too, the optimizer waited 135 us for it while the
+  // main stream was done (profiles/r06fin_step_timeline.txt)
+  TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s, pipe));
   {
-    hipStream_t main_s = s;
-    if (pipe) TRY(pipe->enter(main_s));
-    hipStream_t s = pipe ? pipe->side : main_s;
     int nc = 0;
     TRYB(DCNR_K_ROWWISE, act_b(d, B), col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
     TRY(bias_reduce(d, L, nc, Gr.b0, accumulate, s));
   }
-  TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s, pipe));
   TRY(sj.join(s));   // the side stream's cross gradients, coefficients and sorted ids
   // and the weight gradients; without a hook nothing reads them before the
   // optimizer, so they join at the end (under the dx0 GEMM and embedding sums)
