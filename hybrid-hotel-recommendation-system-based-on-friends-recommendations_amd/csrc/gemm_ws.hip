@@ -35,7 +35,7 @@ namespace dcnr {
 namespace {
 
 // Per-epilogue tile rows and operand-load placement (measured with
-// tools/ws_lab.hip in rounds 2-3, M = 131072, K = N = 512): 64-row tiles where
+// tools/ws_lab.hip in rounds 2-3, removed since in commit 77025d0, M = 131072, K = N = 512): 64-row tiles where
 // registers allow; the epilogues with operands use 32-row tiles and issue
 // every operand load before the MFMAs ("early": RESID 90.5 vs 96.4 us one row
 // block ahead, DROP_BN 104.7 vs 111.9 us at 64 rows); eval BN_RELU at 32 rows
