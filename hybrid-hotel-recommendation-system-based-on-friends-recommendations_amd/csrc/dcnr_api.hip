@@ -932,12 +932,12 @@ dcnr_status bn_bwd_reduce(const dcnr_model_desc* desc, const Dims& d, const Layo
   return DCNR_OK;
 }
 
-// Bias gradient: part [nc][1][Hp] -> grad[H] (never needs the hook).
+// Bias gradient: part [nc][NK][Hp], component 0 -> grad[H] (never needs the hook).
 dcnr_status bias_reduce(const Dims& d, const Layout& L, int nc, float* grad, int accumulate,
-                        hipStream_t s) {
+                        hipStream_t s, int NK = 1) {
   RedFinal rf = red_init(L, RED_BIAS, 0.0, accumulate);
   rf.grad = grad;
-  TRYP(DCNR_K_REDUCE, reduce_fused(DCNR_PREC_FP32, L.part, nc, 1, d.Hp, d.H, nullptr, rf, s));
+  TRYP(DCNR_K_REDUCE, reduce_fused(DCNR_PREC_FP32, L.part, nc, NK, d.Hp, d.H, nullptr, rf, s));
   return DCNR_OK;
 }
 
@@ -1327,6 +1327,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   // the BN backward's row passes folded into those GEMMs (bf16, K = Hp in (256, 512])
   const bool xbn_ok = fuse && d.prec == DCNR_PREC_BF16 && gemm_ws_xbn_supported(NT_EPI_DROP_BN, d.Hp, d.Hp);
   int nc_du = 0;   // > 0: L.du and its BN2 partials were made by the previous dX GEMM
+  bool b0_done = false;   // the initial layer's bias gradient came with G (NT_EPI_RESID_SUM)
   for (int j = d.R - 1; j >= 0; --j) {
     const auto& Bk = P.blk[j];
     auto& Gk = Gr.blk[j];
@@ -1405,7 +1406,8 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
                         L.t2[j - 1], bp, B, &nc_du, s, xbn1 ? &xo : nullptr));
       if (xbn1) TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe));
       Gin = L.duk[j - 1];
-    } else if (xbn1) {   // G = dt1 W1 + du, dt1 made from da and t1 in the GEMM
+    } else if (xbn1) {   // G = dt1 W1 + du, dt1 made from da and t1 in the GEMM,
+                         // G's column sums (the initial layer's bias gradient) in its epilogue
       NtArgs a;
       memset(&a, 0, sizeof(a));
       a.Tx = (const bf16*)L.t1[j];
@@ -1415,8 +1417,12 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
       a.W = (const bf16*)L.W1t[j]; a.ldw = Hp; a.N = Hp;
       a.C = L.G; a.ldc = Hp;
       a.R = du; a.ldr = Hp;
-      TRYB(DCNR_K_GEMM_DX, 5 * act_b(d, B) + w_b(d, d.Hp), gemm_ws(NT_EPI_RESID, a, s));
+      a.part = L.part;
+      int ncg = 0;
+      TRYB(DCNR_K_GEMM_DX, 5 * act_b(d, B) + w_b(d, d.Hp), gemm_ws(NT_EPI_RESID_SUM, a, s, &ncg));
       TRY(linear_dw(d, L, dt1, Hp, Hp, L.h[j], Hp, Hp, B, Gk.w1, H, H, accumulate, s, pipe));
+      TRY(bias_reduce(d, L, ncg, Gr.b0, accumulate, s, 2));
+      b0_done = true;
       Gin = L.G;
       nc_du = 0;
     } else {
@@ -1436,7 +1442,7 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
   // the column sums on it too, the optimizer waited 135 us for it while the
   // main stream was done (profiles/r06fin_step_timeline.txt)
   TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s, pipe));
-  {
+  if (!b0_done) {
     int nc = 0;
     TRYB(DCNR_K_ROWWISE, act_b(d, B), col_sum(d.prec, L.G, B, Hp, Hp, L.part, &nc, s));
     TRY(bias_reduce(d, L, nc, Gr.b0, accumulate, s));

@@ -454,6 +454,10 @@ enum NtEpi : int {
   // relu((acc + bias) * sc + sh + R) with wf, one partial per row per wave of
   // each column slice: headp[slice * 8 + wave][m] (summed by head_parts)
   NT_EPI_BN_RESID_RELU_HEAD = 8,
+  // the train backward's G = dt1 W1 + du of block 0: C bf16 = acc + R[m][n];
+  // part = [sum c, sum c^2] (c the stored value; component 0 is the initial
+  // layer's bias gradient, reduced with RED_BIAS)
+  NT_EPI_RESID_SUM = 9,
 };
 // (c is the stored bf16 value; xhat(T) = (T[m][n] - mean[n]) * invstd[n])
 struct NtArgs {
@@ -494,7 +498,9 @@ dcnr_status gemm_wsp(int epi, const NtArgs& a, hipStream_t s, int* nparts);
 dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts = nullptr);
 // head partials of NT_EPI_BN_RESID_RELU_HEAD: rows of headp written (0: unsupported shape)
 int gemm_ws_head_parts(int64_t N);
-inline bool nt_epi_stats(int epi) { return epi >= NT_EPI_BIAS_STATS && epi <= NT_EPI_DROP_BN; }
+inline bool nt_epi_stats(int epi) {
+  return (epi >= NT_EPI_BIAS_STATS && epi <= NT_EPI_DROP_BN) || epi == NT_EPI_RESID_SUM;
+}
 
 // bf16 weight-gradient GEMM (gemm_dw.hip): slab[split][n][k] = sum over the
 // split's batch rows of A[b][n] * B[b][k]; A = dY [Btot][lda], B = X [Btot][ldb]

@@ -49,7 +49,7 @@ template <int KTP, int EPI> constexpr int ws_tm() {
 }
 template <int EPI> constexpr bool ws_ops_early() {
   return EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN || EPI == NT_EPI_BN_RESID_RELU ||
-         EPI == NT_EPI_BN_RESID_RELU_HEAD;
+         EPI == NT_EPI_BN_RESID_RELU_HEAD || EPI == NT_EPI_RESID_SUM;
 }
 // X-tile buffers in the LDS ring: one tile in flight while one is consumed.
 constexpr int WS_NB = 2;
@@ -123,13 +123,14 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
   constexpr int NB = WS_NB;
   using C = WsCfg<KTP, WS_TM, NB>;
   constexpr int WS_RB = C::RB;
-  constexpr bool STATS = EPI >= NT_EPI_BIAS_STATS && EPI <= NT_EPI_DROP_BN;
+  constexpr bool STATS = (EPI >= NT_EPI_BIAS_STATS && EPI <= NT_EPI_DROP_BN) || EPI == NT_EPI_RESID_SUM;
   constexpr bool HEAD = EPI == NT_EPI_BN_RESID_RELU_HEAD;
-  constexpr bool HAS_R = EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_BN_RESID_RELU || HEAD;
+  constexpr bool HAS_R = EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_BN || EPI == NT_EPI_BN_RESID_RELU || HEAD ||
+                         EPI == NT_EPI_RESID_SUM;
   constexpr bool HAS_HT = EPI == NT_EPI_RESID_BN || EPI == NT_EPI_DROP_BN;
-  constexpr bool HAS_BIAS = EPI <= NT_EPI_BIAS_STATS || EPI >= NT_EPI_BN_RELU;
-  constexpr bool HAS_SS = EPI >= NT_EPI_BN_RELU;   // eval BN affine + ReLU
-  static_assert(!XBN || (WS_NT % C::CPR == 0 && (HAS_HT || EPI == NT_EPI_RESID)),
+  constexpr bool HAS_SS = EPI >= NT_EPI_BN_RELU && EPI <= NT_EPI_BN_RESID_RELU_HEAD;   // eval BN affine + ReLU
+  constexpr bool HAS_BIAS = EPI <= NT_EPI_BIAS_STATS || HAS_SS;
+  static_assert(!XBN || (WS_NT % C::CPR == 0 && (HAS_HT || EPI == NT_EPI_RESID || EPI == NT_EPI_RESID_SUM)),
                 "operand transform: dX epilogues, whole rows");
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63, q = lane >> 4, l15 = lane & 15;
@@ -340,10 +341,11 @@ __global__ __launch_bounds__(WS_NT, 1) void gemm_ws_kernel(NtArgs a) {
           // sums of the stored (bf16-rounded) values
           if (mok) {
             const f2v c[2] = {unpack2(o[cb][0]), unpack2(o[cb][1])};
-            if constexpr (EPI == NT_EPI_BIAS_STATS) {
+            if constexpr (EPI == NT_EPI_BIAS_STATS || EPI == NT_EPI_RESID_SUM) {
 #pragma unroll
               for (int d = 0; d < 2; ++d) {
-                const f2v dd = c[d] - bb[d];
+                f2v dd = c[d];
+                if constexpr (HAS_BIAS) dd -= bb[d];
                 st[0][cb][d] += dd;
                 st[1][cb][d] += dd * dd;
               }
@@ -592,7 +594,8 @@ dcnr_status dispatch_ws(const NtArgs& a, hipStream_t s, int* nparts) {
 
 bool gemm_ws_supported(int64_t K, int64_t N) { return K <= 512 && K % 8 == 0 && N % 8 == 0; }
 bool gemm_ws_xbn_supported(int epi, int64_t K, int64_t N) {
-  return (epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN || epi == NT_EPI_RESID) && K > 256 && K <= 512 &&
+  return (epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN || epi == NT_EPI_RESID || epi == NT_EPI_RESID_SUM) &&
+         K > 256 && K <= 512 &&
          K % 8 == 0 && N % 8 == 0;
 }
 int gemm_ws_head_parts(int64_t N) { return N % 8 == 0 && N <= 4096 ? (int)cdiv(N, WS_TN) * WS_WAVES : 0; }
@@ -602,9 +605,10 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
   if (a.M <= 0 || a.N <= 0) return DCNR_OK;
   const bool ht = epi == NT_EPI_RESID_BN || epi == NT_EPI_DROP_BN;
   if (!gemm_ws_supported(a.K, a.N) || a.ldx % 8 || a.ldw % 8 || a.ldc % 8 ||
-      ((epi == NT_EPI_RESID || epi == NT_EPI_RESID_BN || epi == NT_EPI_BN_RESID_RELU) && (a.ldr % 8 || !a.R)) ||
-      (epi >= NT_EPI_BN_RELU && !a.bn_rm && (!a.bn_scale || !a.bn_shift)) ||
-      (epi >= NT_EPI_BN_RELU && a.bn_rm && (!a.bn_g || !a.bn_b || !a.bn_rv)) ||
+      ((epi == NT_EPI_RESID || epi == NT_EPI_RESID_BN || epi == NT_EPI_BN_RESID_RELU || epi == NT_EPI_RESID_SUM) &&
+       (a.ldr % 8 || !a.R)) ||
+      (epi >= NT_EPI_BN_RELU && epi <= NT_EPI_BN_RESID_RELU_HEAD && !a.bn_rm && (!a.bn_scale || !a.bn_shift)) ||
+      (epi >= NT_EPI_BN_RELU && epi <= NT_EPI_BN_RESID_RELU_HEAD && a.bn_rm && (!a.bn_g || !a.bn_b || !a.bn_rv)) ||
       (epi == NT_EPI_BN_RESID_RELU_HEAD &&
        (!a.wf || !a.headp || !gemm_ws_head_parts(a.N) || a.ldh < a.M ||
         a.ldh * gemm_ws_head_parts(a.N) * 4 >= (int64_t(1) << 31))) ||
@@ -618,6 +622,7 @@ dcnr_status gemm_ws(int epi, const NtArgs& a, hipStream_t s, int* nparts) {
       set_error("gemm_ws: unsupported operand transform (epi %d K=%d N=%d)", epi, a.K, a.N);
       return DCNR_UNSUPPORTED_SHAPE;
     }
+    if (epi == NT_EPI_RESID_SUM) return launch_ws<16, NT_EPI_RESID_SUM, true>(a, s, nparts);
     if (epi == NT_EPI_RESID) return launch_ws<16, NT_EPI_RESID, true>(a, s, nparts);
     return epi == NT_EPI_RESID_BN ? launch_ws<16, NT_EPI_RESID_BN, true>(a, s, nparts)
                                   : launch_ws<16, NT_EPI_DROP_BN, true>(a, s, nparts);

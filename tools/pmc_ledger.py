@@ -22,7 +22,7 @@ from collections import OrderedDict
 CLASSES = [
     ("gather_cross", r"gather_lowrank_kernel|gather_cross_v4_kernel|gather_cross_fwd"),
     ("gemm_fwd", r"gemm_wsp_kernel|gemm_ws_kernel<16, [03](, (\d|true|false))?>"),
-    ("gemm_dx", r"gemm_ws_kernel<16, [1245](, (\d|true|false))?>"),
+    ("gemm_dx", r"gemm_ws_kernel<16, [12459](, (\d|true|false))?>"),
     ("gemm_dw", r"gemm_dw_kernel"),
     ("rowwise", r"rowcol_kernel"),
     ("reduce", r"reduce_small_kernel|reduce_fused_kernel|splitk_reduce_t_kernel|bce_final"),

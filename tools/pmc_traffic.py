@@ -20,7 +20,7 @@ CLASSES = [
     # (template args <KTP, EPI, HB>: HB = 1-bit keep masks)
     ("gemm_fwd", r"gemm_wsp_kernel|gemm_ws_kernel<16, [03](, (\d|true|false))?>"),
     ("gemm_dx_bn", r"gemm_ws_kernel<16, [45](, (\d|true|false))?>"),
-    ("gemm_resid", r"gemm_ws_kernel<16, 2(, (\d|true|false))?>"),
+    ("gemm_resid", r"gemm_ws_kernel<16, [29](, (\d|true|false))?>"),
     ("gemm_f32", r"gemm_ws_kernel<16, 1(, (\d|true|false))?>"),
     ("gemm_eval_bn", r"gemm_ws_kernel<16, [67](, (\d|true|false))?>"),
     ("gemm_dw", r"gemm_dw_kernel"),
