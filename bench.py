@@ -732,7 +732,7 @@ def main():
                 "achieved": dt["achieved_gbs"], "peak": PEAK_HBM / 1e9, "unit": "GB/s",
                 "frac": dt["frac"], "traffic": pmc_traffic(dom),
                 "traffic_source": "profiles/pmc_traffic.json (rocprofv3 --pmc passes of the "
-                                  "committed profile set r06fin, not measured in this run)",
+                                  "committed profile set r06fin2, not measured in this run)",
                 "bytes_per_launch": dt["bytes_per_launch"], "avg_launch_ms": dt["avg_launch_ms"]}
         roof["frac_of_measured_copy"] = dt["achieved_gbs"] / peaks["copy_gbs"]
         if prof_dw and prof_dw.get("gemm_dw", (0, 0, 0))[1] and dom == "gemm_dw":
