@@ -1437,10 +1437,11 @@ dcnr_status dcnr_backward(const dcnr_model_desc* desc, void* const* params, void
     }
   }
   // ---- initial layer: the weight gradient on the side stream (after block
-  // 0's), the bias gradient (column sums of G) here on the main stream, ahead
-  // of the dx0 GEMM.  The side stream's queue sets the backward's tail: with
-  // the column sums on it too, the optimizer waited 135 us for it while the
-  // main stream was done (profiles/r06fin_step_timeline.txt)
+  // 0's); the bias gradient came with G (b0_done) or is a column-sum pass
+  // here on the main stream, ahead of the dx0 GEMM.  The side stream's queue
+  // sets the backward's tail: with the column sums on it, the optimizer
+  // waited 135 us for it while the main stream was done
+  // (profiles/r06fin_step_timeline.txt)
   TRY(linear_dw(d, L, L.G, Hp, Hp, L.x0, d.Dp, d.Dp, B, Gr.W0, H, d.D, accumulate, s, pipe));
   if (!b0_done) {
     int nc = 0;
